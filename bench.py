@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""North-star benchmark: Conformer-Large (17 layers, d512, 8 heads) encoder forward,
+B=32 x T=1000 x 80-mel per GPU, eval mode, through the drop-in
+`nemo.collections.asr.modules.ConformerEncoder` (one C-ABI call per forward).
+
+    python bench.py [--gpus N --steps K --warmup W] [--compute bf16|fp32]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Multi-GPU: utterances shard across ranks with no data-path collective (weak scaling, per-GPU
+B=32); the time is the MAX over ranks between barrier+synchronize brackets.  Rank 0 prints ONE
+JSON line.  See DESIGN.md §Measurement for every field.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
+
+import torch  # noqa: E402
+
+METRIC = "encoder audio-frames/sec, Conformer-Large B=32 T=1000 @1/2/4/8 MI355X"
+PEAK = {"bf16": 2500.0, "fp32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def stage_work(B, T, d, L, H, C=None, F=80, K=31, dff=None, es=2):
+    """Algorithmic work per launch of every stage: (kind, amount) with kind 'flop' or 'byte'."""
+    C = C or d
+    dff = dff or 4 * d
+    T1 = (T - 1) // 2 + 1
+    Tp = (T1 - 1) // 2 + 1
+    F1 = (F - 1) // 2 + 1
+    F2 = (F1 - 1) // 2 + 1
+    M = B * Tp
+    return {
+        "conv1": ("byte", B * F * T * 4 + B * T1 * F1 * C * es),
+        "conv2_gemm": ("flop", 2 * B * Tp * F2 * C * C * 9),
+        "subsample_linear": ("flop", 2 * M * C * F2 * d),
+        "pos_gemm": ("flop", 2 * (2 * Tp - 1) * d * L * d),
+        "layernorm": ("byte", M * d * (4 + es)),
+        "ffn_up_gemm": ("flop", 2 * M * d * dff),
+        "ffn_down_gemm": ("flop", 2 * M * dff * d),
+        "qkv_gemm": ("flop", 2 * M * d * 3 * d),
+        "rel_attention": ("flop", 2 * B * Tp * d * (4 * Tp - 1)),
+        "out_proj_gemm": ("flop", 2 * M * d * d),
+        "pw1_glu_gemm": ("flop", 2 * M * d * 2 * d),
+        "dwconv_bn_swish": ("byte", 2 * M * d * es),
+        "pw2_gemm": ("flop", 2 * M * d * d),
+        "output": ("byte", 2 * M * d * 4),
+    }
+
+
+def cpu_baseline(enc, B, T, budget_s):
+    """Oracle (numpy restatement of the reference) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import conformer_oracle as O  # CPU baseline leg only
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    sd = {k: v.detach().float().cpu().numpy() for k, v in enc.state_dict().items() if v.is_floating_point()}
+    cfg = dict(d_model=512, n_heads=8, n_layers=17)
+    g = np.random.default_rng(0)
+    x = g.standard_normal((1, 80, T), dtype=np.float32)
+    frames, t0, runs = 0, time.perf_counter(), 0
+    while True:
+        O.encoder_forward(x, np.array([T]), sd, cfg)
+        frames += T
+        runs += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(frames / dt, 1), "unit": "audio-frames/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle/conformer_oracle.py numpy fp32, Large-17, {runs} x (B=1, T={T}) utterances, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--compute", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=1000)
+    ap.add_argument("--layers", type=int, default=17)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
+    ap.add_argument("--no-breakdown", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    from nemo.collections.asr.modules import ConformerEncoder
+    torch.manual_seed(0)
+    d, H, L, B, T = 512, 8, args.layers, args.batch, args.seq
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
+    enc.set_compute_mode(args.compute)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, 80, T, device=dev, generator=g)          # synthetic 80-mel, resident in HBM
+    lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
+
+    with torch.inference_mode():
+        for _ in range(args.warmup):
+            y, yl = enc(audio_signal=x, length=lengths)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y, yl = enc(audio_signal=x, length=lengths)
+        barrier()
+        elapsed = time.perf_counter() - t0
+    assert torch.isfinite(y).all().item()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    t_max = float(t.item())
+    frames = world * B * T * args.steps
+    value = frames / t_max
+    ms_step = 1000.0 * t_max / args.steps
+
+    if rank == 0:
+        import conformer_amd
+        es = 2 if args.compute == "bf16" else 4
+        total_flop = None
+        roof = None
+        breakdown = {}
+        if not args.no_breakdown:
+            native = enc._native_for(dev)
+            agg = {}
+            reps = 3
+            with torch.inference_mode():
+                for _ in range(reps):
+                    for k, (ms, n) in native.forward_timed(x, lengths.to(torch.int32)).items():
+                        a = agg.setdefault(k, [0.0, 0])
+                        a[0] += ms / reps
+                        a[1] = n
+            work = stage_work(B, T, d, L, H, es=es)
+            for k, (ms, n) in agg.items():
+                if n == 0:
+                    continue
+                kind, amt = work.get(k, ("byte", 0))
+                per = ms / n
+                rate = amt / (per * 1e-3) / (1e12 if kind == "flop" else 1e9)
+                breakdown[k] = {"ms_total": round(ms, 4), "launches": n, "ms_per_launch": round(per, 5),
+                                ("TFLOP/s" if kind == "flop" else "GB/s"): round(rate, 1)}
+            dom = max((k for k in agg if agg[k][1]), key=lambda k: agg[k][0])
+            kind, amt = work[dom]
+            per_ms = agg[dom][0] / agg[dom][1]
+            if kind == "flop":
+                ach = amt / (per_ms * 1e-3) / 1e12
+                roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK[args.compute],
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": None,
+                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (HIP events, {agg[dom][1]} launches)"}
+            else:
+                ach = amt / (per_ms * 1e-3) / 1e9
+                roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "per_launch": f"{amt / 1e6:.2f} MB in {per_ms:.4f} ms"}
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from conformer_oracle import encoder_flops
+        total_flop = encoder_flops(B, T, d, L)
+        cpu = cpu_baseline(enc, B, T, args.cpu_budget) if args.cpu_budget > 0 else None
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
+            "config": {"workload": f"Conformer-CTC-Large encoder forward (d_model 512, 8 heads, {L} layers, eval), "
+                                   f"B={B}/GPU, T={T} 80-mel frames, random-init weights",
+                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (replicas, no collective)"},
+            "roofline": roof,
+            "model_flops": {"GFLOP_per_step_per_gpu": round(total_flop / 1e9, 1),
+                            "TFLOP/s_per_gpu": round(total_flop / (ms_step * 1e-3) / 1e12, 1),
+                            "frac_of_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+            "cpu_baseline": cpu,
+            "breakdown": breakdown,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,94 @@
+"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h).
+
+The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
+There is deliberately no fallback: if the shared object is missing or fails to load, importing
+the native path raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcfm.so")
+
+CFM_COMPUTE_FP32 = 0
+CFM_COMPUTE_BF16 = 1
+
+STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "UNSUPPORTED", 3: "HIP", 4: "WORKSPACE", 5: "WEIGHTS", 6: "NOMEM"}
+
+# every symbol include/cfm_encoder.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "cfm_last_error", "cfm_version", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
+    "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
+    "cfm_encoder_set_max_audio_length", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
+    "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
+    "cfm_op_rel_attention",
+)
+
+
+class CfmEncoderCfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "feat_in", "n_layers", "d_model", "feat_out", "subsampling_factor", "subsampling_conv_channels",
+        "ff_expansion_factor", "n_heads", "att_context_left", "att_context_right", "xscaling", "pos_emb_max_len",
+        "conv_kernel_size", "conv_norm_type")]
+
+
+class CfmTensorView(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64),
+                ("on_device", ctypes.c_int)]
+
+
+class CfmError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libcfm.so once.  torch must be imported first so the process shares torch's HIP runtime."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (HIP runtime first: libcfm resolves libamdhip64.so.7 to torch's copy)
+    if not os.path.exists(LIB_PATH):
+        raise CfmError(f"native library not built: {LIB_PATH} (run `make -C conformer-nemo_amd/csrc` "
+                       f"or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    sig = {
+        "cfm_last_error": (ctypes.c_char_p, []),
+        "cfm_version": (ci, []),
+        "cfm_encoded_length": (ci, [ci]),
+        "cfm_encoder_create": (ci, [ctypes.POINTER(CfmEncoderCfg), ci, ci, ctypes.POINTER(vp)]),
+        "cfm_encoder_destroy": (None, [vp]),
+        "cfm_encoder_set_weights": (ci, [vp, ctypes.POINTER(CfmTensorView), ci, vp]),
+        "cfm_encoder_param_count": (ci, [vp]),
+        "cfm_encoder_param_name": (ctypes.c_char_p, [vp, ci]),
+        "cfm_encoder_param_numel": (ctypes.c_int64, [vp, ci]),
+        "cfm_encoder_set_max_audio_length": (ci, [vp, ci]),
+        "cfm_encoder_max_audio_length": (ci, [vp]),
+        "cfm_encoder_workspace_size": (sz, [vp, ci, ci]),
+        "cfm_encoder_forward": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp]),
+        "cfm_num_stages": (ci, []),
+        "cfm_stage_name": (ctypes.c_char_p, [ci]),
+        "cfm_encoder_forward_timed": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(ci)]),
+        "cfm_op_layernorm": (ci, [ci, vp, ci, ci, vp, vp, vp, vp, vp]),
+        "cfm_op_linear": (ci, [ci, vp, ci, ci, vp, vp, ci, ci, vp, vp, ctypes.POINTER(sz), vp]),
+        "cfm_op_rel_attention_ws_size": (sz, [ci, ci, ci, ci, ci]),
+        "cfm_op_rel_attention": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = load().cfm_last_error().decode(errors="replace")
+        raise CfmError(f"{what}: {STATUS_NAMES.get(status, status)}: {msg}")

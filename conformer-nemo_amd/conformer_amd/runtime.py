@@ -1,0 +1,170 @@
+"""Host runtime around the C-ABI encoder handle (include/cfm_encoder.h).
+
+`NativeEncoder` owns one `cfm_encoder*` (packed weights + positional table on one GPU) and a
+grow-only device workspace, and runs `cfm_encoder_forward` on torch's current HIP stream.
+Tensors are passed as raw device pointers; torch is used only for device memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Iterable, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+COMPUTE_MODES = {"fp32": _lib.CFM_COMPUTE_FP32, "bf16": _lib.CFM_COMPUTE_BF16}
+
+
+def encoded_length(T: int) -> int:
+    """calc_length (subsampling.py:272-282) via the library (host side)."""
+    return _lib.load().cfm_encoded_length(int(T))
+
+
+def make_cfg(feat_in: int, n_layers: int, d_model: int, feat_out: int = -1, subsampling_factor: int = 4,
+             subsampling_conv_channels: int = -1, ff_expansion_factor: int = 4, n_heads: int = 4,
+             att_context_size=None, xscaling: bool = True, pos_emb_max_len: int = 5000,
+             conv_kernel_size: int = 31, conv_norm_type: str = "batch_norm") -> _lib.CfmEncoderCfg:
+    ctx = list(att_context_size) if att_context_size else [-1, -1]
+    c = _lib.CfmEncoderCfg()
+    c.feat_in, c.n_layers, c.d_model, c.feat_out = int(feat_in), int(n_layers), int(d_model), int(feat_out)
+    c.subsampling_factor = int(subsampling_factor)
+    c.subsampling_conv_channels = int(subsampling_conv_channels)
+    c.ff_expansion_factor = int(ff_expansion_factor)
+    c.n_heads = int(n_heads)
+    c.att_context_left, c.att_context_right = int(ctx[0]), int(ctx[1])
+    c.xscaling = 1 if xscaling else 0
+    c.pos_emb_max_len = int(pos_emb_max_len)
+    c.conv_kernel_size = int(conv_kernel_size)
+    if conv_norm_type not in ("batch_norm", "layer_norm"):
+        raise ValueError(f"conv_norm_type={conv_norm_type} is not valid!")
+    c.conv_norm_type = 0 if conv_norm_type == "batch_norm" else 1
+    return c
+
+
+class NativeEncoder:
+    """One encoder instance on one GPU."""
+
+    def __init__(self, cfg: _lib.CfmEncoderCfg, device: Optional[int] = None, compute: str = "bf16"):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.CfmError("the native Conformer encoder needs a ROCm GPU (torch.cuda.is_available() is False)")
+        if compute not in COMPUTE_MODES:
+            raise ValueError(f"compute must be one of {list(COMPUTE_MODES)}")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.compute = compute
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.cfm_encoder_create(ctypes.byref(cfg), self.device, COMPUTE_MODES[compute], ctypes.byref(h)),
+                   "cfm_encoder_create")
+        self.handle = h
+        self._ws: Optional[torch.Tensor] = None
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.cfm_encoder_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    # ---- weights ------------------------------------------------------------------------------
+    def param_names(self) -> Dict[str, int]:
+        n = self.lib.cfm_encoder_param_count(self.handle)
+        return {self.lib.cfm_encoder_param_name(self.handle, i).decode(): int(self.lib.cfm_encoder_param_numel(self.handle, i))
+                for i in range(n)}
+
+    def set_weights(self, tensors: Dict[str, torch.Tensor]) -> None:
+        """Pack every tensor of the reference state_dict (fp32 copies are made as needed)."""
+        keep, views = [], []
+        for name, t in tensors.items():
+            if not torch.is_floating_point(t):
+                continue
+            t = t.detach()
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                t = t.float().contiguous()
+            keep.append(t)
+            v = _lib.CfmTensorView()
+            v.name = name.encode()
+            v.data = t.data_ptr()
+            v.numel = t.numel()
+            v.on_device = 1 if t.is_cuda else 0
+            views.append(v)
+        arr = (_lib.CfmTensorView * len(views))(*views)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self.lib.cfm_encoder_set_weights(self.handle, arr, len(views), ctypes.c_void_p(stream)),
+                   "cfm_encoder_set_weights")
+        del keep
+
+    # ---- forward ------------------------------------------------------------------------------
+    @property
+    def max_audio_length(self) -> int:
+        return int(self.lib.cfm_encoder_max_audio_length(self.handle))
+
+    def set_max_audio_length(self, n: int) -> None:
+        _lib.check(self.lib.cfm_encoder_set_max_audio_length(self.handle, int(n)), "set_max_audio_length")
+
+    def workspace_size(self, B: int, T: int) -> int:
+        return int(self.lib.cfm_encoder_workspace_size(self.handle, int(B), int(T)))
+
+    def _workspace(self, nbytes: int) -> torch.Tensor:
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = None
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{self.device}")
+        return self._ws
+
+    def forward(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, out_len: Optional[torch.Tensor] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+        if not x_bft.is_cuda or x_bft.dim() != 3:
+            raise ValueError("audio_signal must be a (B, feat_in, T) tensor on the GPU")
+        if x_bft.dtype != torch.float32 or not x_bft.is_contiguous():
+            x_bft = x_bft.float().contiguous()
+        B, F, T = x_bft.shape
+        if F != self.cfg.feat_in:
+            raise ValueError(f"expected feat_in={self.cfg.feat_in}, got {F}")
+        if T > self.max_audio_length:      # set_max_audio_length (conformer_encoder.py:240-241)
+            torch.cuda.synchronize(self.device)
+            self.set_max_audio_length(T)
+        Tp = encoded_length(T)
+        dout = self.cfg.feat_out if (self.cfg.feat_out > 0 and self.cfg.feat_out != self.cfg.d_model) else self.cfg.d_model
+        dev = x_bft.device
+        if out is None:
+            out = torch.empty((B, dout, Tp), dtype=torch.float32, device=dev)
+        if out_len is None:
+            out_len = torch.empty((B,), dtype=torch.int32, device=dev)
+        len_ptr = None
+        if lengths is not None:
+            lengths = lengths.to(device=dev, dtype=torch.int32).contiguous()
+            len_ptr = lengths.data_ptr()
+        nbytes = self.workspace_size(B, T)
+        ws = self._workspace(nbytes)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(self.lib.cfm_encoder_forward(self.handle, x_bft.data_ptr(), len_ptr, B, T, out.data_ptr(),
+                                                out_len.data_ptr(), ws.data_ptr(), nbytes, ctypes.c_void_p(stream)),
+                   "cfm_encoder_forward")
+        return out, out_len
+
+    def forward_timed(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None):
+        """One forward with a HIP event at every kernel-group boundary; returns
+        {stage: (device ms, launches)} (cfm_encoder_forward_timed)."""
+        B, F, T = x_bft.shape
+        Tp = encoded_length(T)
+        dout = self.cfg.feat_out if (self.cfg.feat_out > 0 and self.cfg.feat_out != self.cfg.d_model) else self.cfg.d_model
+        out = torch.empty((B, dout, Tp), dtype=torch.float32, device=x_bft.device)
+        out_len = torch.empty((B,), dtype=torch.int32, device=x_bft.device)
+        len_ptr = None
+        if lengths is not None:
+            lengths = lengths.to(device=x_bft.device, dtype=torch.int32).contiguous()
+            len_ptr = lengths.data_ptr()
+        n = self.lib.cfm_num_stages()
+        ms = (ctypes.c_float * n)()
+        cnt = (ctypes.c_int * n)()
+        nbytes = self.workspace_size(B, T)
+        ws = self._workspace(nbytes)
+        stream = torch.cuda.current_stream(x_bft.device).cuda_stream
+        _lib.check(self.lib.cfm_encoder_forward_timed(self.handle, x_bft.data_ptr(), len_ptr, B, T, out.data_ptr(),
+                                                      out_len.data_ptr(), ws.data_ptr(), nbytes, ctypes.c_void_p(stream),
+                                                      ms, cnt), "cfm_encoder_forward_timed")
+        return {self.lib.cfm_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(n)}

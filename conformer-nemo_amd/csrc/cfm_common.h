@@ -1,0 +1,95 @@
+// Shared device helpers for the gfx950 (CDNA4) Conformer encoder kernels.
+//
+// Compute-type abstraction used by every MFMA kernel in this library
+// ------------------------------------------------------------------
+// All MFMA operands are staged as 32-byte "k-slabs" per matrix row: lane l of a wave supplies
+// row (l & 31) and the 16 bytes at offset 16*(l >> 5) of the slab.
+//   * bf16 : 16 bytes = 8 bf16 = exactly the A/B fragment of v_mfma_f32_32x32x16_bf16
+//            (lane holds A[row l&31][k = 8*(l>>5) + j]).
+//   * fp32 : 16 bytes = 4 floats, consumed by 4 x v_mfma_f32_32x32x2_f32, MFMA e taking element e
+//            (lane half h then contributes logical k = 4h + e; A and B agree, so the sum is the
+//            same dot product in a different order).
+// Loaders, LDS images and swizzles are therefore byte-identical for both compute types; only the
+// per-slab MFMA micro-step differs (`mfma_slab`).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CFM_DEV __device__ __forceinline__
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+
+CFM_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+CFM_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN-preserving)
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+// Scalar load / store in the compute type, math in fp32.
+template <typename T> CFM_DEV float ld_f(const T* p);
+template <> CFM_DEV float ld_f<float>(const float* p) { return *p; }
+template <> CFM_DEV float ld_f<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> CFM_DEV void st_f(T* p, float v);
+template <> CFM_DEV void st_f<float>(float* p, float v) { *p = v; }
+template <> CFM_DEV void st_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// One 32-byte k-slab of a 32x32 output tile: acc += A_slab * B_slab.
+template <typename T> CFM_DEV void mfma_slab(f32x16& acc, const uint4& a, const uint4& b);
+template <> CFM_DEV void mfma_slab<bf16_t>(f32x16& acc, const uint4& a, const uint4& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                acc, 0, 0, 0);
+}
+template <> CFM_DEV void mfma_slab<float>(f32x16& acc, const uint4& a, const uint4& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+}
+
+// C/D layout of a 32x32 MFMA accumulator: element r of lane l sits at
+//   row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5),  col = l & 31.
+CFM_DEV int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// 16 bytes of compute-type values -> / <- fp32.
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  static CFM_DEV void to_f32(const uint4& u, float* f) {
+    f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y); f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+  }
+  static CFM_DEV uint4 from_f32(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  static CFM_DEV void to_f32(const uint4& u, float* f) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  }
+  static CFM_DEV uint4 from_f32(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+CFM_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+CFM_DEV float swishf(float x) { return x / (1.0f + __expf(-x)); }
+CFM_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// Asynchronous 16-byte global -> LDS copy (global_load_lds_dwordx4). The LDS destination is the
+// wave-uniform `lds_base` + 16 * lane; the global source is per lane.
+CFM_DEV void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}

@@ -1,0 +1,67 @@
+// Internal launcher interface between the encoder orchestration (encoder.hip) and the kernels.
+// Not part of the public C-ABI (that is include/cfm_encoder.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfm {
+
+enum Dtype { DT_F32 = 0, DT_BF16 = 1 };
+inline int dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+
+// GEMM tile geometry shared with the weight packer: packed weights are [Npad][Kpad] in the
+// compute type, Npad a multiple of GEMM_BN, Kpad a multiple of GEMM_BK_BYTES / elem_size.
+constexpr int GEMM_BM = 128;
+constexpr int GEMM_BN = 128;
+constexpr int GEMM_BK_BYTES = 128;
+
+enum Epilogue {
+  EPI_STORE = 0,       // C[m,n] = acc + bias[n]                        (compute type)
+  EPI_RELU = 1,        // C = relu(acc + bias)
+  EPI_SWISH = 2,       // C = swish(acc + bias)
+  EPI_RESID = 3,       // X[m,n] (fp32) += alpha * (acc + bias)
+  EPI_SCALE_F32 = 4,   // X[m,n] (fp32)  = (acc + bias) * alpha
+  EPI_GLU_MASK = 5,    // C[m, c] = (a + ba) * sigmoid(g + bg), zero for padded frames (GLU-packed W)
+  EPI_QKV = 6,         // q,k parts -> C (ldc), v part -> Vt[(b*H + h)][d][t] transposed
+};
+
+struct GemmEpi {
+  int mode;
+  const float* bias;   // [Npad] fp32 (may be null)
+  float alpha;
+  void* C; long ldc;   // elements
+  float* X; long ldx;  // fp32 residual / output
+  const int32_t* lens; int Tp;          // pad mask (EPI_GLU_MASK) and row -> (b, t) for EPI_QKV
+  void* Vt; int H; int dkp; int vt_rows; int Tpad;  // EPI_QKV: Vt [(B*H) * vt_rows][Tpad]
+  int qk_cols;         // EPI_QKV: columns < qk_cols go to C, the rest are V
+};
+
+struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)
+  const void* X1;      // (B, T1, F1, C) channels-last, compute type
+  int T1, F1, T2, F2, C;
+};
+
+// C = A[M,K] * Wp[N,K]^T with a fused epilogue. `K` = logical K (elements); A rows are `lda` elements.
+void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int Kpad, int N,
+          const GemmEpi& epi, const void* zero_page, hipStream_t st);
+void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
+               const void* zero_page, hipStream_t st);
+
+void calc_length(const int32_t* len_in, int32_t* len_out, int B, int T, int repeat, hipStream_t st);
+void conv1_subsample(int dtype, const float* x_bft, int B, int F, int T, const float* w9, const float* bias, int C,
+                     void* out, hipStream_t st);
+// LayerNorm over rows of d fp32 values.  out_x (fp32, may alias x) and/or out_t (compute type).
+// If w2/b2 are given, a second LayerNorm is applied to the first's result and written to out_t
+// (the fused "norm_out of layer l + norm_feed_forward1 of layer l+1").
+void layernorm(int dtype, const float* x, int rows, int d, const float* w, const float* b, float* out_x,
+               const float* w2, const float* b2, void* out_t, int swish_out, hipStream_t st);
+void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, const float* w, const float* bias,
+                       const float* bn_mean, const float* bn_inv, const float* bn_w, const float* bn_b,
+                       void* out_t, float* out_prenorm_f32, hipStream_t st);
+void transpose_out(const float* X, int B, int Tp, int d, float* y_bdt, hipStream_t st);
+void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
+                       long ldp, const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
+                       int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
+void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
+
+}  // namespace cfm

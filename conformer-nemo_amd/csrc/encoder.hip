@@ -1,0 +1,827 @@
+// C-ABI implementation: encoder handle, weight packing, workspace layout and the stream-ordered
+// forward (ConformerEncoder.forward_for_export, conformer_encoder.py:236-281) built from the
+// kernels in gemm.hip / attention.hip / misc.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/cfm_encoder.h"
+#include "cfm_kernels.h"
+
+using namespace cfm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct CfmError {
+  cfm_status code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(cfm_status code, const std::string& msg) { throw CfmError{code, msg}; }
+
+#define HIP_OK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) fail(CFM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <class F>
+cfm_status guarded(F&& f) {
+  try {
+    f();
+    return CFM_OK;
+  } catch (const CfmError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return CFM_ERR_INVALID_ARG;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return CFM_ERR_INVALID_ARG;
+  }
+}
+
+inline long round_up(long v, long m) { return (v + m - 1) / m * m; }
+inline uint16_t host_f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// calc_length (subsampling.py:272-282) in float32 on the host.
+int host_calc_length(int len, int repeat) {
+  float L = (float)len;
+  for (int i = 0; i < repeat; ++i) L = std::floor((L + (2.0f * 1 - 3.0f)) / 2.0f + 1.0f);
+  return (int)L;
+}
+
+struct LayerW {
+  long ff1_w1, ff1_b1, ff1_w2, ff1_b2, ff2_w1, ff2_b1, ff2_w2, ff2_b2;
+  long qkv_w, qkv_b, out_w, out_b, pos_u, pos_v;
+  long pw1_w, pw1_b, dw_w, dw_b, bn_mean, bn_inv, bn_w, bn_b, pw2_w, pw2_b;
+  long ln_w[5], ln_b[5];   // ff1, self_att, conv, ff2, out
+};
+
+}  // namespace
+
+struct cfm_encoder {
+  cfm_encoder_cfg cfg;
+  int device, dtype, es;
+  int d, H, dk, dkp, dff, C, F, F1, F2, K, L, dout, vt_rows;
+  int bke;                   // K padding granule in elements (GEMM_BK_BYTES / es)
+  bool has_out_proj;
+  // packed weights (one device allocation)
+  char* wbuf = nullptr;
+  size_t wbytes = 0;
+  bool weights_set = false;
+  long conv1_w, conv1_b, conv2_w, conv2_b, sub_w, sub_b, pos_w, outp_w, outp_b;
+  std::vector<LayerW> layers;
+  // relative positional table (compute type), rows = 2*max_len - 1
+  char* pe = nullptr;
+  int max_len = 0;
+  void* zero_page = nullptr;
+  std::vector<std::pair<std::string, int64_t>> params;
+
+  template <typename P = char>
+  P* w(long off) const { return (P*)(wbuf + off); }
+  long kpad(int k) const { return round_up(k, bke); }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// parameter table (reference state_dict keys)
+// ---------------------------------------------------------------------------------------------
+void build_param_list(cfm_encoder* h) {
+  auto& P = h->params;
+  P.clear();
+  const int d = h->d, C = h->C, dff = h->dff, K = h->K, H = h->H;
+  P.push_back({"pre_encode.conv.0.weight", (int64_t)C * 9});
+  P.push_back({"pre_encode.conv.0.bias", C});
+  P.push_back({"pre_encode.conv.2.weight", (int64_t)C * C * 9});
+  P.push_back({"pre_encode.conv.2.bias", C});
+  P.push_back({"pre_encode.out.weight", (int64_t)d * C * h->F2});
+  P.push_back({"pre_encode.out.bias", d});
+  for (int l = 0; l < h->L; ++l) {
+    const std::string p = "layers." + std::to_string(l) + ".";
+    auto ln = [&](const char* n) { P.push_back({p + n + ".weight", d}); P.push_back({p + n + ".bias", d}); };
+    auto ff = [&](const char* n) {
+      P.push_back({p + n + ".linear1.weight", (int64_t)dff * d}); P.push_back({p + n + ".linear1.bias", dff});
+      P.push_back({p + n + ".linear2.weight", (int64_t)d * dff}); P.push_back({p + n + ".linear2.bias", d});
+    };
+    ln("norm_feed_forward1"); ff("feed_forward1"); ln("norm_conv");
+    P.push_back({p + "conv.pointwise_conv1.weight", (int64_t)2 * d * d});
+    P.push_back({p + "conv.pointwise_conv1.bias", 2 * d});
+    P.push_back({p + "conv.depthwise_conv.weight", (int64_t)d * K});
+    P.push_back({p + "conv.depthwise_conv.bias", d});
+    P.push_back({p + "conv.batch_norm.weight", d});
+    P.push_back({p + "conv.batch_norm.bias", d});
+    if (h->cfg.conv_norm_type == 0) {
+      P.push_back({p + "conv.batch_norm.running_mean", d});
+      P.push_back({p + "conv.batch_norm.running_var", d});
+    }
+    P.push_back({p + "conv.pointwise_conv2.weight", (int64_t)d * d});
+    P.push_back({p + "conv.pointwise_conv2.bias", d});
+    ln("norm_self_att");
+    for (const char* n : {"linear_q", "linear_k", "linear_v", "linear_out"}) {
+      P.push_back({p + "self_attn." + n + ".weight", (int64_t)d * d});
+      P.push_back({p + "self_attn." + n + ".bias", d});
+    }
+    P.push_back({p + "self_attn.linear_pos.weight", (int64_t)d * d});
+    P.push_back({p + "self_attn.pos_bias_u", (int64_t)H * h->dk});
+    P.push_back({p + "self_attn.pos_bias_v", (int64_t)H * h->dk});
+    ln("norm_feed_forward2"); ff("feed_forward2"); ln("norm_out");
+  }
+  if (h->has_out_proj) {
+    P.push_back({"out_proj.weight", (int64_t)h->dout * d});
+    P.push_back({"out_proj.bias", h->dout});
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight packing (host side, once per set_weights)
+// ---------------------------------------------------------------------------------------------
+struct Packer {
+  cfm_encoder* h;
+  std::vector<char> buf;
+  bool dry = true;
+  long off = 0;
+
+  long alloc(long bytes) {
+    const long o = round_up(off, 256);
+    off = o + bytes;
+    if (!dry && (long)buf.size() < off) fail(CFM_ERR_WEIGHTS, "packer overflow");
+    return o;
+  }
+  long f32(const float* src, long n, std::function<float(long)> fn = nullptr) {
+    const long o = alloc(n * 4);
+    if (!dry) {
+      float* dst = (float*)(buf.data() + o);
+      for (long i = 0; i < n; ++i) dst[i] = fn ? fn(i) : src[i];
+    }
+    return o;
+  }
+  // packed [Npad][Kpad] compute-type matrix; val(n, k) for n < N, k < K (others zero)
+  long mat(int N, int K, std::function<float(int, int)> val) {
+    const long Npad = round_up(N, GEMM_BN), Kp = h->kpad(K);
+    const long o = alloc(Npad * Kp * h->es);
+    if (!dry) {
+      char* base = buf.data() + o;
+      std::memset(base, 0, Npad * Kp * h->es);
+      for (int n = 0; n < N; ++n)
+        for (int k = 0; k < K; ++k) {
+          const float v = val(n, k);
+          if (v == 0.0f) continue;
+          if (h->es == 4) ((float*)base)[(long)n * Kp + k] = v;
+          else ((uint16_t*)base)[(long)n * Kp + k] = host_f2bf(v);
+        }
+    }
+    return o;
+  }
+};
+
+void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const float*>& W) {
+  auto get = [&](const std::string& k) -> const float* {
+    auto it = W.find(k);
+    if (it == W.end()) {
+      if (pk.dry) return nullptr;
+      fail(CFM_ERR_WEIGHTS, "missing weight: " + k);
+    }
+    return it->second;
+  };
+  const int d = h->d, C = h->C, dff = h->dff, K = h->K, H = h->H, dk = h->dk, dkp = h->dkp, F2 = h->F2;
+  const float* w;
+  // subsampling
+  h->conv1_w = pk.f32(get("pre_encode.conv.0.weight"), (long)C * 9);
+  h->conv1_b = pk.f32(get("pre_encode.conv.0.bias"), C);
+  w = get("pre_encode.conv.2.weight");                          // (C, C, 3, 3) -> [n][tap*C + c]
+  h->conv2_w = pk.mat(C, 9 * C, [&](int n, int k) { const int tap = k / C, c = k % C; return w[((long)n * C + c) * 9 + tap]; });
+  h->conv2_b = pk.f32(get("pre_encode.conv.2.bias"), C);
+  const float* wsub = get("pre_encode.out.weight");             // (d, C*F2) index c*F2+f -> [n][f*C + c]
+  h->sub_w = pk.mat(d, F2 * C, [&](int n, int k) { const int f = k / C, c = k % C; return wsub[(long)n * C * F2 + (long)c * F2 + f]; });
+  h->sub_b = pk.f32(get("pre_encode.out.bias"), d);
+  // all layers' linear_pos stacked: row (l, head, dd) -> W_l[head*dk + dd]
+  std::vector<const float*> wpos(h->L);
+  for (int l = 0; l < h->L; ++l) wpos[l] = get("layers." + std::to_string(l) + ".self_attn.linear_pos.weight");
+  h->pos_w = pk.mat(h->L * H * dkp, d, [&](int n, int k) {
+    const int l = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
+    return dd < dk ? wpos[l][(long)(hh * dk + dd) * d + k] : 0.0f;
+  });
+  h->layers.resize(h->L);
+  for (int l = 0; l < h->L; ++l) {
+    LayerW& Lw = h->layers[l];
+    const std::string p = "layers." + std::to_string(l) + ".";
+    auto mat_plain = [&](const std::string& key, int N, int Kk) {
+      const float* m = get(key);
+      return pk.mat(N, Kk, [=](int n, int k) { return m[(long)n * Kk + k]; });
+    };
+    Lw.ff1_w1 = mat_plain(p + "feed_forward1.linear1.weight", dff, d);
+    Lw.ff1_b1 = pk.f32(get(p + "feed_forward1.linear1.bias"), dff);
+    Lw.ff1_w2 = mat_plain(p + "feed_forward1.linear2.weight", d, dff);
+    Lw.ff1_b2 = pk.f32(get(p + "feed_forward1.linear2.bias"), d);
+    Lw.ff2_w1 = mat_plain(p + "feed_forward2.linear1.weight", dff, d);
+    Lw.ff2_b1 = pk.f32(get(p + "feed_forward2.linear1.bias"), dff);
+    Lw.ff2_w2 = mat_plain(p + "feed_forward2.linear2.weight", d, dff);
+    Lw.ff2_b2 = pk.f32(get(p + "feed_forward2.linear2.bias"), d);
+    // q | k | v with per-head padding dk -> dkp
+    const float* wq[3] = {get(p + "self_attn.linear_q.weight"), get(p + "self_attn.linear_k.weight"),
+                          get(p + "self_attn.linear_v.weight")};
+    const float* bq[3] = {get(p + "self_attn.linear_q.bias"), get(p + "self_attn.linear_k.bias"),
+                          get(p + "self_attn.linear_v.bias")};
+    Lw.qkv_w = pk.mat(3 * H * dkp, d, [&](int n, int k) {
+      const int part = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
+      return dd < dk ? wq[part][(long)(hh * dk + dd) * d + k] : 0.0f;
+    });
+    Lw.qkv_b = pk.f32(nullptr, round_up(3 * H * dkp, GEMM_BN), [&](long n) -> float {
+      if (n >= 3 * H * dkp) return 0.0f;
+      const int part = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
+      return dd < dk ? bq[part][hh * dk + dd] : 0.0f;
+    });
+    Lw.out_w = mat_plain(p + "self_attn.linear_out.weight", d, d);
+    Lw.out_b = pk.f32(get(p + "self_attn.linear_out.bias"), d);
+    Lw.pos_u = pk.f32(get(p + "self_attn.pos_bias_u"), (long)H * dk);
+    Lw.pos_v = pk.f32(get(p + "self_attn.pos_bias_v"), (long)H * dk);
+    // pointwise_conv1 (2d, d, 1) GLU-packed: 64-col group g = [value 32g.. | gate d+32g..]
+    const float* w1 = get(p + "conv.pointwise_conv1.weight");
+    const float* b1 = get(p + "conv.pointwise_conv1.bias");
+    const int G = (d + 31) / 32;
+    auto glu_src = [d](int n) -> int {   // packed column -> source row of pointwise_conv1 (-1: pad)
+      const int g = n / 64, j = n % 64, c = g * 32 + (j & 31);
+      if (c >= d) return -1;
+      return j < 32 ? c : d + c;
+    };
+    Lw.pw1_w = pk.mat(64 * G, d, [&](int n, int k) { const int s = glu_src(n); return s < 0 ? 0.0f : w1[(long)s * d + k]; });
+    Lw.pw1_b = pk.f32(nullptr, round_up(64 * G, GEMM_BN), [&](long n) -> float {
+      if (n >= 64 * G) return 0.0f;
+      const int s = glu_src((int)n);
+      return s < 0 ? 0.0f : b1[s];
+    });
+    Lw.dw_w = pk.f32(get(p + "conv.depthwise_conv.weight"), (long)d * K);
+    Lw.dw_b = pk.f32(get(p + "conv.depthwise_conv.bias"), d);
+    Lw.bn_w = pk.f32(get(p + "conv.batch_norm.weight"), d);
+    Lw.bn_b = pk.f32(get(p + "conv.batch_norm.bias"), d);
+    if (h->cfg.conv_norm_type == 0) {
+      Lw.bn_mean = pk.f32(get(p + "conv.batch_norm.running_mean"), d);
+      const float* rv = get(p + "conv.batch_norm.running_var");
+      Lw.bn_inv = pk.f32(nullptr, d, [&](long i) -> float { return 1.0f / std::sqrt(rv[i] + 1e-5f); });
+    } else {
+      Lw.bn_mean = Lw.bn_inv = -1;
+    }
+    Lw.pw2_w = mat_plain(p + "conv.pointwise_conv2.weight", d, d);
+    Lw.pw2_b = pk.f32(get(p + "conv.pointwise_conv2.bias"), d);
+    const char* lnn[5] = {"norm_feed_forward1", "norm_self_att", "norm_conv", "norm_feed_forward2", "norm_out"};
+    for (int i = 0; i < 5; ++i) {
+      Lw.ln_w[i] = pk.f32(get(p + lnn[i] + ".weight"), d);
+      Lw.ln_b[i] = pk.f32(get(p + lnn[i] + ".bias"), d);
+    }
+  }
+  if (h->has_out_proj) {
+    const float* wo = get("out_proj.weight");
+    h->outp_w = pk.mat(h->dout, d, [&](int n, int k) { return wo[(long)n * d + k]; });
+    h->outp_b = pk.f32(get("out_proj.bias"), h->dout);
+  }
+}
+
+void build_pe(cfm_encoder* h, int max_len) {
+  // RelPositionalEncoding.extend_pe/create_pe (multi_head_attention.py:235-248, 285-294), float32
+  const int d = h->d, rows = 2 * max_len - 1;
+  std::vector<char> host((size_t)rows * d * h->es);
+  const float scale = (float)(-(std::log(10000.0) / d));
+  std::vector<float> div(d / 2 + 1);
+  for (int i = 0; i < d; i += 2) div[i / 2] = std::exp((float)i * scale);
+  for (int r = 0; r < rows; ++r) {
+    const float pos = (float)(max_len - 1 - r);
+    for (int c = 0; c < d; ++c) {
+      const float a = pos * div[c / 2];
+      const float v = (c % 2 == 0) ? std::sin(a) : std::cos(a);
+      if (h->es == 4) ((float*)host.data())[(long)r * d + c] = v;
+      else ((uint16_t*)host.data())[(long)r * d + c] = host_f2bf(v);
+    }
+  }
+  if (h->pe) (void)hipFree(h->pe);
+  h->pe = nullptr;
+  HIP_OK(hipMalloc(&h->pe, host.size()));
+  HIP_OK(hipMemcpy(h->pe, host.data(), host.size(), hipMemcpyHostToDevice));
+  h->max_len = max_len;
+}
+
+// ---------------------------------------------------------------------------------------------
+// workspace layout
+// ---------------------------------------------------------------------------------------------
+struct WsLayout {
+  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, total;
+  int T1, T2, Tp, M, Tpad;
+};
+
+WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
+  WsLayout w;
+  const long es = h->es;
+  w.T1 = host_calc_length(T, 1);
+  w.T2 = host_calc_length(T, 2);
+  w.Tp = w.T2;
+  w.M = B * w.Tp;
+  w.Tpad = (int)round_up(std::max(w.Tp, 1), 32);
+  long off = 0;
+  auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(bytes, 256) + 256; return o; };
+  const long M = w.M;
+  w.X1 = take((long)B * w.T1 * h->F1 * h->C * es);
+  w.X2 = take((long)B * w.T2 * h->F2 * h->C * es);
+  w.X = take(M * h->d * 4);
+  w.Hn = take(M * h->d * es);
+  w.U = take(M * h->dff * es);
+  w.QK = take(M * 2 * h->H * h->dkp * es);
+  w.Vt = take((long)B * h->H * h->vt_rows * w.Tpad * es);
+  w.O = take(M * h->d * es);
+  w.G = take(M * h->d * es);
+  w.S = take(M * h->d * es);
+  w.P = take((long)(2 * w.Tp - 1) * h->L * h->H * h->dkp * es + 64);
+  w.PN = h->cfg.conv_norm_type == 1 ? take(M * h->d * 4) : -1;
+  w.Y = h->has_out_proj ? take(M * h->dout * 4) : -1;
+  w.total = round_up(off, 256);
+  return w;
+}
+
+GemmEpi epi_of(int mode, const float* bias, float alpha = 1.0f) {
+  GemmEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = mode;
+  e.bias = bias;
+  e.alpha = alpha;
+  return e;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+const char* cfm_last_error(void) { return g_last_error.c_str(); }
+int cfm_version(void) { return 1; }
+int cfm_encoded_length(int len) { return host_calc_length(len, 2); }
+
+cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int compute_mode, cfm_encoder** out) {
+  return guarded([&] {
+    if (!cfg || !out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (compute_mode != CFM_COMPUTE_FP32 && compute_mode != CFM_COMPUTE_BF16) fail(CFM_ERR_INVALID_ARG, "compute_mode");
+    if (cfg->subsampling_factor != 4) fail(CFM_ERR_UNSUPPORTED, "only subsampling='striding', factor 4 is implemented");
+    if (cfg->d_model <= 0 || cfg->n_heads <= 0 || cfg->d_model % cfg->n_heads) fail(CFM_ERR_INVALID_ARG, "d_model % n_heads");
+    if (cfg->d_model % 8) fail(CFM_ERR_UNSUPPORTED, "d_model must be a multiple of 8");
+    if (cfg->d_model > 2048) fail(CFM_ERR_UNSUPPORTED, "d_model > 2048");
+    if (cfg->conv_kernel_size % 2 == 0 || cfg->conv_kernel_size > 65) fail(CFM_ERR_UNSUPPORTED, "conv_kernel_size");
+    if (cfg->feat_in > 262 || cfg->feat_in < 1) fail(CFM_ERR_UNSUPPORTED, "feat_in");
+    if (cfg->n_layers < 0) fail(CFM_ERR_INVALID_ARG, "n_layers");
+    std::unique_ptr<cfm_encoder> h(new cfm_encoder());
+    h->cfg = *cfg;
+    h->device = device;
+    h->dtype = compute_mode == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16;
+    h->es = dtype_size(h->dtype);
+    h->bke = GEMM_BK_BYTES / h->es;
+    h->d = cfg->d_model;
+    h->H = cfg->n_heads;
+    h->dk = h->d / h->H;
+    h->dkp = (int)round_up(h->dk, 16);
+    if (h->dkp > 128) fail(CFM_ERR_UNSUPPORTED, "head dim > 128");
+    h->vt_rows = (int)round_up(h->dkp, 32);
+    h->dff = h->d * cfg->ff_expansion_factor;
+    h->C = cfg->subsampling_conv_channels > 0 ? cfg->subsampling_conv_channels : h->d;
+    if (h->C % 8) fail(CFM_ERR_UNSUPPORTED, "subsampling_conv_channels must be a multiple of 8");
+    h->F = cfg->feat_in;
+    h->F1 = (h->F - 1) / 2 + 1;
+    h->F2 = (h->F1 - 1) / 2 + 1;
+    h->K = cfg->conv_kernel_size;
+    h->L = cfg->n_layers;
+    h->has_out_proj = cfg->feat_out > 0 && cfg->feat_out != h->d;
+    h->dout = h->has_out_proj ? cfg->feat_out : h->d;
+    if (h->dff % 8) fail(CFM_ERR_UNSUPPORTED, "d_ff must be a multiple of 8");
+    int prev = 0;
+    HIP_OK(hipGetDevice(&prev));
+    HIP_OK(hipSetDevice(device));
+    build_param_list(h.get());
+    HIP_OK(hipMalloc(&h->zero_page, 4096));
+    HIP_OK(hipMemset(h->zero_page, 0, 4096));
+    build_pe(h.get(), std::max(cfg->pos_emb_max_len, 1));
+    HIP_OK(hipSetDevice(prev));
+    *out = h.release();
+  });
+}
+
+void cfm_encoder_destroy(cfm_encoder* h) {
+  if (!h) return;
+  if (h->wbuf) (void)hipFree(h->wbuf);
+  if (h->pe) (void)hipFree(h->pe);
+  if (h->zero_page) (void)hipFree(h->zero_page);
+  delete h;
+}
+
+int cfm_encoder_param_count(const cfm_encoder* h) { return h ? (int)h->params.size() : 0; }
+const char* cfm_encoder_param_name(const cfm_encoder* h, int i) {
+  return (h && i >= 0 && i < (int)h->params.size()) ? h->params[i].first.c_str() : nullptr;
+}
+int64_t cfm_encoder_param_numel(const cfm_encoder* h, int i) {
+  return (h && i >= 0 && i < (int)h->params.size()) ? h->params[i].second : -1;
+}
+
+cfm_status cfm_encoder_set_weights(cfm_encoder* h, const cfm_tensor_view* table, int n, void* stream) {
+  return guarded([&] {
+    if (!h || (!table && n)) fail(CFM_ERR_INVALID_ARG, "null argument");
+    int prev = 0;
+    HIP_OK(hipGetDevice(&prev));
+    HIP_OK(hipSetDevice(h->device));
+    if (stream) HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+    std::map<std::string, int64_t> expect(h->params.begin(), h->params.end());
+    std::map<std::string, std::vector<float>> host;
+    std::map<std::string, const float*> W;
+    for (int i = 0; i < n; ++i) {
+      if (!table[i].name) fail(CFM_ERR_INVALID_ARG, "unnamed tensor");
+      const std::string key = table[i].name;
+      auto it = expect.find(key);
+      if (it == expect.end()) continue;   // e.g. num_batches_tracked
+      if (table[i].numel != it->second)
+        fail(CFM_ERR_WEIGHTS, "size mismatch for " + key + ": got " + std::to_string(table[i].numel) +
+                                  ", expected " + std::to_string(it->second));
+      if (table[i].on_device) {
+        std::vector<float>& v = host[key];
+        v.resize(table[i].numel);
+        HIP_OK(hipMemcpy(v.data(), table[i].data, table[i].numel * 4, hipMemcpyDeviceToHost));
+        W[key] = v.data();
+      } else {
+        W[key] = table[i].data;
+      }
+    }
+    for (auto& kv : expect)
+      if (!W.count(kv.first)) fail(CFM_ERR_WEIGHTS, "missing weight: " + kv.first);
+    Packer dry{h};
+    pack_all(h, dry, W);
+    Packer pk{h};
+    pk.dry = false;
+    pk.buf.assign(round_up(dry.off, 256), 0);
+    pack_all(h, pk, W);
+    if (h->wbuf && h->wbytes < pk.buf.size()) { HIP_OK(hipFree(h->wbuf)); h->wbuf = nullptr; }
+    if (!h->wbuf) { HIP_OK(hipMalloc(&h->wbuf, pk.buf.size())); h->wbytes = pk.buf.size(); }
+    HIP_OK(hipMemcpy(h->wbuf, pk.buf.data(), pk.buf.size(), hipMemcpyHostToDevice));
+    h->weights_set = true;
+    HIP_OK(hipSetDevice(prev));
+  });
+}
+
+cfm_status cfm_encoder_set_max_audio_length(cfm_encoder* h, int max_audio_length) {
+  return guarded([&] {
+    if (!h || max_audio_length < 1) fail(CFM_ERR_INVALID_ARG, "bad argument");
+    if (max_audio_length <= h->max_len) return;   // extend_pe only grows (multi_head_attention.py:288)
+    int prev = 0;
+    HIP_OK(hipGetDevice(&prev));
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipDeviceSynchronize());
+    build_pe(h, max_audio_length);
+    HIP_OK(hipSetDevice(prev));
+  });
+}
+
+int cfm_encoder_max_audio_length(const cfm_encoder* h) { return h ? h->max_len : 0; }
+
+size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T) {
+  if (!h || B <= 0 || T <= 0) return 0;
+  return (size_t)ws_layout(h, B, T).total;
+}
+
+}  // extern "C"
+
+namespace {
+
+enum Stage { ST_LEN, ST_CONV1, ST_CONV2, ST_SUBOUT, ST_POS, ST_LN, ST_FFN_UP, ST_FFN_DOWN, ST_QKV, ST_ATTN,
+             ST_OUTPROJ, ST_PW1, ST_DWCONV, ST_PW2, ST_OUT, ST_COUNT };
+const char* kStageNames[ST_COUNT] = {"lengths", "conv1", "conv2_gemm", "subsample_linear", "pos_gemm", "layernorm",
+                                     "ffn_up_gemm", "ffn_down_gemm", "qkv_gemm", "rel_attention", "out_proj_gemm",
+                                     "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output"};
+
+// Records a HIP event on the stream at every stage boundary (timed entry point only).
+struct StageTimer {
+  hipStream_t st;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> ids;
+  void mark(int id) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventRecord(e, st));
+    ev.push_back(e);
+    ids.push_back(id);
+  }
+  void finish(float* ms, int* launches) {
+    mark(-1);
+    HIP_OK(hipEventSynchronize(ev.back()));
+    for (size_t i = 0; i + 1 < ev.size(); ++i) {
+      float t = 0.f;
+      HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t; launches[ids[i]] += 1; }
+    }
+    for (auto e : ev) (void)hipEventDestroy(e);
+  }
+};
+#define TM(id) do { if (tm) tm->mark(id); } while (0)
+
+void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
+                 int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream, StageTimer* tm) {
+  {
+    if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+    if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
+    if (T > h->max_len) fail(CFM_ERR_INVALID_ARG, "T exceeds max_audio_length; call cfm_encoder_set_max_audio_length");
+    const WsLayout wl = ws_layout(h, B, T);
+    if (!workspace || workspace_bytes < (size_t)wl.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = stream;
+    char* ws = (char*)workspace;
+    const int dt = h->dtype, d = h->d, H = h->H, dkp = h->dkp, Tp = wl.Tp, M = wl.M, L = h->L;
+    const int es = h->es;
+    auto W = [&](long off) { return (const void*)(h->wbuf + off); };
+    auto Wf = [&](long off) { return (const float*)(h->wbuf + off); };
+    float* X = (float*)(ws + wl.X);
+    void* Hn = ws + wl.Hn;
+
+    // lengths (subsampling.py:164-171) -> out_len_b, used as the pad mask from here on
+    TM(ST_LEN);
+    calc_length(len_b, out_len_b, B, T, 2, st);
+    const int32_t* lens = out_len_b;
+
+    // ConvSubsampling (subsampling.py:163-176) + xscale (multi_head_attention.py:305-306)
+    TM(ST_CONV1);
+    conv1_subsample(dt, x_bft, B, h->F, T, Wf(h->conv1_w), Wf(h->conv1_b), h->C, ws + wl.X1, st);
+    {
+      TM(ST_CONV2);
+      ConvGeom g{ws + wl.X1, wl.T1, h->F1, wl.T2, h->F2, h->C};
+      GemmEpi e = epi_of(EPI_RELU, Wf(h->conv2_b));
+      e.C = ws + wl.X2;
+      e.ldc = h->C;
+      gemm_conv(dt, g, B, W(h->conv2_w), (int)h->kpad(9 * h->C), h->C, e, h->zero_page, st);
+    }
+    {
+      TM(ST_SUBOUT);
+      const float xs = h->cfg.xscaling ? (float)std::sqrt((double)d) : 1.0f;
+      GemmEpi e = epi_of(EPI_SCALE_F32, Wf(h->sub_b), xs);
+      e.X = X;
+      e.ldx = d;
+      gemm(dt, ws + wl.X2, (long)h->F2 * h->C, M, h->F2 * h->C, W(h->sub_w), (int)h->kpad(h->F2 * h->C), d, e,
+           h->zero_page, st);
+    }
+    const long ldp = (long)L * H * dkp;
+    if (L > 0) {
+      TM(ST_POS);
+      // linear_pos of every layer at once on pos_emb = pe[center - T' : center + T' - 1]
+      GemmEpi e = epi_of(EPI_STORE, nullptr);
+      e.C = ws + wl.P;
+      e.ldc = ldp;
+      const char* pe_slice = h->pe + (long)(h->max_len - Tp) * d * es;
+      gemm(dt, pe_slice, d, 2 * Tp - 1, d, W(h->pos_w), (int)h->kpad(d), (int)ldp, e, h->zero_page, st);
+      TM(ST_LN);
+      layernorm(dt, X, M, d, Wf(h->layers[0].ln_w[0]), Wf(h->layers[0].ln_b[0]), nullptr, nullptr, nullptr, Hn, 0, st);
+    }
+
+    for (int l = 0; l < L; ++l) {
+      const LayerW& Lw = h->layers[l];
+      // ---- FFN1 (conformer_modules.py:99-101) ----
+      {
+        TM(ST_FFN_UP);
+        GemmEpi e = epi_of(EPI_SWISH, Wf(Lw.ff1_b1));
+        e.C = ws + wl.U; e.ldc = h->dff;
+        gemm(dt, Hn, d, M, d, W(Lw.ff1_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
+        TM(ST_FFN_DOWN);
+        GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff1_b2), 0.5f);
+        r.X = X; r.ldx = d;
+        gemm(dt, ws + wl.U, h->dff, M, h->dff, W(Lw.ff1_w2), (int)h->kpad(h->dff), d, r, h->zero_page, st);
+      }
+      // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
+      TM(ST_LN);
+      layernorm(dt, X, M, d, Wf(Lw.ln_w[1]), Wf(Lw.ln_b[1]), nullptr, nullptr, nullptr, Hn, 0, st);
+      {
+        TM(ST_QKV);
+        GemmEpi e = epi_of(EPI_QKV, Wf(Lw.qkv_b));
+        e.C = ws + wl.QK; e.ldc = 2L * H * dkp; e.qk_cols = 2 * H * dkp;
+        e.Vt = ws + wl.Vt; e.H = H; e.dkp = dkp; e.vt_rows = h->vt_rows; e.Tpad = wl.Tpad; e.Tp = Tp;
+        gemm(dt, Hn, d, M, d, W(Lw.qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
+        TM(ST_ATTN);
+        rel_pos_attention(dt, ws + wl.QK, 2L * H * dkp, ws + wl.Vt, h->vt_rows, wl.Tpad,
+                          ws + wl.P + (long)l * H * dkp * es, ldp, Wf(Lw.pos_u), Wf(Lw.pos_v), lens, B, Tp, H, h->dk,
+                          dkp, h->cfg.att_context_left, h->cfg.att_context_right, ws + wl.O, d, st);
+        TM(ST_OUTPROJ);
+        GemmEpi r = epi_of(EPI_RESID, Wf(Lw.out_b), 1.0f);
+        r.X = X; r.ldx = d;
+        gemm(dt, ws + wl.O, d, M, d, W(Lw.out_w), (int)h->kpad(d), d, r, h->zero_page, st);
+      }
+      // ---- convolution module (conformer_modules.py:112-114, 160-180) ----
+      TM(ST_LN);
+      layernorm(dt, X, M, d, Wf(Lw.ln_w[2]), Wf(Lw.ln_b[2]), nullptr, nullptr, nullptr, Hn, 0, st);
+      {
+        TM(ST_PW1);
+        GemmEpi e = epi_of(EPI_GLU_MASK, Wf(Lw.pw1_b));
+        e.C = ws + wl.G; e.ldc = d; e.lens = lens; e.Tp = Tp;
+        gemm(dt, Hn, d, M, d, W(Lw.pw1_w), (int)h->kpad(d), d, e, h->zero_page, st);
+        TM(ST_DWCONV);
+        if (h->cfg.conv_norm_type == 0) {
+          dwconv_norm_swish(dt, ws + wl.G, B, Tp, d, h->K, Wf(Lw.dw_w), Wf(Lw.dw_b), Wf(Lw.bn_mean), Wf(Lw.bn_inv),
+                            Wf(Lw.bn_w), Wf(Lw.bn_b), ws + wl.S, nullptr, st);
+        } else {
+          float* pn = (float*)(ws + wl.PN);
+          dwconv_norm_swish(dt, ws + wl.G, B, Tp, d, h->K, Wf(Lw.dw_w), Wf(Lw.dw_b), nullptr, nullptr, nullptr, nullptr,
+                            nullptr, pn, st);
+          layernorm(dt, pn, M, d, Wf(Lw.bn_w), Wf(Lw.bn_b), nullptr, nullptr, nullptr, ws + wl.S, 1, st);
+        }
+        TM(ST_PW2);
+        GemmEpi r = epi_of(EPI_RESID, Wf(Lw.pw2_b), 1.0f);
+        r.X = X; r.ldx = d;
+        gemm(dt, ws + wl.S, d, M, d, W(Lw.pw2_w), (int)h->kpad(d), d, r, h->zero_page, st);
+      }
+      // ---- FFN2 (conformer_modules.py:116-118) ----
+      TM(ST_LN);
+      layernorm(dt, X, M, d, Wf(Lw.ln_w[3]), Wf(Lw.ln_b[3]), nullptr, nullptr, nullptr, Hn, 0, st);
+      {
+        TM(ST_FFN_UP);
+        GemmEpi e = epi_of(EPI_SWISH, Wf(Lw.ff2_b1));
+        e.C = ws + wl.U; e.ldc = h->dff;
+        gemm(dt, Hn, d, M, d, W(Lw.ff2_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
+        TM(ST_FFN_DOWN);
+        GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff2_b2), 0.5f);
+        r.X = X; r.ldx = d;
+        gemm(dt, ws + wl.U, h->dff, M, h->dff, W(Lw.ff2_w2), (int)h->kpad(h->dff), d, r, h->zero_page, st);
+      }
+      // ---- norm_out (conformer_modules.py:120), fused with the next layer's first LayerNorm ----
+      const bool next = l + 1 < L;
+      const bool want_t = next || h->has_out_proj;
+      TM(ST_LN);
+      layernorm(dt, X, M, d, Wf(Lw.ln_w[4]), Wf(Lw.ln_b[4]), X, next ? Wf(h->layers[l + 1].ln_w[0]) : nullptr,
+                next ? Wf(h->layers[l + 1].ln_b[0]) : nullptr, want_t ? Hn : nullptr, 0, st);
+    }
+
+    const float* fin = X;
+    TM(ST_OUT);
+    if (h->has_out_proj) {   // out_proj (conformer_encoder.py:277-278)
+      if (L == 0) convert_f32(dt, X, Hn, (long)M * d, st);
+      GemmEpi e = epi_of(EPI_SCALE_F32, Wf(h->outp_b), 1.0f);
+      float* Y = (float*)(ws + wl.Y);
+      e.X = Y; e.ldx = h->dout;
+      gemm(dt, Hn, d, M, d, W(h->outp_w), (int)h->kpad(d), h->dout, e, h->zero_page, st);
+      fin = Y;
+    }
+    TM(ST_OUT);
+    transpose_out(fin, B, Tp, h->dout, y_bdt, st);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
+                               int32_t* out_len_b, void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, nullptr);
+  });
+}
+
+int cfm_num_stages(void) { return ST_COUNT; }
+const char* cfm_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : nullptr; }
+
+cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,
+                                     float* y_bdt, int32_t* out_len_b, void* workspace, size_t workspace_bytes,
+                                     void* stream, float* stage_ms, int* stage_launches) {
+  return guarded([&] {
+    if (!stage_ms || !stage_launches) fail(CFM_ERR_INVALID_ARG, "null stage arrays");
+    StageTimer tm{(hipStream_t)stream};
+    run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, &tm);
+    tm.finish(stage_ms, stage_launches);
+  });
+}
+
+// ---- kernel-level entry points -------------------------------------------------------------
+
+cfm_status cfm_op_layernorm(int dtype, const float* x, int rows, int d, const float* w, const float* b, float* y_f32,
+                            void* y_t, void* stream) {
+  return guarded([&] {
+    if (d % 4 || d > 2048) fail(CFM_ERR_UNSUPPORTED, "d must be a multiple of 4 and <= 2048");
+    layernorm(dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, x, rows, d, w, b, y_f32, nullptr, nullptr, y_t, 0,
+              (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w, const float* bias, int N, int act,
+                         void* y, void* pack_ws, size_t* pack_ws_bytes, void* stream) {
+  return guarded([&] {
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    const long Kp = round_up(K, GEMM_BK_BYTES / es), Np = round_up(N, GEMM_BN);
+    const size_t need = (size_t)(Np * Kp * es + round_up(Np * 4, 256) + 4096);
+    if (!pack_ws) {
+      if (!pack_ws_bytes) fail(CFM_ERR_INVALID_ARG, "pack_ws_bytes");
+      *pack_ws_bytes = need;
+      return;
+    }
+    if (K % (16 / es)) fail(CFM_ERR_UNSUPPORTED, "K must be a multiple of 16 bytes");
+    if (pack_ws_bytes && *pack_ws_bytes < need) fail(CFM_ERR_WORKSPACE, "pack workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<float> hw((size_t)N * K), hb(N, 0.0f);
+    HIP_OK(hipMemcpy(hw.data(), w, hw.size() * 4, hipMemcpyDeviceToHost));
+    if (bias) HIP_OK(hipMemcpy(hb.data(), bias, N * 4, hipMemcpyDeviceToHost));
+    std::vector<char> packed((size_t)(Np * Kp * es), 0);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) {
+        const float v = hw[(size_t)n * K + k];
+        if (es == 4) ((float*)packed.data())[n * Kp + k] = v;
+        else ((uint16_t*)packed.data())[n * Kp + k] = host_f2bf(v);
+      }
+    char* base = (char*)pack_ws;
+    char* bdev = base + Np * Kp * es;
+    char* zero = bdev + round_up(Np * 4, 256);
+    HIP_OK(hipMemcpy(base, packed.data(), packed.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(bdev, hb.data(), N * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(zero, 0, 4096));
+    GemmEpi e = epi_of(act == 1 ? EPI_RELU : act == 2 ? EPI_SWISH : EPI_STORE, (const float*)bdev);
+    e.C = y;
+    e.ldc = N;
+    gemm(dt, x, K, M, K, base, (int)Kp, N, e, zero, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk) {
+  const int es = dtype == CFM_COMPUTE_FP32 ? 4 : 2;
+  const long dkp = round_up(dk, 16), vt_rows = round_up(dkp, 32), Tpad = round_up(Tp, 32);
+  const long M = (long)B * Tp;
+  return (size_t)(round_up(M * 2 * H * dkp * es, 256) + round_up((long)B * H * vt_rows * Tpad * es, 256) +
+                  round_up((2L * Tp - 1) * H * dkp * es + 64, 256));
+}
+
+}  // extern "C"
+
+// head re-layout kernels used only by cfm_op_rel_attention (the encoder writes these layouts
+// directly from the QKV / pos GEMM epilogues)
+namespace {
+template <typename T>
+__global__ void pad_heads_kernel(const T* src, long rows, int H, int dk, int dkp, T* dst, long ldd) {
+  const long n = rows * H * dkp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (H * dkp);
+    const int c = (int)(i % (H * dkp)), hh = c / dkp, dd = c % dkp;
+    dst[r * ldd + c] = dd < dk ? src[r * H * dk + hh * dk + dd] : (T)0;
+  }
+}
+template <typename T>
+__global__ void vt_kernel(const T* v, int B, int Tp, int H, int dk, int vt_rows, int Tpad, T* vt) {
+  const long n = (long)B * H * vt_rows * Tpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(i % Tpad);
+    const long rest = i / Tpad;
+    const int dd = (int)(rest % vt_rows);
+    const long bh = rest / vt_rows;
+    const int hh = (int)(bh % H), b = (int)(bh / H);
+    vt[i] = (dd < dk && t < Tp) ? v[((long)b * Tp + t) * H * dk + hh * dk + dd] : (T)0;
+  }
+}
+template <typename T>
+void relayout(const void* q, const void* k, const void* v, const void* p, int B, int Tp, int H, int dk, int dkp,
+              int vt_rows, int Tpad, char* ws, long qk_bytes, long vt_bytes, hipStream_t st) {
+  const long M = (long)B * Tp;
+  T* QK = (T*)ws;
+  T* Vt = (T*)(ws + qk_bytes);
+  T* P = (T*)(ws + qk_bytes + vt_bytes);
+  const dim3 g(1024), b(256);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK, 2L * H * dkp);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)k, M, H, dk, dkp, QK + (long)H * dkp, 2L * H * dkp);
+  hipLaunchKernelGGL(vt_kernel<T>, g, b, 0, st, (const T*)v, B, Tp, H, dk, vt_rows, Tpad, Vt);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp);
+}
+}  // namespace
+
+extern "C" cfm_status cfm_op_rel_attention(int dtype, const void* q, const void* k, const void* v, const void* p,
+                                           const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp,
+                                           int H, int dk, int ctx_left, int ctx_right, void* out, void* ws,
+                                           void* stream) {
+  return guarded([&] {
+    if (dk > 128) fail(CFM_ERR_UNSUPPORTED, "head dim > 128");
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    const int dkp = (int)round_up(dk, 16), vt_rows = (int)round_up(dkp, 32), Tpad = (int)round_up(Tp, 32);
+    const long M = (long)B * Tp;
+    const long qk_bytes = round_up(M * 2 * H * dkp * es, 256);
+    const long vt_bytes = round_up((long)B * H * vt_rows * Tpad * es, 256);
+    hipStream_t st = (hipStream_t)stream;
+    if (dt == DT_F32) relayout<float>(q, k, v, p, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
+    else relayout<uint16_t>(q, k, v, p, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
+    char* w = (char*)ws;
+    rel_pos_attention(dt, w, 2L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes, (long)H * dkp, pos_u,
+                      pos_v, lens, B, Tp, H, dk, dkp, ctx_left, ctx_right, out, (long)H * dk, st);
+    HIP_OK(hipGetLastError());
+  });
+}

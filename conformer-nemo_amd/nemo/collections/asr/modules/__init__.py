@@ -1,0 +1,2 @@
+"""Module plugins resolvable by yaml `_target_` (reference nemo/collections/asr/modules)."""
+from nemo.collections.asr.modules.conformer_encoder import ConformerEncoder  # noqa: F401

@@ -1,0 +1,178 @@
+"""Drop-in `nemo.collections.asr.modules.ConformerEncoder` backed by the MI355X-native library.
+
+Same constructor kwargs (reference conformer_encoder.py:111-132), same module tree / state_dict keys
+(SURVEY §8b), same keyword-only forward contract (:231-234, typecheck) returning
+(outputs (B, d_model | feat_out, T') fp32, encoded_lengths (B,) int32).  The forward runs entirely in
+libcfm.so (include/cfm_encoder.h): one stream-ordered C call per forward on torch's current stream.
+
+Differences from the reference, by design:
+  * eval-mode forward only (dropout identities, BatchNorm running stats); `training=True` raises;
+  * update_max_seq_length's distributed MAX all_reduce (:283-294) is dropped: it only decides
+    whether to regrow the positional table, which is regrown per process on demand instead;
+  * compute precision is selectable: 'bf16' (default, MFMA bf16 operands / fp32 accumulation and
+    fp32 residual stream) or 'fp32' (exact-fp32 MFMA, the 1e-3 parity mode).  Set with the
+    `compute` attribute, `set_compute_mode()`, or the CFM_COMPUTE environment variable.
+"""
+from __future__ import annotations
+
+import math
+import os
+from collections import OrderedDict
+from typing import Optional
+
+import torch
+from torch import nn
+
+from nemo.collections.asr.parts.submodules.conformer_modules import ConformerLayer
+from nemo.collections.asr.parts.submodules.multi_head_attention import PositionalEncoding, RelPositionalEncoding
+from nemo.collections.asr.parts.submodules.subsampling import ConvSubsampling, calc_length
+from nemo.core.classes.common import typecheck
+from nemo.core.classes import Exportable
+from nemo.core.classes.module import NeuralModule
+from nemo.core.neural_types import AcousticEncodedRepresentation, LengthsType, NeuralType, SpectrogramType
+
+__all__ = ["ConformerEncoder"]
+
+
+class ConformerEncoder(NeuralModule, Exportable):
+    def input_example(self, max_batch=1, max_dim=256):
+        dev = next(self.parameters()).device
+        x = torch.randn(max_batch, self._feat_in, max_dim, device=dev)
+        lengths = torch.randint(1, max_dim, (max_batch,), device=dev, dtype=torch.int64)
+        return tuple([x, lengths])
+
+    @property
+    def input_types(self):
+        return OrderedDict({"audio_signal": NeuralType(("B", "D", "T"), SpectrogramType()),
+                            "length": NeuralType(tuple("B"), LengthsType())})
+
+    @property
+    def output_types(self):
+        return OrderedDict({"outputs": NeuralType(("B", "D", "T"), AcousticEncodedRepresentation()),
+                            "encoded_lengths": NeuralType(tuple("B"), LengthsType())})
+
+    def __init__(self, feat_in, n_layers, d_model, feat_out=-1, subsampling="striding", subsampling_factor=4,
+                 subsampling_conv_channels=-1, ff_expansion_factor=4, self_attention_model="rel_pos", n_heads=4,
+                 att_context_size=None, xscaling=True, untie_biases=True, pos_emb_max_len=5000, conv_kernel_size=31,
+                 conv_norm_type="batch_norm", dropout=0.1, dropout_emb=0.1, dropout_att=0.0):
+        super().__init__()
+        if self_attention_model != "rel_pos":
+            raise NotImplementedError(f"self_attention_model='{self_attention_model}': only 'rel_pos' is native")
+        d_ff = d_model * ff_expansion_factor
+        self.d_model = d_model
+        self._feat_in = feat_in
+        self.scale = math.sqrt(self.d_model)
+        self.att_context_size = list(att_context_size) if att_context_size else [-1, -1]
+        self.xscale = math.sqrt(d_model) if xscaling else None
+        if subsampling_conv_channels == -1:
+            subsampling_conv_channels = d_model
+        if not (subsampling and subsampling_factor > 1):
+            raise NotImplementedError("the native path requires conv subsampling")
+        self.pre_encode = ConvSubsampling(subsampling=subsampling, subsampling_factor=subsampling_factor,
+                                          feat_in=feat_in, feat_out=d_model, conv_channels=subsampling_conv_channels,
+                                          activation=nn.ReLU())
+        self._feat_out = d_model
+        pos_bias_u = pos_bias_v = None
+        if not untie_biases:
+            d_head = d_model // n_heads
+            pos_bias_u = nn.Parameter(torch.zeros(n_heads, d_head))
+            pos_bias_v = nn.Parameter(torch.zeros(n_heads, d_head))
+        self.pos_emb_max_len = pos_emb_max_len
+        self.pos_enc = RelPositionalEncoding(d_model=d_model, dropout_rate=dropout, max_len=pos_emb_max_len,
+                                             xscale=self.xscale, dropout_rate_emb=dropout_emb)
+        self.layers = nn.ModuleList([
+            ConformerLayer(d_model=d_model, d_ff=d_ff, self_attention_model=self_attention_model, n_heads=n_heads,
+                           conv_kernel_size=conv_kernel_size, conv_norm_type=conv_norm_type, dropout=dropout,
+                           dropout_att=dropout_att, pos_bias_u=pos_bias_u, pos_bias_v=pos_bias_v)
+            for _ in range(n_layers)])
+        if feat_out > 0 and feat_out != self._feat_out:
+            self.out_proj = nn.Linear(self._feat_out, feat_out)
+            self._feat_out = feat_out
+        else:
+            self.out_proj = None
+            self._feat_out = d_model
+        self._native_cfg = dict(feat_in=feat_in, n_layers=n_layers, d_model=d_model, feat_out=feat_out,
+                                subsampling_factor=subsampling_factor,
+                                subsampling_conv_channels=subsampling_conv_channels,
+                                ff_expansion_factor=ff_expansion_factor, n_heads=n_heads,
+                                att_context_size=self.att_context_size, xscaling=xscaling,
+                                pos_emb_max_len=pos_emb_max_len, conv_kernel_size=conv_kernel_size,
+                                conv_norm_type=conv_norm_type)
+        self.compute = os.environ.get("CFM_COMPUTE", "bf16")
+        self._native = {}           # (device, compute) -> NativeEncoder
+        self._native_versions = {}  # (device, compute) -> weight version snapshot
+        self.max_audio_length = pos_emb_max_len
+        self.use_pad_mask = True
+
+    # ---- reference API ---------------------------------------------------------------------
+    def set_max_audio_length(self, max_audio_length):
+        """Regrow the relative positional table (conformer_encoder.py:218-229)."""
+        self.max_audio_length = max(int(max_audio_length), self.max_audio_length)
+        self.pos_enc.extend_pe(self.max_audio_length)
+        for enc in self._native.values():
+            enc.set_max_audio_length(self.max_audio_length)
+
+    def update_max_seq_length(self, seq_length: int, device=None):
+        if seq_length > self.max_audio_length:
+            self.set_max_audio_length(seq_length)
+
+    def make_pad_mask(self, max_audio_length, seq_lens):
+        return torch.arange(max_audio_length, device=seq_lens.device).expand(seq_lens.size(0), -1) < seq_lens.unsqueeze(-1)
+
+    def enable_pad_mask(self, on=True):
+        mask = self.use_pad_mask
+        self.use_pad_mask = on
+        return mask
+
+    def set_compute_mode(self, compute: str):
+        if compute not in ("bf16", "fp32"):
+            raise ValueError("compute must be 'bf16' or 'fp32'")
+        self.compute = compute
+
+    @staticmethod
+    def calc_encoded_length(length):
+        return calc_length(length, padding=1, kernel_size=3, stride=2, ceil_mode=False, repeat_num=2)
+
+    # ---- native plumbing -----------------------------------------------------------------------
+    def _weight_tensors(self):
+        return {k: v for k, v in self.state_dict(keep_vars=True).items() if torch.is_floating_point(v)}
+
+    def _native_for(self, device: torch.device):
+        from conformer_amd import NativeEncoder, make_cfg
+
+        key = (device.index if device.index is not None else torch.cuda.current_device(), self.compute)
+        enc = self._native.get(key)
+        if enc is None:
+            with torch.cuda.device(key[0]):
+                enc = NativeEncoder(make_cfg(**self._native_cfg), device=key[0], compute=self.compute)
+                if self.max_audio_length > enc.max_audio_length:
+                    enc.set_max_audio_length(self.max_audio_length)
+            self._native[key] = enc
+        tensors = self._weight_tensors()
+        version = tuple((t.data_ptr(), t._version) for t in tensors.values())
+        if self._native_versions.get(key) != version:
+            with torch.cuda.device(key[0]):
+                enc.set_weights(tensors)
+            self._native_versions[key] = version
+        return enc
+
+    def _apply(self, fn, *args, **kwargs):
+        self._native_versions = {}
+        return super()._apply(fn, *args, **kwargs)
+
+    # ---- forward ---------------------------------------------------------------------------------
+    @typecheck()
+    def forward(self, audio_signal, length=None):
+        self.update_max_seq_length(seq_length=audio_signal.size(2), device=audio_signal.device)
+        return self.forward_for_export(audio_signal=audio_signal, length=length)
+
+    @typecheck()
+    def forward_for_export(self, audio_signal, length=None):
+        if self.training:
+            raise NotImplementedError("the native Conformer encoder implements the eval-mode forward; call .eval()")
+        if not self.use_pad_mask:
+            raise NotImplementedError("enable_pad_mask(False) is not supported by the native path")
+        if not audio_signal.is_cuda:
+            raise RuntimeError("ConformerEncoder (MI355X-native) expects audio_signal on a ROCm GPU")
+        enc = self._native_for(audio_signal.device)
+        return enc.forward(audio_signal, length)

@@ -1,0 +1,143 @@
+/*
+ * cfm_encoder.h — C-ABI of the MI355X-native Conformer encoder forward (libcfm.so).
+ *
+ * Drop-in boundary: this library replaces the arithmetic behind
+ *   nemo.collections.asr.modules.ConformerEncoder.forward()        (conformer_encoder.py:231-234)
+ *   ConformerEncoder.forward_for_export()                          (conformer_encoder.py:236-281)
+ * of the reference (nghiahuynh-ai/Conformer-NeMo, a NeMo 1.8.2 fork).  The reference has no native
+ * code on this path; its only "FFI" is the Python plugin contract (yaml `_target_` ->
+ * ConformerEncoder(**kwargs), keyword-only forward(audio_signal=, length=)).  The Python mirror in
+ * conformer-nemo_amd/nemo/collections/asr/modules/conformer_encoder.py binds these entry points
+ * with ctypes.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch types.  All tensor pointers passed to
+ *     cfm_encoder_forward are DEVICE pointers; `stream` is a hipStream_t passed as void*.
+ *   - Every call returns cfm_status; on failure cfm_last_error() returns a thread-local message.
+ *     No C++ exception crosses the ABI.
+ *   - cfm_encoder_forward is stream-ordered and host-sync free (graph-capturable): it allocates
+ *     nothing; all scratch lives in the caller-owned workspace.
+ *   - Threading: one handle per device; concurrent calls on distinct handles are safe.
+ */
+#ifndef CFM_ENCODER_H_
+#define CFM_ENCODER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int cfm_status;
+#define CFM_OK 0
+#define CFM_ERR_INVALID_ARG 1
+#define CFM_ERR_UNSUPPORTED 2
+#define CFM_ERR_HIP 3
+#define CFM_ERR_WORKSPACE 4
+#define CFM_ERR_WEIGHTS 5
+#define CFM_ERR_NOMEM 6
+
+/* Compute modes.  FP32: every contraction on v_mfma_f32_32x32x2_f32 (exact fp32 products) — the
+ * parity mode for the north-star 1e-3 relative gate.  BF16: operands in bf16 on
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation, fp32 residual stream / norms / softmax — the
+ * performance mode. */
+#define CFM_COMPUTE_FP32 0
+#define CFM_COMPUTE_BF16 1
+
+/* Constructor arguments of ConformerEncoder.__init__ (conformer_encoder.py:111-132).
+ * Eval-mode forward only: dropout / dropout_emb / dropout_att are identities and are not passed. */
+typedef struct cfm_encoder_cfg {
+  int feat_in;                   /* feat_in (80)                                     */
+  int n_layers;                  /* n_layers                                         */
+  int d_model;                   /* d_model                                          */
+  int feat_out;                  /* feat_out (-1: none)  -> out_proj if >0 and != d  */
+  int subsampling_factor;        /* must be 4 ('striding', 2 x Conv2d s2)            */
+  int subsampling_conv_channels; /* -1 -> d_model                                    */
+  int ff_expansion_factor;       /* d_ff = d_model * ff_expansion_factor             */
+  int n_heads;                   /* n_heads (self_attention_model must be 'rel_pos') */
+  int att_context_left;          /* att_context_size[0] (-1 = unlimited)             */
+  int att_context_right;         /* att_context_size[1] (-1 = unlimited)             */
+  int xscaling;                  /* 1: x *= sqrt(d_model) (conformer_encoder.py:144) */
+  int pos_emb_max_len;           /* pos_emb_max_len (5000)                           */
+  int conv_kernel_size;          /* conv_kernel_size (31), odd                       */
+  int conv_norm_type;            /* 0 = batch_norm, 1 = layer_norm                   */
+} cfm_encoder_cfg;
+
+/* One named fp32 tensor of the reference state_dict (keys as in SURVEY §8b, without the
+ * `encoder.` prefix).  `on_device` = 1 for device pointers, 0 for host pointers. */
+typedef struct cfm_tensor_view {
+  const char* name;
+  const float* data;
+  int64_t numel;
+  int on_device;
+} cfm_tensor_view;
+
+typedef struct cfm_encoder cfm_encoder;
+
+const char* cfm_last_error(void);
+int cfm_version(void);
+
+/* calc_length (subsampling.py:272-282) on the host: encoder frames for `len` input frames. */
+int cfm_encoded_length(int len);
+
+cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int compute_mode, cfm_encoder** out);
+void cfm_encoder_destroy(cfm_encoder* h);
+
+/* Copy + pack every parameter / buffer of the reference state_dict.  All keys listed by
+ * cfm_encoder_param_count/cfm_encoder_param_name must be present (num_batches_tracked is optional).
+ * May allocate and synchronises `stream`.  Call again whenever the weights change. */
+cfm_status cfm_encoder_set_weights(cfm_encoder* h, const cfm_tensor_view* table, int n, void* stream);
+int cfm_encoder_param_count(const cfm_encoder* h);
+const char* cfm_encoder_param_name(const cfm_encoder* h, int i);
+int64_t cfm_encoder_param_numel(const cfm_encoder* h, int i);
+
+/* set_max_audio_length (conformer_encoder.py:218-229): regrow the relative positional table so
+ * inputs of up to `max_audio_length` frames are accepted.  Allocates; not stream-ordered. */
+cfm_status cfm_encoder_set_max_audio_length(cfm_encoder* h, int max_audio_length);
+int cfm_encoder_max_audio_length(const cfm_encoder* h);
+
+/* Bytes of caller-owned device workspace needed by cfm_encoder_forward for (B, T). */
+size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T);
+
+/* forward_for_export (conformer_encoder.py:236-281), eval mode.
+ *   x_bft      (B, feat_in, T) fp32, device
+ *   len_b      (B,) int32 device, or NULL (every utterance has T frames: conformer_encoder.py:243-246)
+ *   y_bdt      (B, feat_out or d_model, T') fp32 device, T' = cfm_encoded_length(T)
+ *   out_len_b  (B,) int32 device: encoded lengths
+ * Requires T <= cfm_encoder_max_audio_length(h). */
+cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
+                               int32_t* out_len_b, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Same as cfm_encoder_forward, but records a HIP event at every kernel-group boundary on
+ * `stream`, synchronises, and ADDS the per-stage device time (ms) and launch counts into
+ * stage_ms[cfm_num_stages()] / stage_launches[cfm_num_stages()].  Not graph-capturable;
+ * used for the per-kernel roofline in bench.py. */
+int cfm_num_stages(void);
+const char* cfm_stage_name(int i);
+cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,
+                                     float* y_bdt, int32_t* out_len_b, void* workspace, size_t workspace_bytes,
+                                     void* stream, float* stage_ms, int* stage_launches);
+
+/* ---- kernel-level entry points (used by the per-kernel parity tests) ---------------------- */
+/* All buffers are device pointers; `dtype` is CFM_COMPUTE_FP32 (float) or CFM_COMPUTE_BF16 (uint16 bf16). */
+
+/* y = LayerNorm(x) (eps 1e-5) rows x d fp32 -> compute type (and optionally fp32 in y_f32). */
+cfm_status cfm_op_layernorm(int dtype, const float* x, int rows, int d, const float* w, const float* b, float* y_f32,
+                            void* y_t, void* stream);
+/* y[M,N] = x[M,K] . w[N,K]^T + bias (fp32 weights, packed internally into `pack_ws`).
+ * act: 0 none, 1 relu, 2 swish.  Returns the pack workspace size when pack_ws == NULL. */
+cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w, const float* bias, int N, int act,
+                         void* y, void* pack_ws, size_t* pack_ws_bytes, void* stream);
+/* Fused rel-pos attention core on projected q,k,v (M = B*T' rows, d = H*dk, compute type):
+ * out[M, d] = softmax_mask(((q+u)k^T + rel_shift((q+v)p^T)) / sqrt(dk)) v, p = pos projection
+ * rows (2T'-1, d).  Scratch `ws` of cfm_op_rel_attention_ws_size bytes. */
+size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk);
+cfm_status cfm_op_rel_attention(int dtype, const void* q, const void* k, const void* v, const void* p,
+                                const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
+                                int dk, int ctx_left, int ctx_right, void* out, void* ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFM_ENCODER_H_ */

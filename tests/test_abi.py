@@ -1,0 +1,63 @@
+"""CPU-side checks of the C-ABI library (no kernel launches): it loads, exports every symbol that
+include/cfm_encoder.h declares, and its host helpers agree with the oracle."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+import conformer_oracle as O
+from conftest import ROOT
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "cfm_encoder.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cfm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_header_symbols():
+    from conformer_amd import _lib
+    lib = _lib.load()
+    declared = _declared_symbols()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_lib.EXPORTED_SYMBOLS)
+    # and the .so really defines them (not just resolvable through another library)
+    out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
+    for name in declared:
+        assert re.search(rf"\bT {name}\b", out), name
+
+
+def test_encoded_length_matches_oracle():
+    from conformer_amd import _lib
+    lib = _lib.load()
+    Ls = np.arange(0, 5001)
+    ref = O.calc_length(Ls)
+    got = np.array([lib.cfm_encoded_length(int(L)) for L in Ls])
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_create_without_gpu_fails_cleanly():
+    """Without a GPU the library must report an error status, never crash or fall back."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    from conformer_amd import _lib, make_cfg
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    cfg = make_cfg(80, 2, 64, n_heads=4)
+    st = lib.cfm_encoder_create(ctypes.byref(cfg), 0, 1, ctypes.byref(h))
+    assert st != 0
+    assert lib.cfm_last_error()
+
+
+def test_bad_config_rejected():
+    from conformer_amd import _lib, make_cfg
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    cfg = make_cfg(80, 2, 60, n_heads=7)        # d_model % n_heads != 0
+    assert lib.cfm_encoder_create(ctypes.byref(cfg), 0, 1, ctypes.byref(h)) == 1
+    cfg = make_cfg(80, 2, 64, n_heads=4, subsampling_factor=8)
+    assert lib.cfm_encoder_create(ctypes.byref(cfg), 0, 1, ctypes.byref(h)) == 2
