@@ -9,11 +9,11 @@ namespace cfm {
 enum Dtype { DT_F32 = 0, DT_BF16 = 1 };
 inline int dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
 
-// GEMM tile geometry shared with the weight packer: packed weights are [Npad][Kpad] in the
-// compute type, Npad a multiple of GEMM_BN, Kpad a multiple of GEMM_BK_BYTES / elem_size.
-constexpr int GEMM_BM = 128;
-constexpr int GEMM_BN = 128;
+// GEMM geometry shared with the weight packer: packed weights are [Npad][Kpad] in the compute
+// type, Npad a multiple of GEMM_BN (the widest N tile), Kpad a multiple of GEMM_BK_BYTES / elem_size.
+constexpr int GEMM_BN = 256;
 constexpr int GEMM_BK_BYTES = 128;
+inline int round_up_int(int v, int m) { return (v + m - 1) / m * m; }
 
 enum Epilogue {
   EPI_STORE = 0,       // C[m,n] = acc + bias[n]                        (compute type)

@@ -2,14 +2,26 @@
 //
 //   C[M, N] = A[M, K] . Wp[N, K]^T   (+ fused epilogue)
 //
-// Wp is a weight pre-packed at load time ([Npad][Kpad], compute type, zero padded) — the
-// nn.Linear / Conv1d(k=1) layout, so both operands are read along K.  Tile 128x128, 4 waves (2x2),
-// each wave 64x64 = 2x2 MFMA 32x32 tiles.  K is consumed in 128-byte steps staged into a
-// double-buffered LDS image by global_load_lds_dwordx4 (16 B per lane); the XOR swizzle
-// `slot ^ ((row >> 1) & 7)` is applied on the SOURCE address (the LDS image is lane-linear) and
-// on the ds_read_b128 fragment read, which makes every 16-lane read group conflict-free.
-// Out-of-range A rows / K bytes read a zero page, so no tail handling is needed in the main loop.
-// Blocks are remapped so that each XCD owns a contiguous range of tiles (A panels stay in one L2).
+// Wp is a weight pre-packed at load time ([Npad][Kpad], compute type, zero padded) in the
+// nn.Linear / Conv1d(k=1) layout, so both operands are read along K.
+//
+// Main loop (per block: BM x BN tile, WM x WN waves, each wave (BM/WM) x (BN/WN) = MR x NR MFMA
+// 32x32 tiles):
+//   * K is consumed in 128-byte steps (64 bf16 / 32 fp32).  Each step's A and B tiles are copied
+//     HBM/L2 -> LDS by global_load_lds_dwordx4 (16 B per lane, 1 KiB = 8 rows per wave-instruction)
+//     issued from inline asm, so hipcc's waitcnt pass does not see them (it would otherwise put a
+//     vmcnt(0) in front of every ds_read and serialise the prefetch with the MFMAs).
+//   * 3-slot LDS ring: tiles k+1 and k+2 are in flight while tile k is multiplied; a counted
+//     `s_waitcnt vmcnt(G)` + raw s_barrier retires exactly tile k.
+//   * The XOR swizzle `slot ^ ((row >> 1) & 7)` is applied to the per-lane SOURCE address (the LDS
+//     image is lane-linear) and to the ds_read_b128 fragment read: every 16-lane read group hits
+//     16 distinct (bank-row half, slot) positions -> conflict-free.
+//   * Out-of-range A rows / K bytes read a zero page: no tail handling in the loop.
+//   * Blocks are remapped so that each XCD owns a contiguous range of tiles (A panels stay in one L2).
+// Epilogue: the fp32 accumulators are staged through LDS and written back row-major with 16-byte
+// vector accesses (bias, activation, GLU, residual read-modify-write all vectorised).
+#include <cstdlib>
+
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -17,18 +29,54 @@ namespace cfm {
 
 namespace {
 
-constexpr int BM = GEMM_BM, BN = GEMM_BN, BKB = GEMM_BK_BYTES;
-constexpr int NTHREADS = 256;
-constexpr int A_ROWS_PER_THREAD = BM / 32;   // glds instructions per thread for the A tile
-constexpr int B_ROWS_PER_THREAD = BN / 32;
-constexpr int MR = BM / 64, NR = BN / 64;    // 32x32 tiles per wave
+constexpr int BKB = GEMM_BK_BYTES;
+constexpr int NSTAGE = 3;
 
+template <int BM_, int BN_, int WM_, int WN_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int MR = BM / WM / 32, NR = BN / WN / 32;
+  static constexpr int GA = BM / 8 / NW, GB = BN / 8 / NW;     // glds per thread per stage
+  static constexpr int STAGE_BYTES = (BM + BN) * BKB;
+  static constexpr int EPS = BN + 4;                           // fp32 stride of the epilogue image
+  static constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > BM * EPS * 4) ? NSTAGE * STAGE_BYTES : BM * EPS * 4;
+  static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
+};
+
+using T128x128 = Tile<128, 128, 2, 2>;
+using T256x128 = Tile<256, 128, 4, 2>;
+using T128x256 = Tile<128, 256, 2, 4>;
+using T64x128 = Tile<64, 128, 2, 2>;   // wave tile 32 x 64
+
+// ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
+CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+template <int N> CFM_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+CFM_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+CFM_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+CFM_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ---- A-operand loaders -----------------------------------------------------------------------
+template <int G>
 struct ALoadDense {
   const char* A; long lda_b; int M; long kbytes; const char* zero;
-  struct State { const char* row_ptr[A_ROWS_PER_THREAD]; };
+  struct State { const char* row_ptr[G]; };
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
 #pragma unroll
-    for (int i = 0; i < A_ROWS_PER_THREAD; ++i) {
+    for (int i = 0; i < G; ++i) {
       const int m = m0 + rows[i];
       s.row_ptr[i] = (m < M) ? A + (long)m * lda_b : nullptr;
     }
@@ -40,12 +88,13 @@ struct ALoadDense {
 
 // Row m = (b, t2, f2) of the implicit im2col matrix; column byte kb = (tap * C + c) * es with
 // tap = 3*kt + kf; source = X1[b][2*t2 - 1 + kt][2*f2 - 1 + kf][c] (zero outside the image).
+template <int G>
 struct ALoadConv {
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
-  struct State { const char* base[A_ROWS_PER_THREAD]; uint32_t valid[A_ROWS_PER_THREAD]; };
+  struct State { const char* base[G]; uint32_t valid[G]; };
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
 #pragma unroll
-    for (int i = 0; i < A_ROWS_PER_THREAD; ++i) {
+    for (int i = 0; i < G; ++i) {
       const int m = m0 + rows[i];
       uint32_t v = 0;
       const char* base = nullptr;
@@ -60,15 +109,14 @@ struct ALoadConv {
             const int ti = ti0 + kt, fi = fi0 + kf;
             if (ti >= 0 && ti < T1 && fi >= 0 && fi < F1) v |= 1u << (kt * 3 + kf);
           }
-        // pointer to (ti0, fi0) may be out of range; only dereferenced for valid taps
-        base = X1 + (((long)b * T1 + ti0) * F1 + fi0) * tapb;
+        base = X1 + (((long)b * T1 + ti0) * F1 + fi0) * tapb;   // only dereferenced for valid taps
       }
       s.base[i] = base;
       s.valid[i] = v;
     }
   }
   CFM_DEV const void* src(const State& s, int i, long kb) const {
-    int tap = (int)(kb / tapb);
+    const int tap = (int)(kb / tapb);
     const long cb = kb - (long)tap * tapb;
     if (tap >= 9 || !((s.valid[i] >> tap) & 1u)) return zero;
     const int kt = tap / 3, kf = tap - kt * 3;
@@ -81,42 +129,152 @@ struct GemmParams {
   GemmEpi epi;
 };
 
-template <typename T, int EPI>
-CFM_DEV void epi_store(const GemmParams& p, int m, int n, float v) {
+// ---- epilogue: LDS image -> global, 16-byte vectors -------------------------------------------
+template <typename T, int EPI, class TL>
+CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
   const GemmEpi& e = p.epi;
-  if (m >= p.M || n >= p.N) return;
-  const float bias = e.bias ? e.bias[n] : 0.0f;
-  if constexpr (EPI == EPI_STORE) {
-    st_f<T>((T*)e.C + (long)m * e.ldc + n, v + bias);
-  } else if constexpr (EPI == EPI_RELU) {
-    st_f<T>((T*)e.C + (long)m * e.ldc + n, fmaxf(v + bias, 0.0f));
-  } else if constexpr (EPI == EPI_SWISH) {
-    st_f<T>((T*)e.C + (long)m * e.ldc + n, swishf(v + bias));
-  } else if constexpr (EPI == EPI_RESID) {
-    float* x = e.X + (long)m * e.ldx + n;
-    *x = *x + (v + bias) * e.alpha;
-  } else if constexpr (EPI == EPI_SCALE_F32) {
-    e.X[(long)m * e.ldx + n] = (v + bias) * e.alpha;
-  } else if constexpr (EPI == EPI_QKV) {
-    if (n < e.qk_cols) {
-      st_f<T>((T*)e.C + (long)m * e.ldc + n, v + bias);
-    } else {
-      const int nv = n - e.qk_cols;
-      const int h = nv / e.dkp, dd = nv - h * e.dkp;
+  const int tid = threadIdx.x;
+  if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
+    // fp32 output, 4 columns per thread-chunk
+    constexpr int CPR = TL::BN / 4;                 // chunks per row
+    constexpr int RPP = TL::NT / CPR;               // rows per pass
+    constexpr int NP = TL::BM / RPP;
+    const int cc = tid % CPR, r0 = tid / CPR;
+    const int n = n0 + cc * 4;
+    float4 bias = make_float4(0, 0, 0, 0);
+    const bool colok = n < p.N;
+    const bool full = n + 4 <= p.N;                 // partial chunk only if N % 4 != 0 (feat_out)
+    if (colok && e.bias) bias = full ? *(const float4*)(e.bias + n)
+                                     : make_float4(e.bias[n], n + 1 < p.N ? e.bias[n + 1] : 0.f,
+                                                   n + 2 < p.N ? e.bias[n + 2] : 0.f, 0.f);
+    float4 xv[NP];
+    if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int m = m0 + r0 + q * RPP;
+        xv[q] = (full && m < p.M) ? *(const float4*)(e.X + (long)m * e.ldx + n) : make_float4(0, 0, 0, 0);
+        if (!full && colok && m < p.M) {
+          const float* xp = e.X + (long)m * e.ldx + n;
+          xv[q].x = xp[0]; if (n + 1 < p.N) xv[q].y = xp[1]; if (n + 2 < p.N) xv[q].z = xp[2];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int r = r0 + q * RPP;
+      const int m = m0 + r;
+      if (!colok || m >= p.M) continue;
+      const float4 a = *(const float4*)(img + r * TL::EPS + cc * 4);
+      float4 o;
+      if constexpr (EPI == EPI_RESID) {
+        o.x = xv[q].x + (a.x + bias.x) * e.alpha; o.y = xv[q].y + (a.y + bias.y) * e.alpha;
+        o.z = xv[q].z + (a.z + bias.z) * e.alpha; o.w = xv[q].w + (a.w + bias.w) * e.alpha;
+      } else {
+        o.x = (a.x + bias.x) * e.alpha; o.y = (a.y + bias.y) * e.alpha;
+        o.z = (a.z + bias.z) * e.alpha; o.w = (a.w + bias.w) * e.alpha;
+      }
+      float* xo = e.X + (long)m * e.ldx + n;
+      if (full) {
+        *(float4*)xo = o;
+      } else {
+        xo[0] = o.x; if (n + 1 < p.N) xo[1] = o.y; if (n + 2 < p.N) xo[2] = o.z;
+      }
+    }
+  } else if constexpr (EPI == EPI_GLU_MASK) {
+    // packed columns: per 64-column group g, [0,32) = value channels 32g.., [32,64) = gates
+    constexpr int VE = 16 / (int)sizeof(T);          // output elements per 16-byte chunk
+    constexpr int CPR = (TL::BN / 2) / VE;
+    constexpr int RPP = TL::NT / CPR;
+    constexpr int NP = TL::BM / RPP;
+    const int cc = tid % CPR, r0 = tid / CPR;
+    const int oc_local = cc * VE;                    // output channel within the block (BN/2 wide)
+    const int grp = oc_local / 32, j = oc_local % 32;
+    const int ca = grp * 64 + j, cg = grp * 64 + 32 + j;   // packed columns within the tile
+    const int c = n0 / 2 + oc_local;                 // output channel
+    float ba[VE], bg[VE];
+#pragma unroll
+    for (int i = 0; i < VE; ++i) { ba[i] = e.bias[n0 + ca + i]; bg[i] = e.bias[n0 + cg + i]; }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int r = r0 + q * RPP;
+      const int m = m0 + r;
+      if (m >= p.M || c >= p.N) continue;
       const int b = m / e.Tp, t = m - b * e.Tp;
-      st_f<T>((T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t, v + bias);
+      const bool masked = t >= e.lens[b];
+      float o[VE];
+#pragma unroll
+      for (int i = 0; i < VE; ++i) {
+        const float a = img[r * TL::EPS + ca + i] + ba[i];
+        const float g = img[r * TL::EPS + cg + i] + bg[i];
+        o[i] = masked ? 0.0f : a * sigmoidf_(g);
+      }
+      T* dst = (T*)e.C + (long)m * e.ldc + c;
+      if (c + VE <= p.N) {
+        *(uint4*)dst = Vec16<T>::from_f32(o);
+      } else {
+        for (int i = 0; i < VE && c + i < p.N; ++i) st_f<T>(dst + i, o[i]);
+      }
+    }
+  } else {
+    // compute-type output (EPI_STORE / RELU / SWISH / QKV's q,k part); EPI_QKV's v part transposed
+    constexpr int VE = 16 / (int)sizeof(T);
+    constexpr int CPR = TL::BN / VE;
+    constexpr int RPP = TL::NT / CPR;
+    constexpr int NP = TL::BM / RPP;
+    const int cc = tid % CPR, r0 = tid / CPR;
+    const int n = n0 + cc * VE;
+    const int nlim = (EPI == EPI_QKV) ? e.qk_cols : p.N;
+    float bias[VE];
+#pragma unroll
+    for (int i = 0; i < VE; ++i) bias[i] = (e.bias && n + i < p.N) ? e.bias[n + i] : 0.0f;
+    if (n < nlim) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int r = r0 + q * RPP;
+        const int m = m0 + r;
+        if (m >= p.M) continue;
+        float o[VE];
+#pragma unroll
+        for (int i = 0; i < VE; ++i) {
+          float v = img[r * TL::EPS + cc * VE + i] + bias[i];
+          if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
+          if constexpr (EPI == EPI_SWISH) v = swishf(v);
+          o[i] = v;
+        }
+        T* dst = (T*)e.C + (long)m * e.ldc + n;
+        if (n + VE <= nlim && ((e.ldc * (long)sizeof(T)) % 16 == 0)) {
+          *(uint4*)dst = Vec16<T>::from_f32(o);
+        } else {
+          for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
+        }
+      }
+    }
+    if constexpr (EPI == EPI_QKV) {
+      // V columns -> Vt[(b*H + h)][dd][t]: lanes walk rows (time) so stores are contiguous in t
+      if (n0 + TL::BN > e.qk_cols) {
+        const int c_lo = (e.qk_cols > n0 ? e.qk_cols - n0 : 0);
+        for (int idx = tid; idx < TL::BM * TL::BN; idx += TL::NT) {
+          const int r = idx % TL::BM, cl = idx / TL::BM;
+          if (cl < c_lo) continue;
+          const int m = m0 + r, nn = n0 + cl;
+          if (m >= p.M || nn >= p.N) continue;
+          const int nv = nn - e.qk_cols;
+          const int h = nv / e.dkp, dd = nv - h * e.dkp;
+          const int b = m / e.Tp, t = m - b * e.Tp;
+          st_f<T>((T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t,
+                  img[r * TL::EPS + cl] + e.bias[nn]);
+        }
+      }
     }
   }
 }
 
-template <typename T, int EPI, class ALoad>
-__global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmParams p, ALoad aload) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * BKB];
-  auto As = [&](int buf) { return smem + buf * (BM + BN) * BKB; };
-  auto Bs = [&](int buf) { return smem + buf * (BM + BN) * BKB + BM * BKB; };
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+template <typename T, int EPI, class TL, class ALoad>
+__global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload) {
+  __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
 
   // XCD-aware bijective remap: blocks sharing an XCD (bid % 8) get a contiguous tile range.
   const int nblocks = p.Mtiles * p.Ntiles;
@@ -124,128 +282,150 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmParams p, ALoad aloa
   const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int mt = wg / p.Ntiles, nt = wg - mt * p.Ntiles;
-  const int m0 = mt * BM, n0 = nt * BN;
+  const int m0 = mt * TL::BM, n0 = nt * TL::BN;
 
-  // staging geometry: instruction i of this wave covers tile rows (i*4 + wave)*8 .. +7
-  int rows[A_ROWS_PER_THREAD];
-  int slot_off[A_ROWS_PER_THREAD];
+  // staging geometry: instruction i of this wave covers tile rows (i*NW + wave)*8 .. +7
+  int rows[TL::GA];
+  int aslot[TL::GA];
 #pragma unroll
-  for (int i = 0; i < A_ROWS_PER_THREAD; ++i) {
-    rows[i] = (i * 4 + wave) * 8 + (lane >> 3);
-    slot_off[i] = ((lane & 7) ^ ((rows[i] >> 1) & 7)) * 16;   // logical 16-B slot for this lane
+  for (int i = 0; i < TL::GA; ++i) {
+    rows[i] = (i * TL::NW + wave) * 8 + (lane >> 3);
+    aslot[i] = ((lane & 7) ^ ((rows[i] >> 1) & 7)) * 16;
   }
   typename ALoad::State ast;
   aload.prepare(ast, m0, rows);
-  const char* wrow[B_ROWS_PER_THREAD];
-  int wslot[B_ROWS_PER_THREAD];
+  const char* wrow[TL::GB];
 #pragma unroll
-  for (int i = 0; i < B_ROWS_PER_THREAD; ++i) {
-    const int rr = (i * 4 + wave) * 8 + (lane >> 3);
-    wrow[i] = p.W + (long)(n0 + rr) * p.ldw_b;
-    wslot[i] = ((lane & 7) ^ ((rr >> 1) & 7)) * 16;
+  for (int i = 0; i < TL::GB; ++i) {
+    const int rr = (i * TL::NW + wave) * 8 + (lane >> 3);
+    wrow[i] = p.W + (long)(n0 + rr) * p.ldw_b + ((lane & 7) ^ ((rr >> 1) & 7)) * 16;
   }
+  const uint32_t smem_base = lds_addr(smem);
 
-  auto stage = [&](int kt, int buf) {
+  auto stage = [&](int kt, int slot) {
     const long kb0 = (long)kt * BKB;
+    const uint32_t sb = smem_base + slot * TL::STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < A_ROWS_PER_THREAD; ++i)
-      glds16(aload.src(ast, i, kb0 + slot_off[i]), As(buf) + (i * 4 + wave) * 1024);
+    for (int i = 0; i < TL::GA; ++i)
+      glds16_asm(aload.src(ast, i, kb0 + aslot[i]), sb + (i * TL::NW + wave) * 1024);
 #pragma unroll
-    for (int i = 0; i < B_ROWS_PER_THREAD; ++i)
-      glds16(wrow[i] + kb0 + wslot[i], Bs(buf) + (i * 4 + wave) * 1024);
+    for (int i = 0; i < TL::GB; ++i)
+      glds16_asm(wrow[i] + kb0, sb + TL::BM * BKB + (i * TL::NW + wave) * 1024);
   };
 
-  f32x16 acc[MR][NR];
+  f32x16 acc[TL::MR][TL::NR];
 #pragma unroll
-  for (int i = 0; i < MR; ++i)
+  for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-    for (int j = 0; j < NR; ++j) acc[i][j] = f32x16{};
+    for (int j = 0; j < TL::NR; ++j) acc[i][j] = f32x16{};
 
-  // fragment read offsets (row-dependent swizzle), per 32x32 sub-tile
-  int a_off[MR], b_off[NR];
   const int hsel = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    const int rr = wm * (BM / 2) + i * 32 + (lane & 31);
-    a_off[i] = rr * BKB;
-  }
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int rr = wn * (BN / 2) + j * 32 + (lane & 31);
-    b_off[j] = rr * BKB;
-  }
-  const int a_sw = ((lane & 31) >> 1) & 7;   // (row >> 1) & 7 : rows are 32-aligned + (lane & 31)
+  const int a_row0 = wm * (TL::BM / TL::WM) + (lane & 31);
+  const int b_row0 = TL::BM + wn * (TL::BN / TL::WN) + (lane & 31);
+  const int sw = ((lane & 31) >> 1) & 7;   // rows are 32-aligned + (lane & 31)
 
+  const int nk = p.nk;
   stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < p.nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < p.nk) stage(kt + 1, buf ^ 1);
-    const char* Ab = As(buf);
-    const char* Bb = Bs(buf);
+  if (nk > 1) stage(1, 1);
+  int slot = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<TL::GA + TL::GB>();
+    else wait_vmcnt<0>();
+    wait_lgkm0();
+    raw_barrier();
+    if (kt + 2 < nk) stage(kt + 2, slot == 0 ? 2 : slot - 1);
+    const char* Sb = smem + slot * TL::STAGE_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BKB / 32; ++kk) {
-      const int slot = ((2 * kk + hsel) ^ a_sw) * 16;
-      uint4 af[MR], bfv[NR];
+      const int so = ((2 * kk + hsel) ^ sw) * 16;
+      uint4 af[TL::MR], bfv[TL::NR];
 #pragma unroll
-      for (int i = 0; i < MR; ++i) af[i] = *(const uint4*)(Ab + a_off[i] + slot);
+      for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * BKB + so);
 #pragma unroll
-      for (int j = 0; j < NR; ++j) bfv[j] = *(const uint4*)(Bb + b_off[j] + slot);
+      for (int j = 0; j < TL::NR; ++j) bfv[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * BKB + so);
 #pragma unroll
-      for (int i = 0; i < MR; ++i)
+      for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < NR; ++j) mfma_slab<T>(acc[i][j], af[i], bfv[j]);
+        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], af[i], bfv[j]);
     }
-    __syncthreads();
+    slot = (slot == NSTAGE - 1) ? 0 : slot + 1;
   }
 
-  // epilogue
+  // ---- epilogue through LDS ----
+  wait_lgkm0();
+  raw_barrier();                         // every wave is done reading the ring
+  float* img = (float*)smem;
   const int col = lane & 31;
-  if constexpr (EPI == EPI_GLU_MASK) {
-    // packed columns: per 64-column group g, [0,32) = value channels 32g.., [32,64) = gates
-    const GemmEpi& e = p.epi;
 #pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int ngrp = (n0 + wn * (BN / 2)) / 64;     // wave covers exactly one 64-col group (NR == 2)
-      const int c = ngrp * 32 + col;
-      const float ba = e.bias[ngrp * 64 + col], bg = e.bias[ngrp * 64 + 32 + col];
+  for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + acc_row(r, lane);
-        if (m >= p.M || c >= p.N) continue;
-        const int b = m / e.Tp, t = m - b * e.Tp;
-        float v = (acc[i][0][r] + ba) * sigmoidf_(acc[i][1][r] + bg);
-        if (t >= e.lens[b]) v = 0.0f;
-        st_f<T>((T*)e.C + (long)m * e.ldc + c, v);
+    for (int j = 0; j < TL::NR; ++j) {
+      const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int rl = wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane);
+        img[rl * TL::EPS + cl] = acc[i][j][rr];
       }
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int n = n0 + wn * (BN / 2) + j * 32 + col;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * (BM / 2) + i * 32 + acc_row(r, lane);
-          epi_store<T, EPI>(p, m, n, acc[i][j][r]);
-        }
-      }
+  __syncthreads();
+  epilogue<T, EPI, TL>(p, img, m0, n0);
+}
+
+template <typename T, class TL, template <int> class AL, class ALArgs>
+void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
+  using ALoad = AL<TL::GA>;
+  ALoad al;
+  args.fill(al);
+  const dim3 grid(p.Mtiles * p.Ntiles), block(TL::NT);
+  switch (p.epi.mode) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SWISH: hipLaunchKernelGGL((gemm_kernel<T, EPI_SWISH, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_RESID: hipLaunchKernelGGL((gemm_kernel<T, EPI_RESID, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SCALE_F32: hipLaunchKernelGGL((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_GLU_MASK: hipLaunchKernelGGL((gemm_kernel<T, EPI_GLU_MASK, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_QKV: hipLaunchKernelGGL((gemm_kernel<T, EPI_QKV, TL, ALoad>), grid, block, 0, st, p, al); break;
+    default: break;
   }
 }
 
-template <typename T, class ALoad>
-void launch(const GemmParams& p, const ALoad& al, hipStream_t st) {
-  const dim3 grid(p.Mtiles * p.Ntiles), block(NTHREADS);
-  switch (p.epi.mode) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_kernel<T, EPI_STORE, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_RELU: hipLaunchKernelGGL((gemm_kernel<T, EPI_RELU, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_SWISH: hipLaunchKernelGGL((gemm_kernel<T, EPI_SWISH, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_RESID: hipLaunchKernelGGL((gemm_kernel<T, EPI_RESID, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_SCALE_F32: hipLaunchKernelGGL((gemm_kernel<T, EPI_SCALE_F32, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_GLU_MASK: hipLaunchKernelGGL((gemm_kernel<T, EPI_GLU_MASK, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_QKV: hipLaunchKernelGGL((gemm_kernel<T, EPI_QKV, ALoad>), grid, block, 0, st, p, al); break;
-    default: break;
+struct DenseArgs {
+  const char* A; long lda_b; int M; long kbytes; const char* zero;
+  template <class AL> void fill(AL& al) const { al.A = A; al.lda_b = lda_b; al.M = M; al.kbytes = kbytes; al.zero = zero; }
+};
+struct ConvArgs {
+  const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
+  template <class AL> void fill(AL& al) const {
+    al.X1 = X1; al.T1 = T1; al.F1 = F1; al.T2 = T2; al.F2 = F2; al.tapb = tapb; al.M = M; al.zero = zero;
+  }
+};
+
+int packed_width(const GemmEpi& epi, int N) {
+  return epi.mode == EPI_GLU_MASK ? 64 * ((N + 31) / 32) : N;
+}
+
+// Tile choice: prefer the largest tile that still gives >= ~1 block per CU.
+int pick_tile(int M, int Nw) {
+  static const int forced = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
+  if (forced >= 0) return forced;
+  auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((Nw + bn - 1) / bn); };
+  if (blocks(256, 128) >= 240) return 1;
+  if (blocks(128, 128) >= 200) return 0;
+  return 3;
+}
+
+template <typename T, template <int> class AL, class ALArgs>
+void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
+  const int Nw = packed_width(p.epi, p.N);
+  auto setup = [&](int bm, int bn) {
+    p.Mtiles = (p.M + bm - 1) / bm;
+    p.Ntiles = (Nw + bn - 1) / bn;
+  };
+  switch (tile) {
+    case 1: setup(256, 128); launch_epi<T, T256x128, AL>(p, args, st); break;
+    case 2: setup(128, 256); launch_epi<T, T128x256, AL>(p, args, st); break;
+    case 3: setup(64, 128); launch_epi<T, T64x128, AL>(p, args, st); break;
+    default: setup(128, 128); launch_epi<T, T128x128, AL>(p, args, st); break;
   }
 }
 
@@ -254,9 +434,7 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
   p.W = (const char*)Wp;
   p.ldw_b = (long)Kpad * es;
   p.nk = (int)((long)Kpad * es / BKB);
-  p.Mtiles = (M + BM - 1) / BM;
-  p.Ntiles = (N + BN - 1) / BN;
-  if (epi.mode == EPI_GLU_MASK) p.Ntiles = (2 * ((N + 31) / 32) * 32 + BN - 1) / BN;  // packed width 64*ceil(N/32)
+  p.Mtiles = p.Ntiles = 0;
   p.M = M;
   p.N = N;
   p.epi = epi;
@@ -270,9 +448,11 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
   if (M <= 0) return;
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
-  ALoadDense al{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
-  if (dtype == DT_F32) launch<float>(p, al, st);
-  else launch<bf16_t>(p, al, st);
+  DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
+  int tile = pick_tile(M, packed_width(epi, N));
+  if (tile == 2 && round_up_int(packed_width(epi, N), 256) > round_up_int(packed_width(epi, N), GEMM_BN)) tile = 0;
+  if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
+  else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
 }
 
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
@@ -281,9 +461,11 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   if (M <= 0) return;
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
-  ALoadConv al{(const char*)g.X1, g.T1, g.F1, g.T2, g.F2, (long)g.C * es, M, (const char*)zero_page};
-  if (dtype == DT_F32) launch<float>(p, al, st);
-  else launch<bf16_t>(p, al, st);
+  ConvArgs a{(const char*)g.X1, g.T1, g.F1, g.T2, g.F2, (long)g.C * es, M, (const char*)zero_page};
+  int tile = pick_tile(M, N);
+  if (tile == 2) tile = 0;
+  if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
+  else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
 }
 
 }  // namespace cfm
