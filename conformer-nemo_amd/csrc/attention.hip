@@ -1,21 +1,23 @@
 // Fused Transformer-XL relative-position multi-head attention
 // (RelPositionMultiHeadAttention.forward, multi_head_attention.py:172-210, with forward_attention 94-115).
 //
-// For one (batch b, head h, 32-query tile) per wave:
-//   ac[i][j]  = (q_i + u_h) . k_j                               (:191, :199)
-//   bd[i][j]  = (q_i + v_h) . p_{T'-1-i+j}                      (:193, :203-206; rel_shift folded:
-//                                                                 bd_shifted[i][j] = bd[i][T'-1-i+j])
-//   s = (ac + bd) / sqrt(dk); masked keys excluded; softmax; P.V  (:208, :104-112)
-// The score matrix is never written to HBM.  Keys are visited in 32-key tiles with an online
-// (running max / sum) softmax.  Reference masking uses -10000 then zeroes masked probabilities;
-// for a query row with at least one valid key (every valid row: j = i is always valid) the
-// masked terms are exactly 0 in fp32, so excluding them is identical.  Rows i >= len are all
-// masked in the reference: their probabilities are zeroed (:107), so the output row is exactly 0.
+// One wave per (batch b, head h, 32-query tile).  For each 32-key tile:
+//   S^T[j][i] = k_j . (q_i + u_h)                       (ac, :191/:199; computed transposed)
+//   BD^T[r][i] = p_{r0+r} . (q_i + v_h), r in [0, 64)   (:193/:203 over the 63-row window the tile
+//                                                          needs; rel_shift (:159-170) is the skew
+//                                                          bd[i][j] = BD[i][j - i + 31], taken
+//                                                          through a 64x32 fp32 LDS image)
+//   s = (ac + bd) / sqrt(dk), masked keys excluded, online softmax, O += P.V  (:104-112)
+// The transposed orientation puts one query per lane (16 keys in lane l, 16 in lane l^32), so the
+// row max / row sum are in-register plus one cross-half swap, and the probabilities are already
+// the A operand of the P.V MFMA (no LDS round trip; the k-order permutation of a 32x32
+// accumulator used as operand is matched by the Vt chunk loads, see cdna_hip_programming.md §3).
+// Vt (V transposed, keys contiguous) is written by the QKV GEMM epilogue.  K/P/Vt fragments of the
+// next key tile are prefetched into registers while the current tile computes.
 //
-// Per key tile and wave: 32x32 ac (NS MFMA slabs), 32x64 bd window (2 x NS slabs), the skewed
-// gather bd[i][j - i + 31] through an LDS image, a row-per-lane-pair softmax pass, and P.V with
-// V read pre-transposed (Vt, written by the QKV GEMM epilogue) so both MFMA operands are
-// contiguous 16-byte loads.  K, P and Vt come straight from L2 (shared by all query tiles).
+// Masking (SURVEY §7 hard part 2): a query row with >= 1 valid key gets exactly the reference's
+// probabilities (the -10000-filled entries underflow to 0 in fp32); rows i >= len are fully masked
+// in the reference, whose probabilities are then zeroed (:107) -> their output is exactly 0.
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -35,20 +37,82 @@ struct AttnParams {
   char* out; long ldo;
 };
 
-constexpr int ACS = 33;   // fp32 row stride of the ac image (conflict-free row-pair reads)
-constexpr int BDS = 66;   // fp32 row stride of the 32x64 bd image
+constexpr int BDS = 32;   // fp32 row stride of the 64x32 BD^T image (conflict-free skewed reads)
+
+template <typename T> struct VChunk;                          // 4 keys of one Vt row
+template <> struct VChunk<bf16_t> { using type = uint2; };
+template <> struct VChunk<float> { using type = uint4; };
+
+template <typename T, int NS, int ND>
+struct TileRegs {
+  uint4 k[NS];
+  uint4 pa[NS], pb[NS];
+  typename VChunk<T>::type v[ND][4];
+};
+
+template <typename T, int NS, int ND>
+CFM_DEV void load_tile(TileRegs<T, NS, ND>& t, const AttnParams& p, const T* qk, long rowbase, const T* vt_head,
+                       int j0, int i0, int lane) {
+  constexpr int SE = 32 / (int)sizeof(T);
+  const int hsel = lane >> 5, col = lane & 31;
+  const int Tp = p.Tp;
+  const int j = min(j0 + col, Tp - 1);
+  const T* krow = qk + (rowbase + j) * p.ldqk + (long)(p.H + (int)blockIdx.y) * p.dkp;
+  const int pr0 = Tp - 1 - (i0 + 31) + j0;
+  const int ra = min(max(pr0 + col, 0), 2 * Tp - 2);
+  const int rb = min(max(pr0 + 32 + col, 0), 2 * Tp - 2);
+  const T* prowa = (const T*)p.P + (long)ra * p.ldp + (long)blockIdx.y * p.dkp;
+  const T* prowb = (const T*)p.P + (long)rb * p.ldp + (long)blockIdx.y * p.dkp;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int d0 = s * SE + hsel * (SE / 2);
+    t.k[s] = *(const uint4*)(krow + d0);
+    t.pa[s] = *(const uint4*)(prowa + d0);
+    t.pb[s] = *(const uint4*)(prowb + d0);
+  }
+#pragma unroll
+  for (int n = 0; n < ND; ++n)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      t.v[n][q] = *(const typename VChunk<T>::type*)(vt_head + (long)(n * 32 + col) * p.Tpad + j0 + 8 * q + 4 * hsel);
+}
+
+// O[n] += P . V for the 32 keys of the tile; s_acc holds P^T (rows = keys, lane = query).
+template <typename T, int ND> struct PV;
+template <int ND> struct PV<bf16_t, ND> {
+  static CFM_DEV void run(f32x16 (&o)[ND], const f32x16& pt, const uint2 (&v)[ND][4]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = pt[8 * s + e];
+      const uint4 a = Vec16<bf16_t>::from_f32(f);
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const uint4 b = make_uint4(v[n][2 * s].x, v[n][2 * s].y, v[n][2 * s + 1].x, v[n][2 * s + 1].y);
+        mfma_slab<bf16_t>(o[n], a, b);
+      }
+    }
+  }
+};
+template <int ND> struct PV<float, ND> {
+  static CFM_DEV void run(f32x16 (&o)[ND], const f32x16& pt, const uint4 (&v)[ND][4]) {
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint4 c = v[n][r >> 2];
+        const uint32_t bw = (r & 3) == 0 ? c.x : (r & 3) == 1 ? c.y : (r & 3) == 2 ? c.z : c.w;
+        o[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[r], __uint_as_float(bw), o[n], 0, 0, 0);
+      }
+  }
+};
 
 template <typename T, int NS, int ND>
 __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
-  constexpr int es = sizeof(T);
-  constexpr int SE = 32 / es;            // elements per 32-byte slab
-  constexpr int NSK = es;                // slabs per 32-key row (32 keys * es bytes / 32)
-  constexpr int PS = 32 * es + 16;       // byte stride of the P tile rows (padded)
-  __shared__ float ac_s[32 * ACS];
-  __shared__ float bd_s[32 * BDS];
-  __shared__ __attribute__((aligned(16))) char pt_s[32 * PS];
-  __shared__ float alpha_s[32];
-  __shared__ float l_s[32];
+  constexpr int SE = 32 / (int)sizeof(T);
+  __shared__ float bd_s[64 * BDS];
+  __shared__ float row_s[32];
 
   const int lane = threadIdx.x;
   const int hsel = lane >> 5, col = lane & 31;
@@ -57,8 +121,9 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
   const int len = min(p.lens[b], Tp);
   const T* qk = (const T*)p.qk;
   const long rowbase = (long)b * Tp;
+  const T* vt_head = (const T*)p.Vt + ((long)b * p.H + h) * p.vt_rows * p.Tpad;
 
-  // Q fragments with the two per-head biases (q + u for ac, q + v for bd), in fp32 then back.
+  // Q fragments (B operand, lane = query) with the per-head biases: q + u (ac), q + v (bd)
   uint4 qu[NS], qv[NS];
   {
     const int i = min(i0 + col, Tp - 1);
@@ -73,8 +138,10 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
       for (int e = 0; e < SE / 2; ++e) {
         const int d = d0 + e;
         const bool ok = d < p.dk;
-        fu[e] = ok ? f[e] + p.pos_u[h * p.dk + d] : 0.0f;
-        fv[e] = ok ? f[e] + p.pos_v[h * p.dk + d] : 0.0f;
+        const float bu = p.pos_u[h * p.dk + min(d, p.dk - 1)];   // unconditional loads
+        const float bv = p.pos_v[h * p.dk + min(d, p.dk - 1)];
+        fu[e] = ok ? f[e] + bu : 0.0f;
+        fv[e] = ok ? f[e] + bv : 0.0f;
       }
       qu[s] = Vec16<T>::from_f32(fu);
       qv[s] = Vec16<T>::from_f32(fv);
@@ -85,113 +152,104 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
 #pragma unroll
   for (int n = 0; n < ND; ++n) o[n] = f32x16{};
   float m_run = -INFINITY, l_run = 0.0f;
+  const int iq = i0 + col;                     // this lane's query
 
   int jbeg = 0, jend = len;
   if (p.ctx_left >= 0) jbeg = max(0, (i0 - p.ctx_left) & ~31);
   if (p.ctx_right >= 0) jend = min(jend, i0 + 31 + p.ctx_right + 1);
 
-  const int ri = lane >> 1, rc = lane & 1;     // softmax pass: row ri, keys 16rc .. 16rc+15
-  const int ig_row = i0 + ri;
-  const T* vt_head = (const T*)p.Vt + ((long)b * p.H + h) * p.vt_rows * p.Tpad;
+  // register prefetch of the next key tile when it fits the VGPR budget (bf16, dk <= 64)
+  constexpr bool PREFETCH = sizeof(T) == 2 && NS <= 4;
+  TileRegs<T, NS, ND> cur, nxt;
+  if (PREFETCH && jbeg < jend) load_tile(cur, p, qk, rowbase, vt_head, jbeg, i0, lane);
 
   for (int j0 = jbeg; j0 < jend; j0 += 32) {
-    // ---- scores ----
-    f32x16 sac = f32x16{}, sbd0 = f32x16{}, sbd1 = f32x16{};
-    {
-      const int j = min(j0 + col, Tp - 1);
-      const T* krow = qk + (rowbase + j) * p.ldqk + (long)(p.H + h) * p.dkp;
-      const int pr0 = Tp - 1 - (i0 + 31) + j0;
-      const int pa = min(max(pr0 + col, 0), 2 * Tp - 2);
-      const int pb = min(max(pr0 + 32 + col, 0), 2 * Tp - 2);
-      const T* prowa = (const T*)p.P + (long)pa * p.ldp + (long)h * p.dkp;
-      const T* prowb = (const T*)p.P + (long)pb * p.ldp + (long)h * p.dkp;
+    const bool more = j0 + 32 < jend;
+    if constexpr (PREFETCH) {
+      if (more) load_tile(nxt, p, qk, rowbase, vt_head, j0 + 32, i0, lane);
+    } else {
+      load_tile(cur, p, qk, rowbase, vt_head, j0, i0, lane);
+    }
+
+    f32x16 st = f32x16{}, bd0 = f32x16{}, bd1 = f32x16{};
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int d0 = s * SE + hsel * (SE / 2);
-        const uint4 kf = *(const uint4*)(krow + d0);
-        const uint4 pfa = *(const uint4*)(prowa + d0);
-        const uint4 pfb = *(const uint4*)(prowb + d0);
-        mfma_slab<T>(sac, qu[s], kf);
-        mfma_slab<T>(sbd0, qv[s], pfa);
-        mfma_slab<T>(sbd1, qv[s], pfb);
-      }
+    for (int s = 0; s < NS; ++s) {
+      mfma_slab<T>(st, cur.k[s], qu[s]);
+      mfma_slab<T>(bd0, cur.pa[s], qv[s]);
+      mfma_slab<T>(bd1, cur.pb[s], qv[s]);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int i = acc_row(r, lane);
-      ac_s[i * ACS + col] = sac[r];
-      bd_s[i * BDS + col] = sbd0[r];
-      bd_s[i * BDS + 32 + col] = sbd1[r];
+      const int rr = acc_row(r, lane);
+      bd_s[rr * BDS + col] = bd0[r];
+      bd_s[(rr + 32) * BDS + col] = bd1[r];
     }
     __syncthreads();
 
-    // ---- online softmax, two lanes per query row ----
-    float sv[16];
+    // scores for this lane's query and its 16 keys
     float mloc = -INFINITY;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int jj = 16 * rc + e;
+    for (int r = 0; r < 16; ++r) {
+      const int jj = acc_row(r, lane);          // key within the tile
       const int jg = j0 + jj;
-      float s = (ac_s[ri * ACS + jj] + bd_s[ri * BDS + jj - ri + 31]) / p.s_dk;
+      float s = (st[r] + bd_s[(jj - col + 31) * BDS + col]) / p.s_dk;
       bool masked = jg >= len;
-      if (p.ctx_left >= 0) masked |= jg < ig_row - p.ctx_left;
-      if (p.ctx_right >= 0) masked |= jg > ig_row + p.ctx_right;
-      sv[e] = masked ? -INFINITY : s;
-      mloc = fmaxf(mloc, sv[e]);
+      if (p.ctx_left >= 0) masked |= jg < iq - p.ctx_left;
+      if (p.ctx_right >= 0) masked |= jg > iq + p.ctx_right;
+      st[r] = masked ? -INFINITY : s;
+      mloc = fmaxf(mloc, st[r]);
     }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 1, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float m_new = fmaxf(m_run, mloc);
     float alpha = 1.0f, psum = 0.0f;
-    float pv[16];
     if (m_new == -INFINITY) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) pv[e] = 0.0f;
+      for (int r = 0; r < 16; ++r) st[r] = 0.0f;
     } else {
       alpha = __expf(m_run - m_new);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) { pv[e] = __expf(sv[e] - m_new); psum += pv[e]; }
+      for (int r = 0; r < 16; ++r) { st[r] = __expf(st[r] - m_new); psum += st[r]; }
     }
-    psum += __shfl_xor(psum, 1, 64);
+    psum += __shfl_xor(psum, 32, 64);
     l_run = l_run * alpha + psum;
     m_run = m_new;
-    {
-      char* dst = pt_s + ri * PS + 16 * rc * es;
-#pragma unroll
-      for (int q = 0; q < 16 / Vec16<T>::N; ++q)
-        *(uint4*)(dst + 16 * q) = Vec16<T>::from_f32(pv + q * Vec16<T>::N);
-    }
-    if (rc == 0) alpha_s[ri] = alpha;
+    if (hsel == 0) row_s[col] = alpha;
     __syncthreads();
-
-    // ---- rescale and accumulate P.V ----
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float a = alpha_s[acc_row(r, lane)];
+      const float a = row_s[acc_row(r, lane)];
 #pragma unroll
       for (int n = 0; n < ND; ++n) o[n][r] *= a;
     }
-    const bool tail = j0 + 32 > Tp;
+    if (j0 + 32 > Tp) {   // keys >= T' read Vt padding (unspecified): force those V entries to 0
 #pragma unroll
-    for (int s = 0; s < NSK; ++s) {
-      const uint4 pa4 = *(const uint4*)(pt_s + col * PS + s * 32 + hsel * 16);
-      const int k0 = j0 + s * SE + hsel * (SE / 2);
+      for (int n = 0; n < ND; ++n)
 #pragma unroll
-      for (int n = 0; n < ND; ++n) {
-        uint4 vb = *(const uint4*)(vt_head + (long)(n * 32 + col) * p.Tpad + k0);
-        if (tail) {   // keys >= T' hold unspecified data in Vt's padding: force them to 0
-          float f[SE / 2];
-          Vec16<T>::to_f32(vb, f);
-#pragma unroll
-          for (int e = 0; e < SE / 2; ++e) if (k0 + e >= Tp) f[e] = 0.0f;
-          vb = Vec16<T>::from_f32(f);
+        for (int q = 0; q < 4; ++q) {
+          const int kb = j0 + 8 * q + 4 * hsel;
+          if constexpr (sizeof(T) == 2) {
+            uint2& c = cur.v[n][q];
+            if (kb + 0 >= Tp) c.x &= 0xffff0000u;
+            if (kb + 1 >= Tp) c.x &= 0x0000ffffu;
+            if (kb + 2 >= Tp) c.y &= 0xffff0000u;
+            if (kb + 3 >= Tp) c.y &= 0x0000ffffu;
+          } else {
+            uint4& c = cur.v[n][q];
+            if (kb + 0 >= Tp) c.x = 0;
+            if (kb + 1 >= Tp) c.y = 0;
+            if (kb + 2 >= Tp) c.z = 0;
+            if (kb + 3 >= Tp) c.w = 0;
+          }
         }
-        mfma_slab<T>(o[n], pa4, vb);
-      }
     }
+    PV<T, ND>::run(o, st, cur.v);
     __syncthreads();
+    if constexpr (PREFETCH) {
+      if (more) cur = nxt;
+    }
   }
 
-  if (rc == 0) l_s[ri] = l_run;
+  if (hsel == 0) row_s[col] = l_run;
   __syncthreads();
   T* out = (T*)p.out;
 #pragma unroll
@@ -199,7 +257,7 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
     const int i = acc_row(r, lane);
     const int ig = i0 + i;
     if (ig >= Tp) continue;
-    const float l = l_s[i];
+    const float l = row_s[i];
     const bool valid = ig < len && l > 0.0f;
     const float inv = valid ? 1.0f / l : 0.0f;
 #pragma unroll
@@ -222,15 +280,24 @@ template <typename T>
 void launch_t(const AttnParams& p, dim3 grid, hipStream_t st) {
   constexpr int es = sizeof(T);
   const int NS = p.dkp * es / 32;
-  switch (NS) {
-    case 1: launch_nd<T, 1>(p, grid, st); break;
-    case 2: launch_nd<T, 2>(p, grid, st); break;
-    case 3: launch_nd<T, 3>(p, grid, st); break;
-    case 4: launch_nd<T, 4>(p, grid, st); break;
-    case 6: launch_nd<T, 6>(p, grid, st); break;
-    case 8: launch_nd<T, 8>(p, grid, st); break;
-    case 16: launch_nd<T, 16>(p, grid, st); break;
-    default: break;
+  if constexpr (sizeof(T) == 2) {      // dkp in {16, 32, 48, 64, 128}
+    switch (NS) {
+      case 1: launch_nd<T, 1>(p, grid, st); break;
+      case 2: launch_nd<T, 2>(p, grid, st); break;
+      case 3: launch_nd<T, 3>(p, grid, st); break;
+      case 4: launch_nd<T, 4>(p, grid, st); break;
+      case 8: launch_nd<T, 8>(p, grid, st); break;
+      default: break;
+    }
+  } else {
+    switch (NS) {
+      case 2: launch_nd<T, 2>(p, grid, st); break;
+      case 4: launch_nd<T, 4>(p, grid, st); break;
+      case 6: launch_nd<T, 6>(p, grid, st); break;
+      case 8: launch_nd<T, 8>(p, grid, st); break;
+      case 16: launch_nd<T, 16>(p, grid, st); break;
+      default: break;
+    }
   }
 }
 

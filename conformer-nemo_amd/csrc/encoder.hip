@@ -173,6 +173,11 @@ struct Packer {
     }
     return o;
   }
+  // GEMM bias: N floats zero-padded to the N granule (the GEMM adds bias[n] for every tile column)
+  long bias(const float* src, long n) {
+    const long np = round_up(n, GEMM_BN);
+    return f32(nullptr, np, [=](long i) -> float { return i < n ? src[i] : 0.0f; });
+  }
   // packed [Npad][Kpad] compute-type matrix; val(n, k) for n < N, k < K (others zero)
   long mat(int N, int K, std::function<float(int, int)> val) {
     const long Npad = round_up(N, GEMM_BN), Kp = h->kpad(K);
@@ -208,10 +213,10 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
   h->conv1_b = pk.f32(get("pre_encode.conv.0.bias"), C);
   w = get("pre_encode.conv.2.weight");                          // (C, C, 3, 3) -> [n][tap*C + c]
   h->conv2_w = pk.mat(C, 9 * C, [&](int n, int k) { const int tap = k / C, c = k % C; return w[((long)n * C + c) * 9 + tap]; });
-  h->conv2_b = pk.f32(get("pre_encode.conv.2.bias"), C);
+  h->conv2_b = pk.bias(get("pre_encode.conv.2.bias"), C);
   const float* wsub = get("pre_encode.out.weight");             // (d, C*F2) index c*F2+f -> [n][f*C + c]
   h->sub_w = pk.mat(d, F2 * C, [&](int n, int k) { const int f = k / C, c = k % C; return wsub[(long)n * C * F2 + (long)c * F2 + f]; });
-  h->sub_b = pk.f32(get("pre_encode.out.bias"), d);
+  h->sub_b = pk.bias(get("pre_encode.out.bias"), d);
   // all layers' linear_pos stacked: row (l, head, dd) -> W_l[head*dk + dd]
   std::vector<const float*> wpos(h->L);
   for (int l = 0; l < h->L; ++l) wpos[l] = get("layers." + std::to_string(l) + ".self_attn.linear_pos.weight");
@@ -228,13 +233,13 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       return pk.mat(N, Kk, [=](int n, int k) { return m[(long)n * Kk + k]; });
     };
     Lw.ff1_w1 = mat_plain(p + "feed_forward1.linear1.weight", dff, d);
-    Lw.ff1_b1 = pk.f32(get(p + "feed_forward1.linear1.bias"), dff);
+    Lw.ff1_b1 = pk.bias(get(p + "feed_forward1.linear1.bias"), dff);
     Lw.ff1_w2 = mat_plain(p + "feed_forward1.linear2.weight", d, dff);
-    Lw.ff1_b2 = pk.f32(get(p + "feed_forward1.linear2.bias"), d);
+    Lw.ff1_b2 = pk.bias(get(p + "feed_forward1.linear2.bias"), d);
     Lw.ff2_w1 = mat_plain(p + "feed_forward2.linear1.weight", dff, d);
-    Lw.ff2_b1 = pk.f32(get(p + "feed_forward2.linear1.bias"), dff);
+    Lw.ff2_b1 = pk.bias(get(p + "feed_forward2.linear1.bias"), dff);
     Lw.ff2_w2 = mat_plain(p + "feed_forward2.linear2.weight", d, dff);
-    Lw.ff2_b2 = pk.f32(get(p + "feed_forward2.linear2.bias"), d);
+    Lw.ff2_b2 = pk.bias(get(p + "feed_forward2.linear2.bias"), d);
     // q | k | v with per-head padding dk -> dkp
     const float* wq[3] = {get(p + "self_attn.linear_q.weight"), get(p + "self_attn.linear_k.weight"),
                           get(p + "self_attn.linear_v.weight")};
@@ -250,7 +255,7 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       return dd < dk ? bq[part][hh * dk + dd] : 0.0f;
     });
     Lw.out_w = mat_plain(p + "self_attn.linear_out.weight", d, d);
-    Lw.out_b = pk.f32(get(p + "self_attn.linear_out.bias"), d);
+    Lw.out_b = pk.bias(get(p + "self_attn.linear_out.bias"), d);
     Lw.pos_u = pk.f32(get(p + "self_attn.pos_bias_u"), (long)H * dk);
     Lw.pos_v = pk.f32(get(p + "self_attn.pos_bias_v"), (long)H * dk);
     // pointwise_conv1 (2d, d, 1) GLU-packed: 64-col group g = [value 32g.. | gate d+32g..]
@@ -268,7 +273,8 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       const int s = glu_src((int)n);
       return s < 0 ? 0.0f : b1[s];
     });
-    Lw.dw_w = pk.f32(get(p + "conv.depthwise_conv.weight"), (long)d * K);
+    const float* dww = get(p + "conv.depthwise_conv.weight");          // (d, 1, K) -> [K][d]
+    Lw.dw_w = pk.f32(nullptr, (long)d * K, [&](long i) -> float { return dww[(i % d) * K + i / d]; });
     Lw.dw_b = pk.f32(get(p + "conv.depthwise_conv.bias"), d);
     Lw.bn_w = pk.f32(get(p + "conv.batch_norm.weight"), d);
     Lw.bn_b = pk.f32(get(p + "conv.batch_norm.bias"), d);
@@ -280,7 +286,7 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       Lw.bn_mean = Lw.bn_inv = -1;
     }
     Lw.pw2_w = mat_plain(p + "conv.pointwise_conv2.weight", d, d);
-    Lw.pw2_b = pk.f32(get(p + "conv.pointwise_conv2.bias"), d);
+    Lw.pw2_b = pk.bias(get(p + "conv.pointwise_conv2.bias"), d);
     const char* lnn[5] = {"norm_feed_forward1", "norm_self_att", "norm_conv", "norm_feed_forward2", "norm_out"};
     for (int i = 0; i < 5; ++i) {
       Lw.ln_w[i] = pk.f32(get(p + lnn[i] + ".weight"), d);
@@ -290,7 +296,7 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
   if (h->has_out_proj) {
     const float* wo = get("out_proj.weight");
     h->outp_w = pk.mat(h->dout, d, [&](int n, int k) { return wo[(long)n * d + k]; });
-    h->outp_b = pk.f32(get("out_proj.bias"), h->dout);
+    h->outp_b = pk.bias(get("out_proj.bias"), h->dout);
   }
 }
 
@@ -407,6 +413,7 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     h->L = cfg->n_layers;
     h->has_out_proj = cfg->feat_out > 0 && cfg->feat_out != h->d;
     h->dout = h->has_out_proj ? cfg->feat_out : h->d;
+    if (h->dout % 4) fail(CFM_ERR_UNSUPPORTED, "feat_out must be a multiple of 4");
     if (h->dff % 8) fail(CFM_ERR_UNSUPPORTED, "d_ff must be a multiple of 8");
     int prev = 0;
     HIP_OK(hipGetDevice(&prev));
@@ -732,7 +739,7 @@ cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w,
     if (K % (16 / es)) fail(CFM_ERR_UNSUPPORTED, "K must be a multiple of 16 bytes");
     if (pack_ws_bytes && *pack_ws_bytes < need) fail(CFM_ERR_WORKSPACE, "pack workspace too small");
     hipStream_t st = (hipStream_t)stream;
-    std::vector<float> hw((size_t)N * K), hb(N, 0.0f);
+    std::vector<float> hw((size_t)N * K), hb(Np, 0.0f);
     HIP_OK(hipMemcpy(hw.data(), w, hw.size() * 4, hipMemcpyDeviceToHost));
     if (bias) HIP_OK(hipMemcpy(hb.data(), bias, N * 4, hipMemcpyDeviceToHost));
     std::vector<char> packed((size_t)(Np * Kp * es), 0);
@@ -746,7 +753,7 @@ cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w,
     char* bdev = base + Np * Kp * es;
     char* zero = bdev + round_up(Np * 4, 256);
     HIP_OK(hipMemcpy(base, packed.data(), packed.size(), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(bdev, hb.data(), N * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(bdev, hb.data(), Np * 4, hipMemcpyHostToDevice));
     HIP_OK(hipMemset(zero, 0, 4096));
     GemmEpi e = epi_of(act == 1 ? EPI_RELU : act == 2 ? EPI_SWISH : EPI_STORE, (const float*)bdev);
     e.C = y;

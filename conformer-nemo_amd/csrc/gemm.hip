@@ -130,55 +130,43 @@ struct GemmParams {
 };
 
 // ---- epilogue: LDS image -> global, 16-byte vectors -------------------------------------------
+// Every global load here is unconditional (clamped address, value selected afterwards): a load
+// under a per-thread condition is branched around by hipcc and serialised behind its own
+// vmcnt(0) (cdna_hip_programming.md §5, 'Three .s-level traps' (c)).
 template <typename T, int EPI, class TL>
 CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
   const GemmEpi& e = p.epi;
   const int tid = threadIdx.x;
   if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
-    // fp32 output, 4 columns per thread-chunk
+    // fp32 output (N % 4 == 0), 4 columns per thread-chunk
     constexpr int CPR = TL::BN / 4;                 // chunks per row
     constexpr int RPP = TL::NT / CPR;               // rows per pass
     constexpr int NP = TL::BM / RPP;
     const int cc = tid % CPR, r0 = tid / CPR;
     const int n = n0 + cc * 4;
-    float4 bias = make_float4(0, 0, 0, 0);
+    const int nc = min(n, p.N - 4);
     const bool colok = n < p.N;
-    const bool full = n + 4 <= p.N;                 // partial chunk only if N % 4 != 0 (feat_out)
-    if (colok && e.bias) bias = full ? *(const float4*)(e.bias + n)
-                                     : make_float4(e.bias[n], n + 1 < p.N ? e.bias[n + 1] : 0.f,
-                                                   n + 2 < p.N ? e.bias[n + 2] : 0.f, 0.f);
     float4 xv[NP];
     if constexpr (EPI == EPI_RESID) {
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
-        const int m = m0 + r0 + q * RPP;
-        xv[q] = (full && m < p.M) ? *(const float4*)(e.X + (long)m * e.ldx + n) : make_float4(0, 0, 0, 0);
-        if (!full && colok && m < p.M) {
-          const float* xp = e.X + (long)m * e.ldx + n;
-          xv[q].x = xp[0]; if (n + 1 < p.N) xv[q].y = xp[1]; if (n + 2 < p.N) xv[q].z = xp[2];
-        }
+        const int m = min(m0 + r0 + q * RPP, p.M - 1);
+        xv[q] = *(const float4*)(e.X + (long)m * e.ldx + nc);
       }
     }
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
-      if (!colok || m >= p.M) continue;
       const float4 a = *(const float4*)(img + r * TL::EPS + cc * 4);
       float4 o;
       if constexpr (EPI == EPI_RESID) {
-        o.x = xv[q].x + (a.x + bias.x) * e.alpha; o.y = xv[q].y + (a.y + bias.y) * e.alpha;
-        o.z = xv[q].z + (a.z + bias.z) * e.alpha; o.w = xv[q].w + (a.w + bias.w) * e.alpha;
+        o.x = xv[q].x + a.x * e.alpha; o.y = xv[q].y + a.y * e.alpha;
+        o.z = xv[q].z + a.z * e.alpha; o.w = xv[q].w + a.w * e.alpha;
       } else {
-        o.x = (a.x + bias.x) * e.alpha; o.y = (a.y + bias.y) * e.alpha;
-        o.z = (a.z + bias.z) * e.alpha; o.w = (a.w + bias.w) * e.alpha;
+        o.x = a.x * e.alpha; o.y = a.y * e.alpha; o.z = a.z * e.alpha; o.w = a.w * e.alpha;
       }
-      float* xo = e.X + (long)m * e.ldx + n;
-      if (full) {
-        *(float4*)xo = o;
-      } else {
-        xo[0] = o.x; if (n + 1 < p.N) xo[1] = o.y; if (n + 2 < p.N) xo[2] = o.z;
-      }
+      if (colok && m < p.M) *(float4*)(e.X + (long)m * e.ldx + n) = o;
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
     // packed columns: per 64-column group g, [0,32) = value channels 32g.., [32,64) = gates
@@ -191,23 +179,23 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
     const int grp = oc_local / 32, j = oc_local % 32;
     const int ca = grp * 64 + j, cg = grp * 64 + 32 + j;   // packed columns within the tile
     const int c = n0 / 2 + oc_local;                 // output channel
-    float ba[VE], bg[VE];
+    int lenq[NP];
 #pragma unroll
-    for (int i = 0; i < VE; ++i) { ba[i] = e.bias[n0 + ca + i]; bg[i] = e.bias[n0 + cg + i]; }
+    for (int q = 0; q < NP; ++q) lenq[q] = e.lens[min(m0 + r0 + q * RPP, p.M - 1) / e.Tp];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
-      if (m >= p.M || c >= p.N) continue;
-      const int b = m / e.Tp, t = m - b * e.Tp;
-      const bool masked = t >= e.lens[b];
+      const int t = m % e.Tp;
+      const bool masked = t >= lenq[q];
       float o[VE];
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
-        const float a = img[r * TL::EPS + ca + i] + ba[i];
-        const float g = img[r * TL::EPS + cg + i] + bg[i];
+        const float a = img[r * TL::EPS + ca + i];
+        const float g = img[r * TL::EPS + cg + i];
         o[i] = masked ? 0.0f : a * sigmoidf_(g);
       }
+      if (m >= p.M || c >= p.N) continue;
       T* dst = (T*)e.C + (long)m * e.ldc + c;
       if (c + VE <= p.N) {
         *(uint4*)dst = Vec16<T>::from_f32(o);
@@ -224,45 +212,43 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
     const int cc = tid % CPR, r0 = tid / CPR;
     const int n = n0 + cc * VE;
     const int nlim = (EPI == EPI_QKV) ? e.qk_cols : p.N;
-    float bias[VE];
+    const bool vec = n + VE <= nlim && ((e.ldc * (long)sizeof(T)) % 16 == 0);
 #pragma unroll
-    for (int i = 0; i < VE; ++i) bias[i] = (e.bias && n + i < p.N) ? e.bias[n + i] : 0.0f;
-    if (n < nlim) {
+    for (int q = 0; q < NP; ++q) {
+      const int r = r0 + q * RPP;
+      const int m = m0 + r;
+      float o[VE];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const int r = r0 + q * RPP;
-        const int m = m0 + r;
-        if (m >= p.M) continue;
-        float o[VE];
-#pragma unroll
-        for (int i = 0; i < VE; ++i) {
-          float v = img[r * TL::EPS + cc * VE + i] + bias[i];
-          if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
-          if constexpr (EPI == EPI_SWISH) v = swishf(v);
-          o[i] = v;
-        }
-        T* dst = (T*)e.C + (long)m * e.ldc + n;
-        if (n + VE <= nlim && ((e.ldc * (long)sizeof(T)) % 16 == 0)) {
-          *(uint4*)dst = Vec16<T>::from_f32(o);
-        } else {
-          for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
-        }
+      for (int i = 0; i < VE; ++i) {
+        float v = img[r * TL::EPS + cc * VE + i];
+        if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
+        if constexpr (EPI == EPI_SWISH) v = swishf(v);
+        o[i] = v;
+      }
+      if (m >= p.M || n >= nlim) continue;
+      T* dst = (T*)e.C + (long)m * e.ldc + n;
+      if (vec) {
+        *(uint4*)dst = Vec16<T>::from_f32(o);
+      } else {
+        for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
       }
     }
     if constexpr (EPI == EPI_QKV) {
       // V columns -> Vt[(b*H + h)][dd][t]: lanes walk rows (time) so stores are contiguous in t
       if (n0 + TL::BN > e.qk_cols) {
         const int c_lo = (e.qk_cols > n0 ? e.qk_cols - n0 : 0);
-        for (int idx = tid; idx < TL::BM * TL::BN; idx += TL::NT) {
-          const int r = idx % TL::BM, cl = idx / TL::BM;
-          if (cl < c_lo) continue;
-          const int m = m0 + r, nn = n0 + cl;
+        constexpr int CPP = TL::NT / TL::BM;         // columns per pass
+        const int r = tid % TL::BM;
+        const int m = m0 + r;
+        const int mc = min(m, p.M - 1);
+        const int b = mc / e.Tp, t = mc - b * e.Tp;
+        for (int cl = c_lo + tid / TL::BM; cl < TL::BN; cl += CPP) {
+          const int nn = n0 + cl;
+          const float v = img[r * TL::EPS + cl];
           if (m >= p.M || nn >= p.N) continue;
           const int nv = nn - e.qk_cols;
           const int h = nv / e.dkp, dd = nv - h * e.dkp;
-          const int b = m / e.Tp, t = m - b * e.Tp;
-          st_f<T>((T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t,
-                  img[r * TL::EPS + cl] + e.bias[nn]);
+          st_f<T>((T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t, v);
         }
       }
     }
@@ -356,6 +342,13 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   raw_barrier();                         // every wave is done reading the ring
   float* img = (float*)smem;
   const int col = lane & 31;
+  float bcol[TL::NR];                    // bias arrays are zero-padded to the N granule (GEMM_BN)
+#pragma unroll
+  for (int j = 0; j < TL::NR; ++j) bcol[j] = 0.0f;
+  if (p.epi.bias) {
+#pragma unroll
+    for (int j = 0; j < TL::NR; ++j) bcol[j] = p.epi.bias[n0 + wn * (TL::BN / TL::WN) + j * 32 + col];
+  }
 #pragma unroll
   for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
@@ -364,7 +357,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int rl = wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane);
-        img[rl * TL::EPS + cl] = acc[i][j][rr];
+        img[rl * TL::EPS + cl] = acc[i][j][rr] + bcol[j];
       }
     }
   __syncthreads();

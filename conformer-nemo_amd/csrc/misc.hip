@@ -86,7 +86,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int e = 0; e < E4; ++e) {
     const int g = lane + 64 * e;
-    v[e] = (g < d4) ? xr[g] : make_float4(0, 0, 0, 0);
+    const float4 t = xr[min(g, d4 - 1)];            // unconditional (clamped) load, then select
+    v[e] = (g < d4) ? t : make_float4(0, 0, 0, 0);
     s += v[e].x + v[e].y + v[e].z + v[e].w;
   }
   const float inv_d = 1.0f / (float)d;
@@ -106,8 +107,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < E4; ++e) {
       const int g = lane + 64 * e;
+      const float4 wv = ((const float4*)ww)[min(g, d4 - 1)], bv = ((const float4*)bbp)[min(g, d4 - 1)];
       if (g < d4) {
-        const float4 wv = ((const float4*)ww)[g], bv = ((const float4*)bbp)[g];
         v[e].x = (v[e].x - mean) * rstd * wv.x + bv.x;
         v[e].y = (v[e].y - mean) * rstd * wv.y + bv.y;
         v[e].z = (v[e].z - mean) * rstd * wv.z + bv.z;
@@ -137,8 +138,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
           for (int i = 0; i < 4; ++i) f[i] = swishf(f[i]);
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st_f<T>(o + 4 * g + i, f[i]);
+        if constexpr (sizeof(T) == 2) {
+          *(uint2*)(o + 4 * g) = make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                                            (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
+        } else {
+          *(float4*)(o + 4 * g) = make_float4(f[0], f[1], f[2], f[3]);
+        }
       }
     }
   }
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const T* __restrict__ g, in
     if (t >= 0 && t < Tp && c < d) v = ld_f<T>(g + ((long)b * Tp + t) * d + c);
     xs[r][tx] = v;
   }
-  for (int k = ty; k < K; k += 4) ws[k][tx] = (c < d) ? w[(long)c * K + k] : 0.0f;
+  for (int k = ty; k < K; k += 4) ws[k][tx] = (c < d) ? w[(long)k * d + c] : 0.0f;   // w packed [K][d]
   __syncthreads();
   if (c >= d) return;
   const float bi = bias[c];
@@ -187,6 +192,53 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const T* __restrict__ g, in
     } else {
       const float y = (a - mu) * inv * gw + gb;
       st_f<T>(out + o, swishf(y));
+    }
+  }
+}
+
+// Register-window variant for a compile-time kernel size K (31 in every reference config):
+// thread = one channel x DT consecutive frames; its DT + K - 1 input frames are loaded straight from
+// global (lanes = consecutive channels -> coalesced rows) into registers, weights ([K][d] packed)
+// likewise, and the DT x K products run on fully static register indices.
+template <typename T, int K, int DT>
+__global__ __launch_bounds__(256) void dwconv_reg_kernel(const T* __restrict__ g, int Tp, int d,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         const float* __restrict__ bn_mean,
+                                                         const float* __restrict__ bn_inv,
+                                                         const float* __restrict__ bn_w,
+                                                         const float* __restrict__ bn_b, T* __restrict__ out,
+                                                         float* __restrict__ prenorm) {
+  constexpr int PAD = (K - 1) / 2, NX = DT + K - 1;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  const int b = blockIdx.z, t0 = blockIdx.x * DT;
+  if (c >= d) return;
+  const T* gc = g + (long)b * Tp * d + c;
+  float x[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int t = t0 - PAD + i;
+    // unconditional load of a clamped frame, zeroed after: a load under a per-element condition
+    // would be branched around and serialised behind its own vmcnt(0)
+    const float v = ld_f<T>(gc + (long)min(max(t, 0), Tp - 1) * d);
+    x[i] = (t >= 0 && t < Tp) ? v : 0.0f;
+  }
+  float wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[(long)k * d + c];
+  const float bi = bias[c];
+  float mu = 0.f, inv = 1.f, gw = 1.f, gb = 0.f;
+  if (!prenorm) { mu = bn_mean[c]; inv = bn_inv[c]; gw = bn_w[c]; gb = bn_b[c]; }
+  T* oc = out + (long)b * Tp * d + c;
+#pragma unroll
+  for (int j = 0; j < DT; ++j) {
+    float a = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) a = fmaf(wk[k], x[j + k], a);
+    a += bi;
+    const int t = t0 + j;
+    if (t < Tp) {
+      if (prenorm) prenorm[((long)b * Tp + t) * d + c] = a;
+      else st_f<T>(oc + (long)t * d, swishf((a - mu) * inv * gw + gb));
     }
   }
 }
@@ -257,6 +309,17 @@ void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, co
                        const float* bn_mean, const float* bn_inv, const float* bn_w, const float* bn_b, void* out_t,
                        float* out_prenorm_f32, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
+  if (K == 31) {
+    constexpr int DT = 32;
+    const dim3 grid((Tp + DT - 1) / DT, (d + 255) / 256, B), block(256);
+    if (dtype == DT_F32)
+      hipLaunchKernelGGL((dwconv_reg_kernel<float, 31, DT>), grid, block, 0, st, (const float*)g, Tp, d, w, bias,
+                         bn_mean, bn_inv, bn_w, bn_b, (float*)out_t, out_prenorm_f32);
+    else
+      hipLaunchKernelGGL((dwconv_reg_kernel<bf16_t, 31, DT>), grid, block, 0, st, (const bf16_t*)g, Tp, d, w, bias,
+                         bn_mean, bn_inv, bn_w, bn_b, (bf16_t*)out_t, out_prenorm_f32);
+    return;
+  }
   const dim3 grid((Tp + 31) / 32, (d + 63) / 64, B), block(256);
   if (dtype == DT_F32)
     hipLaunchKernelGGL(dwconv_kernel<float>, grid, block, 0, st, (const float*)g, Tp, d, K, w, bias, bn_mean, bn_inv,
