@@ -21,9 +21,9 @@ STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "UNSUPPORTED", 3: "HIP", 4: "WORKS
 EXPORTED_SYMBOLS = (
     "cfm_last_error", "cfm_version", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
-    "cfm_encoder_set_max_audio_length", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
+    "cfm_encoder_set_max_audio_length", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
     "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
-    "cfm_op_rel_attention",
+    "cfm_op_rel_attention", "cfm_bench_gemm",
 )
 
 
@@ -69,6 +69,7 @@ def load() -> ctypes.CDLL:
         "cfm_encoder_param_numel": (ctypes.c_int64, [vp, ci]),
         "cfm_encoder_set_max_audio_length": (ci, [vp, ci]),
         "cfm_encoder_max_audio_length": (ci, [vp]),
+        "cfm_encoder_set_microbatches": (ci, [vp, ci]),
         "cfm_encoder_workspace_size": (sz, [vp, ci, ci]),
         "cfm_encoder_forward": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp]),
         "cfm_num_stages": (ci, []),
@@ -78,6 +79,7 @@ def load() -> ctypes.CDLL:
         "cfm_op_layernorm": (ci, [ci, vp, ci, ci, vp, vp, vp, vp, vp]),
         "cfm_op_linear": (ci, [ci, vp, ci, ci, vp, vp, ci, ci, vp, vp, ctypes.POINTER(sz), vp]),
         "cfm_op_rel_attention_ws_size": (sz, [ci, ci, ci, ci, ci]),
+        "cfm_bench_gemm": (ci, [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(ctypes.c_float)]),
         "cfm_op_rel_attention": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():

@@ -105,6 +105,10 @@ class NativeEncoder:
     def set_max_audio_length(self, n: int) -> None:
         _lib.check(self.lib.cfm_encoder_set_max_audio_length(self.handle, int(n)), "set_max_audio_length")
 
+    def set_microbatches(self, n: int) -> None:
+        """Split each forward's batch over up to n concurrent streams (bitwise-identical results)."""
+        _lib.check(self.lib.cfm_encoder_set_microbatches(self.handle, int(n)), "set_microbatches")
+
     def workspace_size(self, B: int, T: int) -> int:
         return int(self.lib.cfm_encoder_workspace_size(self.handle, int(B), int(T)))
 

@@ -18,22 +18,25 @@
 // Masking (SURVEY §7 hard part 2): a query row with >= 1 valid key gets exactly the reference's
 // probabilities (the -10000-filled entries underflow to 0 in fp32); rows i >= len are fully masked
 // in the reference, whose probabilities are then zeroed (:107) -> their output is exactly 0.
+#include <cstdlib>
+
 #include "cfm_common.h"
 #include "cfm_kernels.h"
+
+#define CFM_DEV_HOST_INLINE __host__ __device__ inline
 
 namespace cfm {
 
 namespace {
 
 struct AttnParams {
-  const char* qk; long ldqk;      // elements; Q at col h*dkp, K at col H*dkp + h*dkp
+  const char* qk; long ldqk;      // [q+u | q+v | k], each H*dkp columns (EPI_QKV epilogue)
   const char* Vt; int vt_rows; int Tpad;
   const char* P; long ldp;        // P for head h at col h*dkp, rows 0 .. 2T'-2
-  const float* pos_u; const float* pos_v;
   const int32_t* lens;
   int Tp, H, dk, dkp;
   int ctx_left, ctx_right;
-  float s_dk;
+  // (q + u), (q + v) arrive pre-scaled by log2(e)/sqrt(dk): scores are in log2 units
   char* out; long ldo;
 };
 
@@ -57,7 +60,7 @@ CFM_DEV void load_tile(TileRegs<T, NS, ND>& t, const AttnParams& p, const T* qk,
   const int hsel = lane >> 5, col = lane & 31;
   const int Tp = p.Tp;
   const int j = min(j0 + col, Tp - 1);
-  const T* krow = qk + (rowbase + j) * p.ldqk + (long)(p.H + (int)blockIdx.y) * p.dkp;
+  const T* krow = qk + (rowbase + j) * p.ldqk + (long)(2 * p.H + (int)blockIdx.y) * p.dkp;
   const int pr0 = Tp - 1 - (i0 + 31) + j0;
   const int ra = min(max(pr0 + col, 0), 2 * Tp - 2);
   const int rb = min(max(pr0 + 32 + col, 0), 2 * Tp - 2);
@@ -108,6 +111,76 @@ template <int ND> struct PV<float, ND> {
   }
 };
 
+// ---- shared per-tile pieces ------------------------------------------------------------------
+constexpr float RESCALE_THR = 8.0f;   // log2 units: P entries may reach 2^8 before O is rescaled (T13)
+
+// Scores of this lane's query against its 16 keys of the tile: s = ac + bd (already in log2 units,
+// Q was pre-scaled by log2(e)/sqrt(dk)); masked keys -> -inf.  Masking runs only on tiles that
+// need it (uniform branch).
+CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, int j0, int len, int iq, int lane) {
+  const int col = lane & 31;
+  const bool need_mask = (j0 + 32 > len) || p.ctx_left >= 0 || p.ctx_right >= 0;
+  float mloc = -INFINITY;
+  if (!need_mask) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = acc_row(r, lane);
+      st[r] += bd_s[(jj - col + 31) * BDS + col];
+      mloc = fmaxf(mloc, st[r]);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = acc_row(r, lane);
+      const int jg = j0 + jj;
+      const float sc = st[r] + bd_s[(jj - col + 31) * BDS + col];
+      bool masked = jg >= len;
+      if (p.ctx_left >= 0) masked |= jg < iq - p.ctx_left;
+      if (p.ctx_right >= 0) masked |= jg > iq + p.ctx_right;
+      st[r] = masked ? -INFINITY : sc;
+      mloc = fmaxf(mloc, st[r]);
+    }
+  }
+  return fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+}
+
+// Online softmax with deferred rescale: the running max of a row is raised only when the tile max
+// exceeds it by more than RESCALE_THR (then O and l are rescaled, alpha broadcast through row_s);
+// otherwise probabilities are taken against the stale max (<= 2^THR, exact after the final 1/l).
+// Rows with no valid key so far (m = -inf) get p = exp2(-inf) = 0.
+template <int ND>
+CFM_DEV void softmax_tile(f32x16& st, float mloc, float& m_run, float& l_run, f32x16 (&o)[ND], float* row_s,
+                          int lane) {
+  const int hsel = lane >> 5, col = lane & 31;
+  const bool grow = mloc > m_run + RESCALE_THR;
+  if (__any(grow)) {
+    const float m_new = grow ? mloc : m_run;
+    // rows that did not grow keep alpha = 1 (also avoids (-inf) - (-inf)); 0 when m_run was -inf
+    const float alpha = grow ? __builtin_amdgcn_exp2f(m_run - m_new) : 1.0f;
+    l_run *= alpha;
+    m_run = m_new;
+    if (hsel == 0) row_s[col] = alpha;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float a = row_s[acc_row(r, lane)];
+#pragma unroll
+      for (int n = 0; n < ND; ++n) o[n][r] *= a;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  const float m_use = m_run == -INFINITY ? 0.0f : m_run;
+  float psum = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    st[r] = __builtin_amdgcn_exp2f(st[r] - m_use);
+    psum += st[r];
+  }
+  l_run += psum + __shfl_xor(psum, 32, 64);
+}
+
 template <typename T, int NS, int ND>
 __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
   constexpr int SE = 32 / (int)sizeof(T);
@@ -123,7 +196,7 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
   const long rowbase = (long)b * Tp;
   const T* vt_head = (const T*)p.Vt + ((long)b * p.H + h) * p.vt_rows * p.Tpad;
 
-  // Q fragments (B operand, lane = query) with the per-head biases: q + u (ac), q + v (bd)
+  // Q fragments (B operand, lane = query), already biased by the QKV epilogue: q + u (ac), q + v (bd)
   uint4 qu[NS], qv[NS];
   {
     const int i = min(i0 + col, Tp - 1);
@@ -131,20 +204,8 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int d0 = s * SE + hsel * (SE / 2);
-      const uint4 raw = *(const uint4*)(qrow + d0);
-      float f[SE / 2], fu[SE / 2], fv[SE / 2];
-      Vec16<T>::to_f32(raw, f);
-#pragma unroll
-      for (int e = 0; e < SE / 2; ++e) {
-        const int d = d0 + e;
-        const bool ok = d < p.dk;
-        const float bu = p.pos_u[h * p.dk + min(d, p.dk - 1)];   // unconditional loads
-        const float bv = p.pos_v[h * p.dk + min(d, p.dk - 1)];
-        fu[e] = ok ? f[e] + bu : 0.0f;
-        fv[e] = ok ? f[e] + bv : 0.0f;
-      }
-      qu[s] = Vec16<T>::from_f32(fu);
-      qv[s] = Vec16<T>::from_f32(fv);
+      qu[s] = *(const uint4*)(qrow + d0);
+      qv[s] = *(const uint4*)(qrow + (long)p.H * p.dkp + d0);
     }
   }
 
@@ -186,41 +247,9 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
     }
     __syncthreads();
 
-    // scores for this lane's query and its 16 keys
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int jj = acc_row(r, lane);          // key within the tile
-      const int jg = j0 + jj;
-      float s = (st[r] + bd_s[(jj - col + 31) * BDS + col]) / p.s_dk;
-      bool masked = jg >= len;
-      if (p.ctx_left >= 0) masked |= jg < iq - p.ctx_left;
-      if (p.ctx_right >= 0) masked |= jg > iq + p.ctx_right;
-      st[r] = masked ? -INFINITY : s;
-      mloc = fmaxf(mloc, st[r]);
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float m_new = fmaxf(m_run, mloc);
-    float alpha = 1.0f, psum = 0.0f;
-    if (m_new == -INFINITY) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[r] = 0.0f;
-    } else {
-      alpha = __expf(m_run - m_new);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { st[r] = __expf(st[r] - m_new); psum += st[r]; }
-    }
-    psum += __shfl_xor(psum, 32, 64);
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-    if (hsel == 0) row_s[col] = alpha;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float a = row_s[acc_row(r, lane)];
-#pragma unroll
-      for (int n = 0; n < ND; ++n) o[n][r] *= a;
-    }
+    // scores for this lane's query and its 16 keys, then the online softmax
+    const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane);
+    softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
     if (j0 + 32 > Tp) {   // keys >= T' read Vt padding (unspecified): force those V entries to 0
 #pragma unroll
       for (int n = 0; n < ND; ++n)
@@ -268,6 +297,220 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-resident variant (bf16): one block per (b, h) with NW waves; K and Vt of the utterance-head
+// are copied into LDS once (zero-filled beyond T'), every wave walks its 32-query tiles reading K/V
+// fragments from LDS (conflict-free strides: K rows padded by 16 B, Vt rows by 8 B) while the
+// P window is streamed from L2 one key tile ahead.  Same arithmetic as rel_attn_kernel.
+// ---------------------------------------------------------------------------------------------
+struct LdsGeom {
+  int tp32, ks, vs;           // keys rounded to 32, K row stride (bytes), Vt row stride (bytes)
+  int k_off, v_off, bd_off, bytes;
+};
+
+CFM_DEV_HOST_INLINE LdsGeom lds_geom(int Tp, int dkp, int vt_rows, int nw) {
+  LdsGeom g;
+  g.tp32 = (Tp + 31) / 32 * 32;
+  g.ks = dkp * 2 + 16;
+  g.vs = g.tp32 * 2 + 8;
+  g.k_off = 0;
+  g.v_off = g.tp32 * g.ks;
+  g.bd_off = g.v_off + vt_rows * g.vs;
+  g.bd_off = (g.bd_off + 15) / 16 * 16;
+  g.bytes = g.bd_off + nw * (64 * BDS * 4 + 32 * 4);
+  return g;
+}
+
+template <int NS, int ND, int NW>
+__global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
+  using T = bf16_t;
+  constexpr int SE = 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hsel = lane >> 5, col = lane & 31;
+  const int bh = blockIdx.x;
+  const int b = bh / p.H, h = bh - b * p.H;
+  const int Tp = p.Tp;
+  const int len = min(p.lens[b], Tp);
+  const LdsGeom g = lds_geom(Tp, p.dkp, p.vt_rows, NW);
+  const T* qk = (const T*)p.qk;
+  const long rowbase = (long)b * Tp;
+  char* Ks = smem + g.k_off;
+  char* Vs = smem + g.v_off;
+  float* bd_s = (float*)(smem + g.bd_off + wave * (64 * BDS * 4 + 32 * 4));
+  float* row_s = bd_s + 64 * BDS;
+
+  // ---- stage K [tp32][dkp] and Vt [vt_rows][tp32] of this (b, h) into LDS (zeros past T') ----
+  // Loads are issued in batches of BATCH (all in flight) before their LDS writes: a load->write
+  // loop body would otherwise expose one full HBM latency per iteration.
+  {
+    constexpr int BATCH = 8;
+    const int kchunks = p.dkp / 8;                          // 16-byte chunks per K row
+    const int kn = g.tp32 * kchunks;
+    const T* kbase = qk + rowbase * p.ldqk + (long)(2 * p.H + h) * p.dkp;
+    for (int i0 = tid; i0 < kn; i0 += NW * 64 * BATCH) {
+      uint4 v[BATCH];
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int i = min(i0 + u * NW * 64, kn - 1);
+        const int r = i / kchunks, c = i - r * kchunks;
+        v[u] = *(const uint4*)(kbase + (long)min(r, Tp - 1) * p.ldqk + c * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int i = i0 + u * NW * 64;
+        const int r = i / kchunks, c = i - r * kchunks;
+        if (i < kn) *(uint4*)(Ks + r * g.ks + c * 16) = r < Tp ? v[u] : make_uint4(0, 0, 0, 0);
+      }
+    }
+    const T* vt_head = (const T*)p.Vt + ((long)b * p.H + h) * p.vt_rows * p.Tpad;
+    const int vchunks = g.tp32 / 4;                         // 8-byte chunks (4 keys) per Vt row
+    const int vn = p.vt_rows * vchunks;
+    for (int i0 = tid; i0 < vn; i0 += NW * 64 * BATCH) {
+      uint2 v[BATCH];
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int i = min(i0 + u * NW * 64, vn - 1);
+        const int r = i / vchunks, c = i - r * vchunks;
+        v[u] = *(const uint2*)(vt_head + (long)r * p.Tpad + c * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; ++u) {
+        const int i = i0 + u * NW * 64;
+        const int r = i / vchunks, c = i - r * vchunks;
+        const int k0 = c * 4;
+        uint2 w = v[u];
+        if (k0 + 0 >= Tp) w.x &= 0xffff0000u;
+        if (k0 + 1 >= Tp) w.x &= 0x0000ffffu;
+        if (k0 + 2 >= Tp) w.y &= 0xffff0000u;
+        if (k0 + 3 >= Tp) w.y &= 0x0000ffffu;
+        if (i < vn) *(uint2*)(Vs + r * g.vs + c * 8) = w;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int nqt = (Tp + 31) / 32;
+  for (int qt = wave; qt < nqt; qt += NW) {
+    const int i0 = qt * 32;
+    uint4 qu[NS], qv[NS];
+    {
+      const int i = min(i0 + col, Tp - 1);
+      const T* qrow = qk + (rowbase + i) * p.ldqk + (long)h * p.dkp;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int d0 = s * SE + hsel * (SE / 2);
+        qu[s] = *(const uint4*)(qrow + d0);
+        qv[s] = *(const uint4*)(qrow + (long)p.H * p.dkp + d0);
+      }
+    }
+    f32x16 o[ND];
+#pragma unroll
+    for (int n = 0; n < ND; ++n) o[n] = f32x16{};
+    float m_run = -INFINITY, l_run = 0.0f;
+    const int iq = i0 + col;
+    int jbeg = 0, jend = len;
+    if (p.ctx_left >= 0) jbeg = max(0, (i0 - p.ctx_left) & ~31);
+    if (p.ctx_right >= 0) jend = min(jend, i0 + 31 + p.ctx_right + 1);
+
+    auto load_p = [&](int j0, uint4 (&pa)[NS], uint4 (&pb)[NS]) {
+      const int pr0 = Tp - 1 - (i0 + 31) + j0;
+      const int ra = min(max(pr0 + col, 0), 2 * Tp - 2);
+      const int rb = min(max(pr0 + 32 + col, 0), 2 * Tp - 2);
+      const T* prowa = (const T*)p.P + (long)ra * p.ldp + (long)h * p.dkp;
+      const T* prowb = (const T*)p.P + (long)rb * p.ldp + (long)h * p.dkp;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int d0 = s * SE + hsel * (SE / 2);
+        pa[s] = *(const uint4*)(prowa + d0);
+        pb[s] = *(const uint4*)(prowb + d0);
+      }
+    };
+    uint4 pa[NS], pb[NS], na[NS], nb[NS];
+    if (jbeg < jend) load_p(jbeg, pa, pb);
+    for (int j0 = jbeg; j0 < jend; j0 += 32) {
+      const bool more = j0 + 32 < jend;
+      if (more) load_p(j0 + 32, na, nb);
+      f32x16 st = f32x16{}, bd0 = f32x16{}, bd1 = f32x16{};
+      const char* krow = Ks + (j0 + col) * g.ks + hsel * 16;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint4 kf = *(const uint4*)(krow + s * 32);
+        mfma_slab<T>(st, kf, qu[s]);
+        mfma_slab<T>(bd0, pa[s], qv[s]);
+        mfma_slab<T>(bd1, pb[s], qv[s]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = acc_row(r, lane);
+        bd_s[rr * BDS + col] = bd0[r];
+        bd_s[(rr + 32) * BDS + col] = bd1[r];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
+      __builtin_amdgcn_wave_barrier();
+      const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane);
+      softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
+      uint2 v[ND][4];
+#pragma unroll
+      for (int n = 0; n < ND; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[n][q] = *(const uint2*)(Vs + (n * 32 + col) * g.vs + (j0 + 8 * q + 4 * hsel) * 2);
+      PV<T, ND>::run(o, st, v);
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // bd_s / row_s reads done before the next tile rewrites them
+      __builtin_amdgcn_wave_barrier();
+      if (more) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) { pa[s] = na[s]; pb[s] = nb[s]; }
+      }
+    }
+    if (hsel == 0) row_s[col] = l_run;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    T* out = (T*)p.out;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, lane);
+      const int ig = i0 + i;
+      const float l = row_s[i];
+      const bool valid = ig < len && l > 0.0f;
+      const float inv = valid ? 1.0f / l : 0.0f;
+      if (ig >= Tp) continue;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int d = n * 32 + col;
+        if (d < p.dk) st_f<T>(out + (rowbase + ig) * p.ldo + (long)h * p.dk + d, valid ? o[n][r] * inv : 0.0f);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// launches the LDS-resident kernel if its image fits; returns false otherwise
+template <int NS>
+bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
+  constexpr int DKP = NS * 16;
+  constexpr int ND = (DKP + 31) / 32;
+  const int nqt = (p.Tp + 31) / 32;
+  const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
+  const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
+  constexpr int LDS_MAX = 160 * 1024;
+  static bool attr_set = [] {
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LDS_MAX);
+    return true;
+  }();
+  (void)attr_set;
+  (void)nqt;
+  (void)g8;
+  if (g4.bytes <= LDS_MAX) {
+    hipLaunchKernelGGL((rel_attn_lds_kernel<NS, ND, 4>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
+    return true;
+  }
+  return false;
+}
+
 template <typename T, int NS>
 void launch_nd(const AttnParams& p, dim3 grid, hipStream_t st) {
   constexpr int es = sizeof(T);
@@ -304,21 +547,36 @@ void launch_t(const AttnParams& p, dim3 grid, hipStream_t st) {
 }  // namespace
 
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
-                       long ldp, const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
+                       long ldp, const int32_t* lens, int B, int Tp, int H,
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
   AttnParams p;
   p.qk = (const char*)qk; p.ldqk = ldqk;
   p.Vt = (const char*)Vt; p.vt_rows = vt_rows; p.Tpad = Tpad;
   p.P = (const char*)P; p.ldp = ldp;
-  p.pos_u = pos_u; p.pos_v = pos_v; p.lens = lens;
+  p.lens = lens;
   p.Tp = Tp; p.H = H; p.dk = dk; p.dkp = dkp;
   p.ctx_left = ctx_left; p.ctx_right = ctx_right;
-  p.s_dk = (float)__builtin_sqrt((double)dk);
   p.out = (char*)out; p.ldo = ldo;
   const dim3 grid((Tp + 31) / 32, H, B);
-  if (dtype == DT_F32) launch_t<float>(p, grid, st);
-  else launch_t<bf16_t>(p, grid, st);
+  if (dtype == DT_F32) {
+    launch_t<float>(p, grid, st);
+    return;
+  }
+  static const bool lds_ok = [] { const char* s = getenv("CFM_ATTN_STREAM"); return !(s && atoi(s)); }();
+  if (lds_ok) {
+    bool done = false;
+    switch (dkp) {
+      case 16: done = launch_lds<1>(p, B, st); break;
+      case 32: done = launch_lds<2>(p, B, st); break;
+      case 48: done = launch_lds<3>(p, B, st); break;
+      case 64: done = launch_lds<4>(p, B, st); break;
+      case 128: done = launch_lds<8>(p, B, st); break;
+      default: break;
+    }
+    if (done) return;
+  }
+  launch_t<bf16_t>(p, grid, st);
 }
 
 }  // namespace cfm

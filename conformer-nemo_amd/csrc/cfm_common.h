@@ -84,8 +84,10 @@ CFM_DEV float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-CFM_DEV float swishf(float x) { return x / (1.0f + __expf(-x)); }
-CFM_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// x * sigmoid(x) and sigmoid(x) with v_exp_f32 + v_rcp_f32 (~1 ulp each) instead of an IEEE
+// divide sequence: the epilogues apply these to every output element.
+CFM_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+CFM_DEV float swishf(float x) { return x * sigmoidf_(x); }
 
 // Asynchronous 16-byte global -> LDS copy (global_load_lds_dwordx4). The LDS destination is the
 // wave-uniform `lds_base` + 16 * lane; the global source is per lane.

@@ -22,7 +22,7 @@ enum Epilogue {
   EPI_RESID = 3,       // X[m,n] (fp32) += alpha * (acc + bias)
   EPI_SCALE_F32 = 4,   // X[m,n] (fp32)  = (acc + bias) * alpha
   EPI_GLU_MASK = 5,    // C[m, c] = (a + ba) * sigmoid(g + bg), zero for padded frames (GLU-packed W)
-  EPI_QKV = 6,         // q,k parts -> C (ldc), v part -> Vt[(b*H + h)][d][t] transposed
+  EPI_QKV = 6,         // packed cols [q | k | v]: C = [q+u | q+v | k] (ldc = 3*H*dkp), v -> Vt[(b*H+h)][d][t]
 };
 
 struct GemmEpi {
@@ -33,7 +33,9 @@ struct GemmEpi {
   float* X; long ldx;  // fp32 residual / output
   const int32_t* lens; int Tp;          // pad mask (EPI_GLU_MASK) and row -> (b, t) for EPI_QKV
   void* Vt; int H; int dkp; int vt_rows; int Tpad;  // EPI_QKV: Vt [(B*H) * vt_rows][Tpad]
-  int qk_cols;         // EPI_QKV: columns < qk_cols go to C, the rest are V
+  int qk_cols;         // EPI_QKV: columns < qk_cols (= 2*H*dkp) are q and k, the rest are V
+  const float* uv;     // EPI_QKV: pos_bias_u then pos_bias_v, each [H][dkp] zero-padded
+  float qscale;        // EPI_QKV: (q + u), (q + v) are written pre-multiplied by log2(e) / sqrt(dk)
 };
 
 struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)
@@ -44,6 +46,8 @@ struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (
 // C = A[M,K] * Wp[N,K]^T with a fused epilogue. `K` = logical K (elements); A rows are `lda` elements.
 void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int Kpad, int N,
           const GemmEpi& epi, const void* zero_page, hipStream_t st);
+// -1 = automatic tile choice; otherwise 0:128x128 1:256x128 2:128x256 3:64x128. Returns the previous value.
+int set_gemm_tile_override(int tile);
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                const void* zero_page, hipStream_t st);
 
@@ -59,8 +63,10 @@ void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, co
                        const float* bn_mean, const float* bn_inv, const float* bn_w, const float* bn_b,
                        void* out_t, float* out_prenorm_f32, hipStream_t st);
 void transpose_out(const float* X, int B, int Tp, int d, float* y_bdt, hipStream_t st);
+// qk: [(q+u)*c | (q+v)*c | k] per row (ldqk = 3*H*dkp, c = log2(e)/sqrt(dk)), written by the EPI_QKV
+// GEMM epilogue; the softmax then runs in base 2 on unscaled score sums.
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
-                       long ldp, const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
+                       long ldp, const int32_t* lens, int B, int Tp, int H,
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/cfm_encoder.h"
+#include "cfm_common.h"
 #include "cfm_kernels.h"
 
 using namespace cfm;
@@ -69,7 +70,7 @@ int host_calc_length(int len, int repeat) {
 
 struct LayerW {
   long ff1_w1, ff1_b1, ff1_w2, ff1_b2, ff2_w1, ff2_b1, ff2_w2, ff2_b2;
-  long qkv_w, qkv_b, out_w, out_b, pos_u, pos_v;
+  long qkv_w, qkv_b, out_w, out_b, uv;   // uv: pos_bias_u | pos_bias_v, [H][dkp] each, zero-padded
   long pw1_w, pw1_b, dw_w, dw_b, bn_mean, bn_inv, bn_w, bn_b, pw2_w, pw2_b;
   long ln_w[5], ln_b[5];   // ff1, self_att, conv, ff2, out
 };
@@ -91,6 +92,10 @@ struct cfm_encoder {
   // relative positional table (compute type), rows = 2*max_len - 1
   char* pe = nullptr;
   int max_len = 0;
+  // micro-batch concurrency: the batch is split into `microbatches` parts run on their own streams
+  int microbatches = 2;
+  std::vector<hipStream_t> sub_streams;
+  std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
   void* zero_page = nullptr;
   std::vector<std::pair<std::string, int64_t>> params;
 
@@ -256,8 +261,12 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
     });
     Lw.out_w = mat_plain(p + "self_attn.linear_out.weight", d, d);
     Lw.out_b = pk.bias(get(p + "self_attn.linear_out.bias"), d);
-    Lw.pos_u = pk.f32(get(p + "self_attn.pos_bias_u"), (long)H * dk);
-    Lw.pos_v = pk.f32(get(p + "self_attn.pos_bias_v"), (long)H * dk);
+    const float* pu = get(p + "self_attn.pos_bias_u");
+    const float* pv = get(p + "self_attn.pos_bias_v");
+    Lw.uv = pk.f32(nullptr, 2L * H * dkp, [&](long i) -> float {
+      const int part = (int)(i / (H * dkp)), r = (int)(i % (H * dkp)), hh = r / dkp, dd = r % dkp;
+      return dd < dk ? (part ? pv : pu)[hh * dk + dd] : 0.0f;
+    });
     // pointwise_conv1 (2d, d, 1) GLU-packed: 64-col group g = [value 32g.. | gate d+32g..]
     const float* w1 = get(p + "conv.pointwise_conv1.weight");
     const float* b1 = get(p + "conv.pointwise_conv1.bias");
@@ -323,6 +332,19 @@ void build_pe(cfm_encoder* h, int max_len) {
   h->max_len = max_len;
 }
 
+void ensure_streams(cfm_encoder* h, int n) {
+  while ((int)h->sub_streams.size() < n) {
+    hipStream_t st;
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    h->sub_streams.push_back(st);
+  }
+  while ((int)h->sub_events.size() < n + 1) {
+    hipEvent_t ev;
+    HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    h->sub_events.push_back(ev);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // workspace layout
 // ---------------------------------------------------------------------------------------------
@@ -347,7 +369,7 @@ WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
   w.X = take(M * h->d * 4);
   w.Hn = take(M * h->d * es);
   w.U = take(M * h->dff * es);
-  w.QK = take(M * 2 * h->H * h->dkp * es);
+  w.QK = take(M * 3 * h->H * h->dkp * es);
   w.Vt = take((long)B * h->H * h->vt_rows * w.Tpad * es);
   w.O = take(M * h->d * es);
   w.G = take(M * h->d * es);
@@ -358,6 +380,11 @@ WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
   w.total = round_up(off, 256);
   return w;
 }
+
+// (q + u) and (q + v) are stored pre-scaled so that exp2(score) == exp(score_ref / sqrt(dk))
+float attn_qscale(int dk) { return (float)(1.4426950408889634 / std::sqrt((double)dk)); }
+
+size_t split_workspace(const cfm_encoder* h, int B, int T);
 
 GemmEpi epi_of(int mode, const float* bias, float alpha = 1.0f) {
   GemmEpi e;
@@ -422,6 +449,8 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     HIP_OK(hipMalloc(&h->zero_page, 4096));
     HIP_OK(hipMemset(h->zero_page, 0, 4096));
     build_pe(h.get(), std::max(cfg->pos_emb_max_len, 1));
+    if (const char* mb = getenv("CFM_MICROBATCH")) h->microbatches = std::max(1, std::min(8, atoi(mb)));
+    ensure_streams(h.get(), 8);
     HIP_OK(hipSetDevice(prev));
     *out = h.release();
   });
@@ -432,6 +461,8 @@ void cfm_encoder_destroy(cfm_encoder* h) {
   if (h->wbuf) (void)hipFree(h->wbuf);
   if (h->pe) (void)hipFree(h->pe);
   if (h->zero_page) (void)hipFree(h->zero_page);
+  for (auto st : h->sub_streams) (void)hipStreamDestroy(st);
+  for (auto ev : h->sub_events) (void)hipEventDestroy(ev);
   delete h;
 }
 
@@ -503,7 +534,7 @@ int cfm_encoder_max_audio_length(const cfm_encoder* h) { return h ? h->max_len :
 
 size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T) {
   if (!h || B <= 0 || T <= 0) return 0;
-  return (size_t)ws_layout(h, B, T).total;
+  return std::max(split_workspace(h, B, T), (size_t)ws_layout(h, B, T).total);
 }
 
 }  // extern "C"
@@ -541,8 +572,21 @@ struct StageTimer {
 };
 #define TM(id) do { if (tm) tm->mark(id); } while (0)
 
+void pos_gemm(cfm_encoder* h, int Tp, void* dst, hipStream_t st) {
+  // linear_pos of every layer at once on pos_emb = pe[center - T' : center + T' - 1]
+  // (batch-independent, multi_head_attention.py:187 + RelPositionalEncoding.forward :311-313)
+  const long ldp = (long)h->L * h->H * h->dkp;
+  GemmEpi e = epi_of(EPI_STORE, nullptr);
+  e.C = dst;
+  e.ldc = ldp;
+  const char* pe_slice = h->pe + (long)(h->max_len - Tp) * h->d * h->es;
+  gemm(h->dtype, pe_slice, h->d, 2 * Tp - 1, h->d, h->wbuf + h->pos_w, (int)h->kpad(h->d), (int)ldp, e, h->zero_page,
+       st);
+}
+
 void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
-                 int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream, StageTimer* tm) {
+                 int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream, StageTimer* tm,
+                 const char* P_ext = nullptr) {
   {
     if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
     if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
@@ -585,14 +629,10 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
            h->zero_page, st);
     }
     const long ldp = (long)L * H * dkp;
+    const char* Pbuf = P_ext ? P_ext : ws + wl.P;
     if (L > 0) {
       TM(ST_POS);
-      // linear_pos of every layer at once on pos_emb = pe[center - T' : center + T' - 1]
-      GemmEpi e = epi_of(EPI_STORE, nullptr);
-      e.C = ws + wl.P;
-      e.ldc = ldp;
-      const char* pe_slice = h->pe + (long)(h->max_len - Tp) * d * es;
-      gemm(dt, pe_slice, d, 2 * Tp - 1, d, W(h->pos_w), (int)h->kpad(d), (int)ldp, e, h->zero_page, st);
+      if (!P_ext) pos_gemm(h, Tp, ws + wl.P, st);
       TM(ST_LN);
       layernorm(dt, X, M, d, Wf(h->layers[0].ln_w[0]), Wf(h->layers[0].ln_b[0]), nullptr, nullptr, nullptr, Hn, 0, st);
     }
@@ -616,12 +656,13 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
       {
         TM(ST_QKV);
         GemmEpi e = epi_of(EPI_QKV, Wf(Lw.qkv_b));
-        e.C = ws + wl.QK; e.ldc = 2L * H * dkp; e.qk_cols = 2 * H * dkp;
+        e.C = ws + wl.QK; e.ldc = 3L * H * dkp; e.qk_cols = 2 * H * dkp; e.uv = Wf(Lw.uv);
+        e.qscale = attn_qscale(h->dk);
         e.Vt = ws + wl.Vt; e.H = H; e.dkp = dkp; e.vt_rows = h->vt_rows; e.Tpad = wl.Tpad; e.Tp = Tp;
         gemm(dt, Hn, d, M, d, W(Lw.qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
         TM(ST_ATTN);
-        rel_pos_attention(dt, ws + wl.QK, 2L * H * dkp, ws + wl.Vt, h->vt_rows, wl.Tpad,
-                          ws + wl.P + (long)l * H * dkp * es, ldp, Wf(Lw.pos_u), Wf(Lw.pos_v), lens, B, Tp, H, h->dk,
+        rel_pos_attention(dt, ws + wl.QK, 3L * H * dkp, ws + wl.Vt, h->vt_rows, wl.Tpad,
+                          Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk,
                           dkp, h->cfg.att_context_left, h->cfg.att_context_right, ws + wl.O, d, st);
         TM(ST_OUTPROJ);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.out_b), 1.0f);
@@ -688,6 +729,53 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
   }
 }
 
+int split_parts(const cfm_encoder* h, int B) { return std::max(1, std::min(h->microbatches, B / 4)); }
+
+// Micro-batch concurrency: utterances are independent (every row of every kernel is computed
+// the same way whatever its batch neighbours - tests/test_gpu_encoder.py checks bitwise batch
+// invariance), so the batch is split into parts that run on their own streams, forked from and
+// joined back into the caller's stream with events (graph-capture safe).  The per-launch latency
+// chain of one part's small GEMMs then overlaps another part's work.  The batch-independent
+// linear_pos GEMM runs once, before the fork.
+size_t split_workspace(const cfm_encoder* h, int B, int T) {
+  const int n = split_parts(h, B);
+  if (n == 1) return (size_t)ws_layout(h, B, T).total;
+  const int bmax = (B + n - 1) / n;
+  return (size_t)n * ws_layout(h, bmax, T).total;
+}
+
+void run_split(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
+               int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  const int n = split_parts(h, B);
+  if (n == 1) {
+    run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, stream, nullptr);
+    return;
+  }
+  if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+  if (T > h->max_len) fail(CFM_ERR_INVALID_ARG, "T exceeds max_audio_length; call cfm_encoder_set_max_audio_length");
+  if (!workspace || workspace_bytes < split_workspace(h, B, T)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+  ensure_streams(h, n);
+  const int bmax = (B + n - 1) / n;
+  const WsLayout wl = ws_layout(h, bmax, T);
+  char* ws = (char*)workspace;
+  const int Tp = wl.Tp;
+  const char* P = ws + wl.P;                       // part 0's P region holds the shared projection
+  if (h->L > 0) pos_gemm(h, Tp, ws + wl.P, stream);
+  HIP_OK(hipEventRecord(h->sub_events[0], stream));
+  int b0 = 0;
+  for (int i = 0; i < n; ++i) {
+    const int bi = B / n + (i < B % n ? 1 : 0);
+    hipStream_t si = h->sub_streams[i];
+    HIP_OK(hipStreamWaitEvent(si, h->sub_events[0], 0));
+    run_forward(h, x_bft + (long)b0 * h->F * T, len_b ? len_b + b0 : nullptr, bi, T,
+                y_bdt + (long)b0 * h->dout * Tp, out_len_b + b0, ws + (long)i * wl.total, wl.total, si, nullptr,
+                h->L > 0 ? P : nullptr);
+    HIP_OK(hipEventRecord(h->sub_events[1 + i], si));
+    HIP_OK(hipStreamWaitEvent(stream, h->sub_events[1 + i], 0));
+    b0 += bi;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -695,7 +783,16 @@ extern "C" {
 cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
                                int32_t* out_len_b, void* workspace, size_t workspace_bytes, void* stream) {
   return guarded([&] {
-    run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, nullptr);
+    if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
+    run_split(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream);
+  });
+}
+
+cfm_status cfm_encoder_set_microbatches(cfm_encoder* h, int n) {
+  return guarded([&] {
+    if (!h || n < 1 || n > 8) fail(CFM_ERR_INVALID_ARG, "microbatches must be in [1, 8]");
+    h->microbatches = n;
   });
 }
 
@@ -767,7 +864,7 @@ size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk) {
   const int es = dtype == CFM_COMPUTE_FP32 ? 4 : 2;
   const long dkp = round_up(dk, 16), vt_rows = round_up(dkp, 32), Tpad = round_up(Tp, 32);
   const long M = (long)B * Tp;
-  return (size_t)(round_up(M * 2 * H * dkp * es, 256) + round_up((long)B * H * vt_rows * Tpad * es, 256) +
+  return (size_t)(round_up(M * 3 * H * dkp * es, 256) + round_up((long)B * H * vt_rows * Tpad * es, 256) +
                   round_up((2L * Tp - 1) * H * dkp * es + 64, 256));
 }
 
@@ -777,12 +874,15 @@ size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk) {
 // directly from the QKV / pos GEMM epilogues)
 namespace {
 template <typename T>
-__global__ void pad_heads_kernel(const T* src, long rows, int H, int dk, int dkp, T* dst, long ldd) {
+__global__ void pad_heads_kernel(const T* src, long rows, int H, int dk, int dkp, T* dst, long ldd, const float* bias,
+                                 float scale) {
   const long n = rows * H * dkp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long r = i / (H * dkp);
     const int c = (int)(i % (H * dkp)), hh = c / dkp, dd = c % dkp;
-    dst[r * ldd + c] = dd < dk ? src[r * H * dk + hh * dk + dd] : (T)0;
+    float v = 0.0f;
+    if (dd < dk) v = (ld_f<T>(src + r * H * dk + hh * dk + dd) + (bias ? bias[hh * dk + dd] : 0.0f)) * scale;
+    st_f<T>(dst + r * ldd + c, v);
   }
 }
 template <typename T>
@@ -798,17 +898,23 @@ __global__ void vt_kernel(const T* v, int B, int Tp, int H, int dk, int vt_rows,
   }
 }
 template <typename T>
-void relayout(const void* q, const void* k, const void* v, const void* p, int B, int Tp, int H, int dk, int dkp,
-              int vt_rows, int Tpad, char* ws, long qk_bytes, long vt_bytes, hipStream_t st) {
+void relayout(const void* q, const void* k, const void* v, const void* p, const float* pos_u, const float* pos_v, int B,
+              int Tp, int H, int dk, int dkp, int vt_rows, int Tpad, char* ws, long qk_bytes, long vt_bytes,
+              hipStream_t st) {
   const long M = (long)B * Tp;
   T* QK = (T*)ws;
   T* Vt = (T*)(ws + qk_bytes);
   T* P = (T*)(ws + qk_bytes + vt_bytes);
   const dim3 g(1024), b(256);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK, 2L * H * dkp);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)k, M, H, dk, dkp, QK + (long)H * dkp, 2L * H * dkp);
+  const long ld = 3L * H * dkp;
+  const float qs = attn_qscale(dk);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK, ld, pos_u, qs);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK + (long)H * dkp, ld, pos_v, qs);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)k, M, H, dk, dkp, QK + 2L * H * dkp, ld,
+                     (const float*)nullptr, 1.0f);
   hipLaunchKernelGGL(vt_kernel<T>, g, b, 0, st, (const T*)v, B, Tp, H, dk, vt_rows, Tpad, Vt);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp);
+  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp,
+                     (const float*)nullptr, 1.0f);
 }
 }  // namespace
 
@@ -821,14 +927,75 @@ extern "C" cfm_status cfm_op_rel_attention(int dtype, const void* q, const void*
     const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
     const int dkp = (int)round_up(dk, 16), vt_rows = (int)round_up(dkp, 32), Tpad = (int)round_up(Tp, 32);
     const long M = (long)B * Tp;
-    const long qk_bytes = round_up(M * 2 * H * dkp * es, 256);
+    const long qk_bytes = round_up(M * 3 * H * dkp * es, 256);
     const long vt_bytes = round_up((long)B * H * vt_rows * Tpad * es, 256);
     hipStream_t st = (hipStream_t)stream;
-    if (dt == DT_F32) relayout<float>(q, k, v, p, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
-    else relayout<uint16_t>(q, k, v, p, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
+    if (dt == DT_F32)
+      relayout<float>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
+    else
+      relayout<bf16_t>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
     char* w = (char*)ws;
-    rel_pos_attention(dt, w, 2L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes, (long)H * dkp, pos_u,
-                      pos_v, lens, B, Tp, H, dk, dkp, ctx_left, ctx_right, out, (long)H * dk, st);
+    rel_pos_attention(dt, w, 3L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes, (long)H * dkp, lens,
+                      B, Tp, H, dk, dkp, ctx_left, ctx_right, out, (long)H * dk, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+// ---- GEMM microbenchmark (tools/gemm_bench.py) ----------------------------------------------
+namespace {
+__global__ void fill_rand_kernel(uint16_t* p, long n, uint32_t seed, int as_f32) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    const float f = ((x & 0xffffff) / 16777216.0f) * 2.0f - 1.0f;
+    if (as_f32) ((float*)p)[i] = f;
+    else { uint32_t u = __float_as_uint(f); p[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16); }
+  }
+}
+}  // namespace
+
+extern "C" cfm_status cfm_bench_gemm(int dtype, int tile, int epilogue, int M, int N, int K, int iters,
+                                     float* avg_ms) {
+  return guarded([&] {
+    if (!avg_ms || M <= 0 || N <= 0 || K <= 0 || iters <= 0) fail(CFM_ERR_INVALID_ARG, "bad argument");
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    const long Kp = round_up(K, GEMM_BK_BYTES / es), Np = round_up(N, GEMM_BN);
+    const int epi_mode = epilogue;
+    const long Nout = epi_mode == EPI_GLU_MASK ? N : N;
+    char *A = nullptr, *W = nullptr, *C = nullptr, *bias = nullptr, *zero = nullptr, *lens = nullptr;
+    HIP_OK(hipMalloc(&A, (size_t)M * Kp * es));
+    HIP_OK(hipMalloc(&W, (size_t)Np * 2 * Kp * es));
+    HIP_OK(hipMalloc(&C, (size_t)M * Np * 4));
+    HIP_OK(hipMalloc(&bias, (size_t)Np * 2 * 4));
+    HIP_OK(hipMalloc(&zero, 4096));
+    HIP_OK(hipMalloc(&lens, 4096));
+    HIP_OK(hipMemset(zero, 0, 4096));
+    HIP_OK(hipMemset(bias, 0, (size_t)Np * 2 * 4));
+    HIP_OK(hipMemset(C, 0, (size_t)M * Np * 4));
+    std::vector<int32_t> hl(1024, 1 << 30);
+    HIP_OK(hipMemcpy(lens, hl.data(), 4096, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)A, (long)M * Kp * (es / 2), 1u, 0);
+    hipLaunchKernelGGL(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)W, (long)Np * 2 * Kp * (es / 2), 2u, 0);
+    GemmEpi e = epi_of(epi_mode, (const float*)bias, 1.0f);
+    e.C = C; e.ldc = Nout; e.X = (float*)C; e.ldx = Nout; e.lens = (const int32_t*)lens; e.Tp = 1 << 20;
+    e.Vt = C; e.H = 1; e.dkp = 64; e.vt_rows = 64; e.Tpad = M; e.qk_cols = 2 * N / 3; e.uv = (const float*)bias;
+    e.qscale = 1.0f;
+    if (epi_mode == EPI_QKV) e.ldc = 4 * N / 3;
+    const int prev = set_gemm_tile_override(tile);
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) gemm(dt, A, Kp, M, K, W, (int)Kp, N, e, zero, 0);
+    HIP_OK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) gemm(dt, A, Kp, M, K, W, (int)Kp, N, e, zero, 0);
+    HIP_OK(hipEventRecord(e1, 0));
+    HIP_OK(hipEventSynchronize(e1));
+    set_gemm_tile_override(prev);
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    *avg_ms = ms / iters;
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    (void)hipFree(A); (void)hipFree(W); (void)hipFree(C); (void)hipFree(bias); (void)hipFree(zero); (void)hipFree(lens);
     HIP_OK(hipGetLastError());
   });
 }

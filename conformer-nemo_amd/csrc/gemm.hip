@@ -30,24 +30,27 @@ namespace cfm {
 namespace {
 
 constexpr int BKB = GEMM_BK_BYTES;
-constexpr int NSTAGE = 3;
 
-template <int BM_, int BN_, int WM_, int WN_>
+// NS_ = LDS ring depth: NS_ - 1 K-steps are in flight while one is multiplied.
+template <int BM_, int BN_, int WM_, int WN_, int NS_>
 struct Tile {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NSTAGE = NS_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int MR = BM / WM / 32, NR = BN / WN / 32;
   static constexpr int GA = BM / 8 / NW, GB = BN / 8 / NW;     // glds per thread per stage
   static constexpr int STAGE_BYTES = (BM + BN) * BKB;
-  static constexpr int EPS = BN + 4;                           // fp32 stride of the epilogue image
+  static constexpr int EPS = BN;     // fp32 stride of the epilogue image (row writes / 16-B row reads are conflict-free)
   static constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > BM * EPS * 4) ? NSTAGE * STAGE_BYTES : BM * EPS * 4;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
 };
 
-using T128x128 = Tile<128, 128, 2, 2>;
-using T256x128 = Tile<256, 128, 4, 2>;
-using T128x256 = Tile<128, 256, 2, 4>;
-using T64x128 = Tile<64, 128, 2, 2>;   // wave tile 32 x 64
+using T128x128 = Tile<128, 128, 2, 2, 2>;   // 2 x 32 KiB ring: 2 blocks / CU
+using T256x128 = Tile<256, 128, 4, 2, 3>;   // 3 x 48 KiB
+using T128x256 = Tile<128, 256, 2, 4, 3>;   // 3 x 48 KiB
+using T64x128 = Tile<64, 128, 2, 2, 3>;     // 3 x 24 KiB: 2 blocks / CU, wave tile 32 x 64
+using T128x128s3 = Tile<128, 128, 2, 2, 3>; // 3 x 32 KiB
+using T64x128s2 = Tile<64, 128, 2, 2, 2>;   // 2 x 24 KiB: 3 blocks / CU
+using T128x64 = Tile<128, 64, 2, 2, 2>;     // 2 x 24 KiB, wave tile 64 x 32
 
 // ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
 CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
@@ -58,6 +61,15 @@ CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
 template <int N> CFM_DEV void wait_vmcnt() {
   static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `ahead` stages of G loads each are still in flight (ahead in [0, MAXA])
+template <int G, int MAXA> CFM_DEV void wait_stages(int ahead) {
+  if constexpr (MAXA <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (ahead >= MAXA) wait_vmcnt<G * MAXA>();
+    else wait_stages<G, MAXA - 1>(ahead);
+  }
 }
 CFM_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 CFM_DEV void raw_barrier() {
@@ -212,6 +224,17 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
     const int cc = tid % CPR, r0 = tid / CPR;
     const int n = n0 + cc * VE;
     const int nlim = (EPI == EPI_QKV) ? e.qk_cols : p.N;
+    // EPI_QKV: q chunk -> (q + u) at n and (q + v) at n + H*dkp; k chunk -> n + H*dkp
+    const int hq = (EPI == EPI_QKV) ? e.qk_cols / 2 : 0;
+    float ub[VE], vb[VE];
+    if constexpr (EPI == EPI_QKV) {
+#pragma unroll
+      for (int i = 0; i < VE; ++i) {
+        const int nq = min(n + i, hq - 1);
+        ub[i] = e.uv[nq];
+        vb[i] = e.uv[hq + nq];
+      }
+    }
     const bool vec = n + VE <= nlim && ((e.ldc * (long)sizeof(T)) % 16 == 0);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -226,6 +249,19 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
         o[i] = v;
       }
       if (m >= p.M || n >= nlim) continue;
+      if constexpr (EPI == EPI_QKV) {
+        T* row = (T*)e.C + (long)m * e.ldc;
+        if (n < hq) {
+          float ou[VE], ov[VE];
+#pragma unroll
+          for (int i = 0; i < VE; ++i) { ou[i] = (o[i] + ub[i]) * e.qscale; ov[i] = (o[i] + vb[i]) * e.qscale; }
+          *(uint4*)(row + n) = Vec16<T>::from_f32(ou);
+          *(uint4*)(row + hq + n) = Vec16<T>::from_f32(ov);
+        } else {
+          *(uint4*)(row + hq + n) = Vec16<T>::from_f32(o);
+        }
+        continue;
+      }
       T* dst = (T*)e.C + (long)m * e.ldc + n;
       if (vec) {
         *(uint4*)dst = Vec16<T>::from_f32(o);
@@ -311,15 +347,17 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   const int sw = ((lane & 31) >> 1) & 7;   // rows are 32-aligned + (lane & 31)
 
   const int nk = p.nk;
-  stage(0, 0);
-  if (nk > 1) stage(1, 1);
+  constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s, s);
   int slot = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) wait_vmcnt<TL::GA + TL::GB>();
-    else wait_vmcnt<0>();
+    // tiles kt+1 .. min(kt+NS-2, nk-1) may stay in flight
+    wait_stages<G, NS - 2>(min(NS - 2, nk - 1 - kt));
     wait_lgkm0();
     raw_barrier();
-    if (kt + 2 < nk) stage(kt + 2, slot == 0 ? 2 : slot - 1);
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
     const char* Sb = smem + slot * TL::STAGE_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BKB / 32; ++kk) {
@@ -334,7 +372,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
         for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], af[i], bfv[j]);
     }
-    slot = (slot == NSTAGE - 1) ? 0 : slot + 1;
+    slot = (slot == NS - 1) ? 0 : slot + 1;
   }
 
   // ---- epilogue through LDS ----
@@ -398,13 +436,16 @@ int packed_width(const GemmEpi& epi, int N) {
 }
 
 // Tile choice: prefer the largest tile that still gives >= ~1 block per CU.
-int pick_tile(int M, int Nw) {
-  static const int forced = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
-  if (forced >= 0) return forced;
-  auto blocks = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((Nw + bn - 1) / bn); };
-  if (blocks(256, 128) >= 240) return 1;
-  if (blocks(128, 128) >= 200) return 0;
-  return 3;
+int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
+
+// Tile choice (tools/gemm_bench.py on MI355X): large-M GEMMs (the implicit conv) take 256x128;
+// the M ~ 8k layer GEMMs are latency-bound per block and run best with small 64x128 tiles at
+// 3 blocks / CU, except the GLU epilogue (two 64-column halves per group) which prefers 128x128.
+int pick_tile(int M, int Nw, int epi) {
+  if (g_tile_override >= 0) return g_tile_override;
+  if ((long)M * Nw >= (long)32 << 20) return 1;
+  if (epi == EPI_GLU_MASK) return 0;
+  return 5;
 }
 
 template <typename T, template <int> class AL, class ALArgs>
@@ -418,6 +459,9 @@ void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
     case 1: setup(256, 128); launch_epi<T, T256x128, AL>(p, args, st); break;
     case 2: setup(128, 256); launch_epi<T, T128x256, AL>(p, args, st); break;
     case 3: setup(64, 128); launch_epi<T, T64x128, AL>(p, args, st); break;
+    case 4: setup(128, 128); launch_epi<T, T128x128s3, AL>(p, args, st); break;
+    case 5: setup(64, 128); launch_epi<T, T64x128s2, AL>(p, args, st); break;
+    case 6: setup(128, 64); launch_epi<T, T128x64, AL>(p, args, st); break;
     default: setup(128, 128); launch_epi<T, T128x128, AL>(p, args, st); break;
   }
 }
@@ -436,14 +480,19 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
 
 }  // namespace
 
+int set_gemm_tile_override(int tile) {
+  const int prev = g_tile_override;
+  g_tile_override = tile;
+  return prev;
+}
+
 void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int Kpad, int N, const GemmEpi& epi,
           const void* zero_page, hipStream_t st) {
   if (M <= 0) return;
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
-  int tile = pick_tile(M, packed_width(epi, N));
-  if (tile == 2 && round_up_int(packed_width(epi, N), 256) > round_up_int(packed_width(epi, N), GEMM_BN)) tile = 0;
+  int tile = pick_tile(M, packed_width(epi, N), epi.mode);
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
 }
@@ -455,8 +504,7 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   ConvArgs a{(const char*)g.X1, g.T1, g.F1, g.T2, g.F2, (long)g.C * es, M, (const char*)zero_page};
-  int tile = pick_tile(M, N);
-  if (tile == 2) tile = 0;
+  int tile = pick_tile(M, N, epi.mode);
   if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
   else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
 }

@@ -97,6 +97,11 @@ int64_t cfm_encoder_param_numel(const cfm_encoder* h, int i);
 cfm_status cfm_encoder_set_max_audio_length(cfm_encoder* h, int max_audio_length);
 int cfm_encoder_max_audio_length(const cfm_encoder* h);
 
+/* Micro-batch concurrency (default 2, env CFM_MICROBATCH): the batch is split into up to n parts
+ * (each >= 4 utterances) that run on library-owned streams forked from / joined into `stream`.
+ * Outputs are bitwise identical for any n. */
+cfm_status cfm_encoder_set_microbatches(cfm_encoder* h, int n);
+
 /* Bytes of caller-owned device workspace needed by cfm_encoder_forward for (B, T). */
 size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T);
 
@@ -136,6 +141,10 @@ size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk);
 cfm_status cfm_op_rel_attention(int dtype, const void* q, const void* k, const void* v, const void* p,
                                 const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
                                 int dk, int ctx_left, int ctx_right, void* out, void* ws, void* stream);
+
+/* GEMM microbenchmark on synthetic data: average device ms of `iters` launches of the encoder's
+ * GEMM (M x N x K, epilogue id as in csrc/cfm_kernels.h, tile -1 = automatic choice).  Allocates. */
+cfm_status cfm_bench_gemm(int dtype, int tile, int epilogue, int M, int N, int K, int iters, float* avg_ms);
 
 #ifdef __cplusplus
 }

@@ -111,6 +111,12 @@ def test_batch_invariance_full_size(compute):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(y1.cpu().numpy()[0], y[30])      # batch invariance, bitwise
     np.testing.assert_array_equal(y2.cpu().numpy(), y)             # determinism, bitwise
+    for mb in (1, 3, 8):                                           # micro-batch streams: bitwise equal
+        enc.set_microbatches(mb)
+        y3, yl3 = enc.forward(torch.from_numpy(x).cuda(), torch.from_numpy(lens).cuda())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(y3.cpu().numpy(), y)
+        np.testing.assert_array_equal(yl3.cpu().numpy(), yl)
 
 
 def test_dropin_module_forward():
