@@ -58,6 +58,21 @@ def stage_work(B, T, d, L, H, C=None, F=80, K=31, dff=None, es=2):
     }
 
 
+def pmc_traffic(stage, B, T, L, compute):
+    """HBM bytes per launch of `stage` from the newest committed PMC summary (profiles/*_traffic.json,
+    written by tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected), or None.
+    Only valid for the shape it was collected on (Large-17, B=32, T=1000, bf16)."""
+    import glob
+    if (B, T, L, compute) != (32, 1000, 17, "bf16"):
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None
+    st = json.load(open(files[-1]))["stages"].get(stage)
+    return None if st is None else {"bytes_per_launch": st["hbm_bytes"], "fetch": st["fetch_bytes"],
+                                    "write": st["write_bytes"], "file": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(enc, B, T, budget_s):
     """Oracle (numpy restatement of the reference) on the host cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -168,16 +183,21 @@ def main():
             dom = max((k for k in agg if agg[k][1]), key=lambda k: agg[k][0])
             kind, amt = work[dom]
             per_ms = agg[dom][0] / agg[dom][1]
+            tr = pmc_traffic(dom, B, T, L, args.compute)
+            traffic = None if tr is None else tr["bytes_per_launch"]
             if kind == "flop":
                 ach = amt / (per_ms * 1e-3) / 1e12
                 roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK[args.compute],
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": None,
-                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (HIP events, {agg[dom][1]} launches)"}
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": traffic,
+                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (HIP events around 8-launch replay bursts, {agg[dom][1]} launches per forward)"}
             else:
                 ach = amt / (per_ms * 1e-3) / 1e9
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "per_launch": f"{amt / 1e6:.2f} MB in {per_ms:.4f} ms"}
+            roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
+            if tr is not None:
+                roof["traffic_source"] = tr["file"]
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from conformer_oracle import encoder_flops
         total_flop = encoder_flops(B, T, d, L)

@@ -151,8 +151,9 @@ class NativeEncoder:
         return out, out_len
 
     def forward_timed(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None):
-        """One forward with a HIP event at every kernel-group boundary; returns
-        {stage: (device ms, launches)} (cfm_encoder_forward_timed)."""
+        """Per-stage kernel timing (cfm_encoder_forward_timed: every launch replayed in a burst of 8
+        between HIP events).  Returns {stage: (device ms per forward, launches per forward)}.
+        Timing only: the outputs of this call are not the forward's."""
         B, F, T = x_bft.shape
         Tp = encoded_length(T)
         dout = self.cfg.feat_out if (self.cfg.feat_out > 0 and self.cfg.feat_out != self.cfg.d_model) else self.cfg.d_model

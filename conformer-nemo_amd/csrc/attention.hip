@@ -505,7 +505,7 @@ bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   (void)nqt;
   (void)g8;
   if (g4.bytes <= LDS_MAX) {
-    hipLaunchKernelGGL((rel_attn_lds_kernel<NS, ND, 4>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 4>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
     return true;
   }
   return false;
@@ -516,7 +516,7 @@ void launch_nd(const AttnParams& p, dim3 grid, hipStream_t st) {
   constexpr int es = sizeof(T);
   constexpr int DKP = NS * 32 / es;
   constexpr int ND = (DKP + 31) / 32;
-  hipLaunchKernelGGL((rel_attn_kernel<T, NS, ND>), grid, dim3(64), 0, st, p);
+  cfm_launch((rel_attn_kernel<T, NS, ND>), grid, dim3(64), 0, st, p);
 }
 
 template <typename T>

@@ -17,6 +17,9 @@
 #include "cfm_kernels.h"
 
 using namespace cfm;
+namespace cfm {
+thread_local KernelClock* g_kclock = nullptr;
+}
 
 namespace {
 
@@ -547,28 +550,38 @@ const char* kStageNames[ST_COUNT] = {"lengths", "conv1", "conv2_gemm", "subsampl
                                      "ffn_up_gemm", "ffn_down_gemm", "qkv_gemm", "rel_attention", "out_proj_gemm",
                                      "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output"};
 
-// Records a HIP event on the stream at every stage boundary (timed entry point only).
-struct StageTimer {
-  hipStream_t st;
+// Stage timer (timed entry point only): installed as the thread's KernelClock, it brackets every
+// launch's burst of kBurst replays with two events and attributes the per-launch average to the
+// stage last marked.  A stage's time is the sum over its kernels; its launch count the number of
+// kernels of one forward.
+struct StageTimer final : KernelClock {
+  static constexpr int kBurst = 8;
+  int cur = -1;
   std::vector<hipEvent_t> ev;
   std::vector<int> ids;
-  void mark(int id) {
+  void mark(int id) { cur = id; }
+  hipEvent_t rec(hipStream_t st) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventRecord(e, st));
     ev.push_back(e);
-    ids.push_back(id);
+    return e;
   }
+  int begin(hipStream_t st) override { rec(st); ids.push_back(cur); return kBurst; }
+  void end(hipStream_t st) override { rec(st); }
   void finish(float* ms, int* launches) {
-    mark(-1);
-    HIP_OK(hipEventSynchronize(ev.back()));
-    for (size_t i = 0; i + 1 < ev.size(); ++i) {
+    if (!ev.empty()) HIP_OK(hipEventSynchronize(ev.back()));
+    for (size_t i = 0; i < ids.size(); ++i) {
       float t = 0.f;
-      HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
-      if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t; launches[ids[i]] += 1; }
+      HIP_OK(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+      if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t / kBurst; launches[ids[i]] += 1; }
     }
-    for (auto e : ev) (void)hipEventDestroy(e);
   }
+  ~StageTimer() override { for (auto e : ev) (void)hipEventDestroy(e); }
+};
+struct ClockGuard {
+  explicit ClockGuard(KernelClock* c) { g_kclock = c; }
+  ~ClockGuard() { g_kclock = nullptr; }
 };
 #define TM(id) do { if (tm) tm->mark(id); } while (0)
 
@@ -804,8 +817,11 @@ cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const i
                                      void* stream, float* stage_ms, int* stage_launches) {
   return guarded([&] {
     if (!stage_ms || !stage_launches) fail(CFM_ERR_INVALID_ARG, "null stage arrays");
-    StageTimer tm{(hipStream_t)stream};
-    run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, &tm);
+    StageTimer tm;
+    {
+      ClockGuard g(&tm);
+      run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, &tm);
+    }
     tm.finish(stage_ms, stage_launches);
   });
 }
@@ -908,12 +924,12 @@ void relayout(const void* q, const void* k, const void* v, const void* p, const 
   const dim3 g(1024), b(256);
   const long ld = 3L * H * dkp;
   const float qs = attn_qscale(dk);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK, ld, pos_u, qs);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK + (long)H * dkp, ld, pos_v, qs);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)k, M, H, dk, dkp, QK + 2L * H * dkp, ld,
+  cfm_launch(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK, ld, pos_u, qs);
+  cfm_launch(pad_heads_kernel<T>, g, b, 0, st, (const T*)q, M, H, dk, dkp, QK + (long)H * dkp, ld, pos_v, qs);
+  cfm_launch(pad_heads_kernel<T>, g, b, 0, st, (const T*)k, M, H, dk, dkp, QK + 2L * H * dkp, ld,
                      (const float*)nullptr, 1.0f);
-  hipLaunchKernelGGL(vt_kernel<T>, g, b, 0, st, (const T*)v, B, Tp, H, dk, vt_rows, Tpad, Vt);
-  hipLaunchKernelGGL(pad_heads_kernel<T>, g, b, 0, st, (const T*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp,
+  cfm_launch(vt_kernel<T>, g, b, 0, st, (const T*)v, B, Tp, H, dk, vt_rows, Tpad, Vt);
+  cfm_launch(pad_heads_kernel<T>, g, b, 0, st, (const T*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp,
                      (const float*)nullptr, 1.0f);
 }
 }  // namespace
@@ -974,8 +990,8 @@ extern "C" cfm_status cfm_bench_gemm(int dtype, int tile, int epilogue, int M, i
     HIP_OK(hipMemset(C, 0, (size_t)M * Np * 4));
     std::vector<int32_t> hl(1024, 1 << 30);
     HIP_OK(hipMemcpy(lens, hl.data(), 4096, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)A, (long)M * Kp * (es / 2), 1u, 0);
-    hipLaunchKernelGGL(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)W, (long)Np * 2 * Kp * (es / 2), 2u, 0);
+    cfm_launch(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)A, (long)M * Kp * (es / 2), 1u, 0);
+    cfm_launch(fill_rand_kernel, dim3(1024), dim3(256), 0, 0, (uint16_t*)W, (long)Np * 2 * Kp * (es / 2), 2u, 0);
     GemmEpi e = epi_of(epi_mode, (const float*)bias, 1.0f);
     e.C = C; e.ldc = Nout; e.X = (float*)C; e.ldx = Nout; e.lens = (const int32_t*)lens; e.Tp = 1 << 20;
     e.Vt = C; e.H = 1; e.dkp = 64; e.vt_rows = 64; e.Tpad = M; e.qk_cols = 2 * N / 3; e.uv = (const float*)bias;

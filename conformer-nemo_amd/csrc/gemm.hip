@@ -409,13 +409,13 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   args.fill(al);
   const dim3 grid(p.Mtiles * p.Ntiles), block(TL::NT);
   switch (p.epi.mode) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_RELU: hipLaunchKernelGGL((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_SWISH: hipLaunchKernelGGL((gemm_kernel<T, EPI_SWISH, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_RESID: hipLaunchKernelGGL((gemm_kernel<T, EPI_RESID, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_SCALE_F32: hipLaunchKernelGGL((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_GLU_MASK: hipLaunchKernelGGL((gemm_kernel<T, EPI_GLU_MASK, TL, ALoad>), grid, block, 0, st, p, al); break;
-    case EPI_QKV: hipLaunchKernelGGL((gemm_kernel<T, EPI_QKV, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_RELU: cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SWISH: cfm_launch((gemm_kernel<T, EPI_SWISH, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_RESID: cfm_launch((gemm_kernel<T, EPI_RESID, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SCALE_F32: cfm_launch((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_GLU_MASK: cfm_launch((gemm_kernel<T, EPI_GLU_MASK, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_QKV: cfm_launch((gemm_kernel<T, EPI_QKV, TL, ALoad>), grid, block, 0, st, p, al); break;
     default: break;
   }
 }

@@ -270,7 +270,7 @@ __global__ void convert_kernel(const float* __restrict__ src, T* __restrict__ ds
 
 void calc_length(const int32_t* len_in, int32_t* len_out, int B, int T, int repeat, hipStream_t st) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(calc_length_kernel, dim3((B + 63) / 64), dim3(64), 0, st, len_in, len_out, B, T, repeat);
+  cfm_launch(calc_length_kernel, dim3((B + 63) / 64), dim3(64), 0, st, len_in, len_out, B, T, repeat);
 }
 
 void conv1_subsample(int dtype, const float* x, int B, int F, int T, const float* w9, const float* bias, int C,
@@ -279,9 +279,9 @@ void conv1_subsample(int dtype, const float* x, int B, int F, int T, const float
   if (B <= 0 || T1 <= 0) return;
   const dim3 grid(B * T1, (C / 8 + 63) / 64), block(64, 4);
   if (dtype == DT_F32)
-    hipLaunchKernelGGL(conv1_kernel<float>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (float*)out);
+    cfm_launch(conv1_kernel<float>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (float*)out);
   else
-    hipLaunchKernelGGL(conv1_kernel<bf16_t>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (bf16_t*)out);
+    cfm_launch(conv1_kernel<bf16_t>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (bf16_t*)out);
 }
 
 template <typename T>
@@ -289,10 +289,10 @@ static void ln_launch(int E4, const float* x, int rows, int d, const float* w, c
                       const float* w2, const float* b2, T* ot, int sw, hipStream_t st) {
   const dim3 grid((rows + 3) / 4), block(256);
   switch (E4) {
-    case 1: hipLaunchKernelGGL((layernorm_kernel<T, 1>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
-    case 2: hipLaunchKernelGGL((layernorm_kernel<T, 2>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
-    case 4: hipLaunchKernelGGL((layernorm_kernel<T, 4>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
-    default: hipLaunchKernelGGL((layernorm_kernel<T, 8>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
+    case 1: cfm_launch((layernorm_kernel<T, 1>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
+    case 2: cfm_launch((layernorm_kernel<T, 2>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
+    case 4: cfm_launch((layernorm_kernel<T, 4>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
+    default: cfm_launch((layernorm_kernel<T, 8>), grid, block, 0, st, x, rows, d, w, b, ox, w2, b2, ot, sw); break;
   }
 }
 
@@ -313,32 +313,32 @@ void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, co
     constexpr int DT = 32;
     const dim3 grid((Tp + DT - 1) / DT, (d + 255) / 256, B), block(256);
     if (dtype == DT_F32)
-      hipLaunchKernelGGL((dwconv_reg_kernel<float, 31, DT>), grid, block, 0, st, (const float*)g, Tp, d, w, bias,
+      cfm_launch((dwconv_reg_kernel<float, 31, DT>), grid, block, 0, st, (const float*)g, Tp, d, w, bias,
                          bn_mean, bn_inv, bn_w, bn_b, (float*)out_t, out_prenorm_f32);
     else
-      hipLaunchKernelGGL((dwconv_reg_kernel<bf16_t, 31, DT>), grid, block, 0, st, (const bf16_t*)g, Tp, d, w, bias,
+      cfm_launch((dwconv_reg_kernel<bf16_t, 31, DT>), grid, block, 0, st, (const bf16_t*)g, Tp, d, w, bias,
                          bn_mean, bn_inv, bn_w, bn_b, (bf16_t*)out_t, out_prenorm_f32);
     return;
   }
   const dim3 grid((Tp + 31) / 32, (d + 63) / 64, B), block(256);
   if (dtype == DT_F32)
-    hipLaunchKernelGGL(dwconv_kernel<float>, grid, block, 0, st, (const float*)g, Tp, d, K, w, bias, bn_mean, bn_inv,
+    cfm_launch(dwconv_kernel<float>, grid, block, 0, st, (const float*)g, Tp, d, K, w, bias, bn_mean, bn_inv,
                        bn_w, bn_b, (float*)out_t, out_prenorm_f32);
   else
-    hipLaunchKernelGGL(dwconv_kernel<bf16_t>, grid, block, 0, st, (const bf16_t*)g, Tp, d, K, w, bias, bn_mean, bn_inv,
+    cfm_launch(dwconv_kernel<bf16_t>, grid, block, 0, st, (const bf16_t*)g, Tp, d, K, w, bias, bn_mean, bn_inv,
                        bn_w, bn_b, (bf16_t*)out_t, out_prenorm_f32);
 }
 
 void transpose_out(const float* X, int B, int Tp, int d, float* y, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
-  hipLaunchKernelGGL(transpose_kernel, dim3((Tp + 31) / 32, (d + 31) / 32, B), dim3(256), 0, st, X, Tp, d, y);
+  cfm_launch(transpose_kernel, dim3((Tp + 31) / 32, (d + 31) / 32, B), dim3(256), 0, st, X, Tp, d, y);
 }
 
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st) {
   if (n <= 0) return;
   const int blocks = (int)std::min<long>((n + 255) / 256, 4096);
-  if (dtype == DT_F32) hipLaunchKernelGGL(convert_kernel<float>, dim3(blocks), dim3(256), 0, st, src, (float*)dst, n);
-  else hipLaunchKernelGGL(convert_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, src, (bf16_t*)dst, n);
+  if (dtype == DT_F32) cfm_launch(convert_kernel<float>, dim3(blocks), dim3(256), 0, st, src, (float*)dst, n);
+  else cfm_launch(convert_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, src, (bf16_t*)dst, n);
 }
 
 }  // namespace cfm

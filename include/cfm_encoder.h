@@ -114,10 +114,11 @@ size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T);
 cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
                                int32_t* out_len_b, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Same as cfm_encoder_forward, but records a HIP event at every kernel-group boundary on
- * `stream`, synchronises, and ADDS the per-stage device time (ms) and launch counts into
- * stage_ms[cfm_num_stages()] / stage_launches[cfm_num_stages()].  Not graph-capturable;
- * used for the per-kernel roofline in bench.py. */
+/* Per-stage kernel timing on `stream` (single stream, no micro-batch split): every kernel launch
+ * of the forward is replayed 8 times back-to-back between two HIP events, and the per-launch
+ * average is ADDED into stage_ms[stage]; stage_launches[stage] += kernels per forward.
+ * Synchronises.  The outputs of this call are NOT the forward's (replayed residual adds) — timing
+ * only.  Not graph-capturable; used for the per-kernel roofline in bench.py. */
 int cfm_num_stages(void);
 const char* cfm_stage_name(int i);
 cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,

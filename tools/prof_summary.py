@@ -24,5 +24,22 @@ def main(path, top=30):
     print(f"{'TOTAL':90s} {'':6s} {tot / 1e6:9.3f}")
 
 
+def main_trace(path, top=40):
+    """Group a kernel_trace.csv by (kernel, grid): separates e.g. the B=32 single-stream launches of
+    forward_timed from the micro-batched B=16 launches of the timed loop."""
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
+        a = agg.setdefault(key, [0, 0.0])
+        a[0] += 1
+        a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    print(f"{'kernel':90s} {'grid':>9s} {'calls':>6s} {'total_ms':>9s} {'avg_us':>9s}")
+    for (name, grid), (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{name:90s} {grid:9d} {n:6d} {t / 1e6:9.3f} {t / n / 1e3:9.2f}")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 30)
+    if sys.argv[1] == "--trace":
+        main_trace(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 40)
+    else:
+        main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 30)
