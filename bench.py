@@ -99,6 +99,19 @@ def cpu_baseline(enc, B, T, budget_s):
             "sample": f"oracle/conformer_oracle.py numpy fp32, Large-17, {runs} x (B=1, T={T}) utterances, {dt:.1f} s"}
 
 
+def max_over_ranks(elapsed, dev, dist):
+    """Wall time of the job = MAX of the per-rank elapsed times (ranks run replicas)."""
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_throughput(t_max, world, B, T, steps):
+    """Whole-job audio-frames/s: every rank processes its own B utterances of T frames per step."""
+    return world * B * T * steps / t_max
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,12 +160,8 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
     assert torch.isfinite(y).all().item()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    t_max = float(t.item())
-    frames = world * B * T * args.steps
-    value = frames / t_max
+    t_max = max_over_ranks(elapsed, dev, dist)
+    value = job_throughput(t_max, world, B, T, args.steps)
     ms_step = 1000.0 * t_max / args.steps
 
     if rank == 0:
