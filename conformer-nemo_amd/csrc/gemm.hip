@@ -21,6 +21,7 @@
 // Epilogue: the fp32 accumulators are staged through LDS and written back row-major with 16-byte
 // vector accesses (bias, activation, GLU, residual read-modify-write all vectorised).
 #include <cstdlib>
+#include <type_traits>
 
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -29,28 +30,46 @@ namespace cfm {
 
 namespace {
 
-constexpr int BKB = GEMM_BK_BYTES;
-
 // NS_ = LDS ring depth: NS_ - 1 K-steps are in flight while one is multiplied.
-template <int BM_, int BN_, int WM_, int WN_, int NS_>
+// EP_ = epilogue passes: the fp32 accumulator image is staged through LDS BM/EP_ rows at a time
+// (the wave rows wm in [p*WM/EP, (p+1)*WM/EP) write in pass p), so a 256x256 tile fits 128 KiB.
+// BK_ = bytes of K per stage and row (128 or 64; the packed K granule GEMM_BK_BYTES is a multiple).
+//   One glds wave-instruction fills 1 KiB = RPI rows x BK bytes; the 16-byte slots of a row are
+//   XOR-swizzled by (row / (16 / SLOTS)) % SLOTS so each 16-lane ds_read_b128 group hits 16
+//   distinct bank positions.
+template <int BM_, int BN_, int WM_, int WN_, int NS_, int EP_ = 1, int BK_ = 128>
 struct Tile {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NSTAGE = NS_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NSTAGE = NS_, EP = EP_, BKB = BK_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int MR = BM / WM / 32, NR = BN / WN / 32;
-  static constexpr int GA = BM / 8 / NW, GB = BN / 8 / NW;     // glds per thread per stage
+  static constexpr int SLOTS = BKB / 16, RPI = 1024 / BKB, SWDIV = 16 / SLOTS;
+  static constexpr int GA = BM / RPI / NW, GB = BN / RPI / NW;     // glds per thread per stage
   static constexpr int STAGE_BYTES = (BM + BN) * BKB;
   static constexpr int EPS = BN;     // fp32 stride of the epilogue image (row writes / 16-B row reads are conflict-free)
-  static constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > BM * EPS * 4) ? NSTAGE * STAGE_BYTES : BM * EPS * 4;
+  static constexpr int EPI_BYTES = BM / EP * EPS * 4;
+  static constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > EPI_BYTES) ? NSTAGE * STAGE_BYTES : EPI_BYTES;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
+  static_assert(BKB == 64 || BKB == 128, "stage depth");
+  static_assert(GEMM_BK_BYTES % BKB == 0, "packed K granule");
+  static_assert(WM % EP == 0, "epilogue passes split the wave rows");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+  static CFM_DEV int swz(int row) { return (row / SWDIV) % SLOTS; }
+};
+// The rows of one epilogue pass, seen by the epilogue as a (BM/EP) x BN tile.
+template <class TL>
+struct EpiView {
+  static constexpr int BM = TL::BM / TL::EP, BN = TL::BN, NT = TL::NT, EPS = TL::EPS;
 };
 
 using T128x128 = Tile<128, 128, 2, 2, 2>;   // 2 x 32 KiB ring: 2 blocks / CU
 using T256x128 = Tile<256, 128, 4, 2, 3>;   // 3 x 48 KiB
-using T128x256 = Tile<128, 256, 2, 4, 3>;   // 3 x 48 KiB
-using T64x128 = Tile<64, 128, 2, 2, 3>;     // 3 x 24 KiB: 2 blocks / CU, wave tile 32 x 64
-using T128x128s3 = Tile<128, 128, 2, 2, 3>; // 3 x 32 KiB
 using T64x128s2 = Tile<64, 128, 2, 2, 2>;   // 2 x 24 KiB: 3 blocks / CU
-using T128x64 = Tile<128, 64, 2, 2, 2>;     // 2 x 24 KiB, wave tile 64 x 32
+// 1 block / CU tiles
+using T256x256 = Tile<256, 256, 2, 4, 4, 2, 64>;    // 8 waves, 4 x 32 KiB, wave tile 128 x 64
+using T128x128d = Tile<128, 128, 2, 2, 8, 1, 64>;   // 4 waves, 8 x 16 KiB
+using T256x128d = Tile<256, 128, 4, 2, 5, 1, 64>;   // 8 waves, 5 x 24 KiB, wave tile 64 x 64
+using T128x256d = Tile<128, 256, 2, 4, 5, 1, 64>;   // 8 waves, 5 x 24 KiB, wave tile 64 x 64
+using T256x256w = Tile<256, 256, 2, 4, 2, 2, 128>;  // 8 waves, 2 x 64 KiB
 
 // ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
 CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
@@ -84,6 +103,7 @@ CFM_DEV uint32_t lds_addr(const void* p) {
 // ---- A-operand loaders -----------------------------------------------------------------------
 template <int G>
 struct ALoadDense {
+  static constexpr bool kConv = false;
   const char* A; long lda_b; int M; long kbytes; const char* zero;
   struct State { const char* row_ptr[G]; };
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
@@ -102,6 +122,7 @@ struct ALoadDense {
 // tap = 3*kt + kf; source = X1[b][2*t2 - 1 + kt][2*f2 - 1 + kf][c] (zero outside the image).
 template <int G>
 struct ALoadConv {
+  static constexpr bool kConv = true;   // conv2 + ReLU only
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
   struct State { const char* base[G]; uint32_t valid[G]; };
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
@@ -137,7 +158,7 @@ struct ALoadConv {
 };
 
 struct GemmParams {
-  const char* W; long ldw_b; int nk; int Mtiles, Ntiles; int M, N;
+  const char* W; long ldw_b; int kb; int Mtiles, Ntiles; int M, N;   // kb = packed K bytes per row
   GemmEpi epi;
 };
 
@@ -311,28 +332,28 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   int aslot[TL::GA];
 #pragma unroll
   for (int i = 0; i < TL::GA; ++i) {
-    rows[i] = (i * TL::NW + wave) * 8 + (lane >> 3);
-    aslot[i] = ((lane & 7) ^ ((rows[i] >> 1) & 7)) * 16;
+    rows[i] = (i * TL::NW + wave) * TL::RPI + lane / TL::SLOTS;
+    aslot[i] = ((lane % TL::SLOTS) ^ TL::swz(rows[i])) * 16;
   }
   typename ALoad::State ast;
   aload.prepare(ast, m0, rows);
   const char* wrow[TL::GB];
 #pragma unroll
   for (int i = 0; i < TL::GB; ++i) {
-    const int rr = (i * TL::NW + wave) * 8 + (lane >> 3);
-    wrow[i] = p.W + (long)(n0 + rr) * p.ldw_b + ((lane & 7) ^ ((rr >> 1) & 7)) * 16;
+    const int rr = (i * TL::NW + wave) * TL::RPI + lane / TL::SLOTS;
+    wrow[i] = p.W + (long)(n0 + rr) * p.ldw_b + ((lane % TL::SLOTS) ^ TL::swz(rr)) * 16;
   }
   const uint32_t smem_base = lds_addr(smem);
 
   auto stage = [&](int kt, int slot) {
-    const long kb0 = (long)kt * BKB;
+    const long kb0 = (long)kt * TL::BKB;
     const uint32_t sb = smem_base + slot * TL::STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < TL::GA; ++i)
       glds16_asm(aload.src(ast, i, kb0 + aslot[i]), sb + (i * TL::NW + wave) * 1024);
 #pragma unroll
     for (int i = 0; i < TL::GB; ++i)
-      glds16_asm(wrow[i] + kb0, sb + TL::BM * BKB + (i * TL::NW + wave) * 1024);
+      glds16_asm(wrow[i] + kb0, sb + TL::BM * TL::BKB + (i * TL::NW + wave) * 1024);
   };
 
   f32x16 acc[TL::MR][TL::NR];
@@ -344,9 +365,9 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   const int hsel = lane >> 5;
   const int a_row0 = wm * (TL::BM / TL::WM) + (lane & 31);
   const int b_row0 = TL::BM + wn * (TL::BN / TL::WN) + (lane & 31);
-  const int sw = ((lane & 31) >> 1) & 7;   // rows are 32-aligned + (lane & 31)
+  const int sw = TL::swz(lane & 31);       // rows are 32-aligned + (lane & 31)
 
-  const int nk = p.nk;
+  const int nk = p.kb / TL::BKB;
   constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB;
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -360,13 +381,13 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     if (kt + NS - 1 < nk) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
     const char* Sb = smem + slot * TL::STAGE_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < BKB / 32; ++kk) {
+    for (int kk = 0; kk < TL::BKB / 32; ++kk) {
       const int so = ((2 * kk + hsel) ^ sw) * 16;
       uint4 af[TL::MR], bfv[TL::NR];
 #pragma unroll
-      for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * BKB + so);
+      for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * TL::BKB + so);
 #pragma unroll
-      for (int j = 0; j < TL::NR; ++j) bfv[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * BKB + so);
+      for (int j = 0; j < TL::NR; ++j) bfv[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * TL::BKB + so);
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
@@ -375,7 +396,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     slot = (slot == NS - 1) ? 0 : slot + 1;
   }
 
-  // ---- epilogue through LDS ----
+  // ---- epilogue through LDS, BM/EP rows per pass ----
   wait_lgkm0();
   raw_barrier();                         // every wave is done reading the ring
   float* img = (float*)smem;
@@ -387,19 +408,26 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
     for (int j = 0; j < TL::NR; ++j) bcol[j] = p.epi.bias[n0 + wn * (TL::BN / TL::WN) + j * 32 + col];
   }
+  constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
-  for (int i = 0; i < TL::MR; ++i)
+  for (int pass = 0; pass < TL::EP; ++pass) {
+    if (pass > 0) __syncthreads();       // the previous pass has read the image
+    if (wm / WPP == pass) {
 #pragma unroll
-    for (int j = 0; j < TL::NR; ++j) {
-      const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+      for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int rl = wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane);
-        img[rl * TL::EPS + cl] = acc[i][j][rr] + bcol[j];
-      }
+        for (int j = 0; j < TL::NR; ++j) {
+          const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr) {
+            const int rl = (wm % WPP) * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane);
+            img[rl * TL::EPS + cl] = acc[i][j][rr] + bcol[j];
+          }
+        }
     }
-  __syncthreads();
-  epilogue<T, EPI, TL>(p, img, m0, n0);
+    __syncthreads();
+    epilogue<T, EPI, EpiView<TL>>(p, img, m0 + pass * EpiView<TL>::BM, n0);
+  }
 }
 
 template <typename T, class TL, template <int> class AL, class ALArgs>
@@ -408,6 +436,10 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   ALoad al;
   args.fill(al);
   const dim3 grid(p.Mtiles * p.Ntiles), block(TL::NT);
+  if constexpr (ALoad::kConv) {
+    cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al);
+    return;
+  }
   switch (p.epi.mode) {
     case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
     case EPI_RELU: cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al); break;
@@ -435,12 +467,13 @@ int packed_width(const GemmEpi& epi, int N) {
   return epi.mode == EPI_GLU_MASK ? 64 * ((N + 31) / 32) : N;
 }
 
-// Tile choice: prefer the largest tile that still gives >= ~1 block per CU.
 int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
 
-// Tile choice (tools/gemm_bench.py on MI355X): large-M GEMMs (the implicit conv) take 256x128;
-// the M ~ 8k layer GEMMs are latency-bound per block and run best with small 64x128 tiles at
-// 3 blocks / CU, except the GLU epilogue (two 64-column halves per group) which prefers 128x128.
+// Tile ids (CFM_GEMM_TILE / set_gemm_tile_override):
+//   0 128x128 NS2 | 1 256x128 NS3 | 5 64x128 NS2          (128-byte K-steps, several blocks / CU)
+//   7 256x256 NS4 | 8 128x128 NS8 | 9 256x128 NS5 | 10 128x256 NS5   (64-byte K-steps, 1 block / CU)
+//   11 256x256 NS2 (128-byte K-steps)
+// The fp32 parity mode instantiates 0, 1 and 5 only (other ids fall back to 0).
 int pick_tile(int M, int Nw, int epi) {
   if (g_tile_override >= 0) return g_tile_override;
   if ((long)M * Nw >= (long)32 << 20) return 1;
@@ -455,22 +488,31 @@ void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
     p.Mtiles = (p.M + bm - 1) / bm;
     p.Ntiles = (Nw + bn - 1) / bn;
   };
+  constexpr bool kDeep = std::is_same<T, bf16_t>::value;
   switch (tile) {
-    case 1: setup(256, 128); launch_epi<T, T256x128, AL>(p, args, st); break;
-    case 2: setup(128, 256); launch_epi<T, T128x256, AL>(p, args, st); break;
-    case 3: setup(64, 128); launch_epi<T, T64x128, AL>(p, args, st); break;
-    case 4: setup(128, 128); launch_epi<T, T128x128s3, AL>(p, args, st); break;
-    case 5: setup(64, 128); launch_epi<T, T64x128s2, AL>(p, args, st); break;
-    case 6: setup(128, 64); launch_epi<T, T128x64, AL>(p, args, st); break;
-    default: setup(128, 128); launch_epi<T, T128x128, AL>(p, args, st); break;
+    case 1: setup(256, 128); launch_epi<T, T256x128, AL>(p, args, st); return;
+    case 5: setup(64, 128); launch_epi<T, T64x128s2, AL>(p, args, st); return;
+    default: break;
   }
+  if constexpr (kDeep) {
+    switch (tile) {
+      case 7: setup(256, 256); launch_epi<T, T256x256, AL>(p, args, st); return;
+      case 8: setup(128, 128); launch_epi<T, T128x128d, AL>(p, args, st); return;
+      case 9: setup(256, 128); launch_epi<T, T256x128d, AL>(p, args, st); return;
+      case 10: setup(128, 256); launch_epi<T, T128x256d, AL>(p, args, st); return;
+      case 11: setup(256, 256); launch_epi<T, T256x256w, AL>(p, args, st); return;
+      default: break;
+    }
+  }
+  setup(128, 128);
+  launch_epi<T, T128x128, AL>(p, args, st);
 }
 
 GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const GemmEpi& epi) {
   GemmParams p;
   p.W = (const char*)Wp;
   p.ldw_b = (long)Kpad * es;
-  p.nk = (int)((long)Kpad * es / BKB);
+  p.kb = (int)((long)Kpad * es);
   p.Mtiles = p.Ntiles = 0;
   p.M = M;
   p.N = N;

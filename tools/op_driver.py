@@ -28,11 +28,20 @@ def attn(iters):
     torch.cuda.synchronize()
 
 
+GEMM_SHAPES = {"ffn_up": (8000, 2048, 512, 2), "ffn_down": (8000, 512, 2048, 3), "qkv": (8000, 1536, 512, 6),
+               "out": (8000, 512, 512, 3), "ref4096": (4096, 4096, 4096, 0), "conv2": (160000, 512, 4608, 0)}
+
+
 def gemm(iters):
+    """gemm [iters] [tile] [shape,shape...] — env-free tile choice for PMC passes."""
     lib = _lib.load()
     ms = ctypes.c_float(0)
-    for name, M, N, K, epi in [("ffn_up", 8000, 2048, 512, 2), ("ffn_down", 8000, 512, 2048, 3)]:
-        _lib.check(lib.cfm_bench_gemm(1, -1, epi, M, N, K, iters, ctypes.byref(ms)), name)
+    tile = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+    names = sys.argv[4].split(",") if len(sys.argv) > 4 else ["ffn_up", "ffn_down"]
+    for name in names:
+        M, N, K, epi = GEMM_SHAPES[name]
+        _lib.check(lib.cfm_bench_gemm(1, tile, epi, M, N, K, iters, ctypes.byref(ms)), name)
+        print(f"{name} tile {tile}: {ms.value * 1e3:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
