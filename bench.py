@@ -198,7 +198,7 @@ def main():
                 ach = amt / (per_ms * 1e-3) / 1e12
                 roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK[args.compute],
                         "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": traffic,
-                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (HIP events around 8-launch replay bursts, {agg[dom][1]} launches per forward)"}
+                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (stop events in each dispatch packet, chained, {agg[dom][1]} launches per forward)"}
             else:
                 ach = amt / (per_ms * 1e-3) / 1e9
                 roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

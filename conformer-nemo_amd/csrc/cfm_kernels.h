@@ -7,25 +7,34 @@
 
 namespace cfm {
 
-// Kernel clock for cfm_encoder_forward_timed: when installed on the calling thread, every launch
-// is replayed begin()-many times back-to-back between two stream events, so the measured per-launch
-// time is the kernel's steady-state duration (marker overhead amortised over the burst) rather
-// than the gap between single-launch stream markers.  Replays are numerically harmless (every
-// kernel is idempotent except the residual adds, which stay finite) but the timed call's outputs
-// are not the forward's.
+// Kernel clock for cfm_encoder_forward_timed.  When installed on the calling thread, every launch
+// goes through it:
+//   * chain mode: each kernel carries a stop event in its own dispatch packet
+//     (hipExtLaunchKernel); a kernel's time is the gap between its stop and the previous kernel's
+//     stop on the stream (its execution + the dispatch gap), measured inside a normal forward;
+//   * burst mode: each launch is replayed reps() times back-to-back between two stream events
+//     (steady state, warm caches); the timed call's outputs are then not the forward's.
 struct KernelClock {
-  virtual int begin(hipStream_t st) = 0;   // records the start event, returns the burst length
-  virtual void end(hipStream_t st) = 0;    // records the stop event
+  virtual int reps() = 0;
+  virtual void begin(hipStream_t st) = 0;
+  virtual hipEvent_t stop_event() = 0;
+  virtual void end(hipStream_t st) = 0;
   virtual ~KernelClock() = default;
 };
 extern thread_local KernelClock* g_kclock;
 
 template <typename F, typename... Args>
 inline void cfm_launch(F kernel, dim3 grid, dim3 block, uint32_t lds_bytes, hipStream_t st, Args... args) {
-  const int reps = g_kclock ? g_kclock->begin(st) : 1;
-  for (int r = 0; r < reps; ++r)
+  KernelClock* c = g_kclock;
+  if (!c) {
     hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, nullptr, nullptr, 0, args...);
-  if (g_kclock) g_kclock->end(st);
+    return;
+  }
+  c->begin(st);
+  for (int r = 1; r < c->reps(); ++r)
+    hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, nullptr, nullptr, 0, args...);
+  hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, nullptr, c->stop_event(), 0, args...);
+  c->end(st);
 }
 
 enum Dtype { DT_F32 = 0, DT_BF16 = 1 };
@@ -70,6 +79,8 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
           const GemmEpi& epi, const void* zero_page, hipStream_t st);
 // -1 = automatic tile choice; otherwise 0:128x128 1:256x128 2:128x256 3:64x128. Returns the previous value.
 int set_gemm_tile_override(int tile);
+// Microbenchmark probe bits for the dense GEMM (1 no main-loop loads, 2 no epilogue, 4 one K-step); 0 in production.
+int set_gemm_probe(int probe);
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                const void* zero_page, hipStream_t st);
 

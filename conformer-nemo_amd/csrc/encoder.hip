@@ -550,31 +550,44 @@ const char* kStageNames[ST_COUNT] = {"lengths", "conv1", "conv2_gemm", "subsampl
                                      "ffn_up_gemm", "ffn_down_gemm", "qkv_gemm", "rel_attention", "out_proj_gemm",
                                      "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output"};
 
-// Stage timer (timed entry point only): installed as the thread's KernelClock, it brackets every
-// launch's burst of kBurst replays with two events and attributes the per-launch average to the
-// stage last marked.  A stage's time is the sum over its kernels; its launch count the number of
-// kernels of one forward.
+// Stage timer (timed entry point only), installed as the thread's KernelClock.
+//   chain (default): one stop event per kernel, in the dispatch packet; per-kernel time = stop(k) -
+//     stop(k-1) (a start marker precedes the first kernel); outputs are the forward's.
+//   burst (env CFM_STAGE_CLOCK=burst): kBurst back-to-back replays between two stream events.
+// A stage's time is the sum over its kernels; its launch count the number of kernels per forward.
 struct StageTimer final : KernelClock {
   static constexpr int kBurst = 8;
+  const bool burst = [] { const char* s = getenv("CFM_STAGE_CLOCK"); return s && std::string(s) == "burst"; }();
   int cur = -1;
-  std::vector<hipEvent_t> ev;
+  std::vector<hipEvent_t> ev;   // burst: (start, stop) per kernel; chain: marker, then stop per kernel
   std::vector<int> ids;
-  void mark(int id) { cur = id; }
-  hipEvent_t rec(hipStream_t st) {
+  hipEvent_t make() {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipEventRecord(e, st));
     ev.push_back(e);
     return e;
   }
-  int begin(hipStream_t st) override { rec(st); ids.push_back(cur); return kBurst; }
-  void end(hipStream_t st) override { rec(st); }
+  void mark(int id) { cur = id; }
+  int reps() override { return burst ? kBurst : 1; }
+  void begin(hipStream_t st) override {
+    ids.push_back(cur);
+    if (burst || ev.empty()) HIP_OK(hipEventRecord(make(), st));
+  }
+  hipEvent_t stop_event() override { return burst ? nullptr : make(); }
+  void end(hipStream_t st) override {
+    if (burst) HIP_OK(hipEventRecord(make(), st));
+  }
   void finish(float* ms, int* launches) {
     if (!ev.empty()) HIP_OK(hipEventSynchronize(ev.back()));
     for (size_t i = 0; i < ids.size(); ++i) {
       float t = 0.f;
-      HIP_OK(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
-      if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t / kBurst; launches[ids[i]] += 1; }
+      if (burst) {
+        HIP_OK(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+        t /= kBurst;
+      } else {
+        HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      }
+      if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t; launches[ids[i]] += 1; }
     }
   }
   ~StageTimer() override { for (auto e : ev) (void)hipEventDestroy(e); }
@@ -976,7 +989,8 @@ extern "C" cfm_status cfm_bench_gemm(int dtype, int tile, int epilogue, int M, i
     if (!avg_ms || M <= 0 || N <= 0 || K <= 0 || iters <= 0) fail(CFM_ERR_INVALID_ARG, "bad argument");
     const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
     const long Kp = round_up(K, GEMM_BK_BYTES / es), Np = round_up(N, GEMM_BN);
-    const int epi_mode = epilogue;
+    const int epi_mode = epilogue & 15;   // bits 4-5: GEMM probe (see set_gemm_probe)
+    const int prev_probe = set_gemm_probe(epilogue >> 4);
     const long Nout = epi_mode == EPI_GLU_MASK ? N : N;
     char *A = nullptr, *W = nullptr, *C = nullptr, *bias = nullptr, *zero = nullptr, *lens = nullptr;
     HIP_OK(hipMalloc(&A, (size_t)M * Kp * es));
@@ -1007,6 +1021,7 @@ extern "C" cfm_status cfm_bench_gemm(int dtype, int tile, int epilogue, int M, i
     HIP_OK(hipEventRecord(e1, 0));
     HIP_OK(hipEventSynchronize(e1));
     set_gemm_tile_override(prev);
+    set_gemm_probe(prev_probe);
     float ms = 0.f;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     *avg_ms = ms / iters;

@@ -159,6 +159,7 @@ struct ALoadConv {
 
 struct GemmParams {
   const char* W; long ldw_b; int kb; int Mtiles, Ntiles; int M, N;   // kb = packed K bytes per row
+  int probe;   // microbenchmark probes only (cfm_bench_gemm): 1 no main-loop loads, 2 no epilogue, 4 one K-step
   GemmEpi epi;
 };
 
@@ -367,35 +368,64 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   const int b_row0 = TL::BM + wn * (TL::BN / TL::WN) + (lane & 31);
   const int sw = TL::swz(lane & 31);       // rows are 32-aligned + (lane & 31)
 
-  const int nk = p.kb / TL::BKB;
-  constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB;
+  const int nk = (p.probe & 4) ? 1 : p.kb / TL::BKB;
+  constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB, KSUB = TL::BKB / 32;
+  auto read_frags = [&](const char* Sb, int kk, uint4* af, uint4* bf) {
+    const int so = ((2 * kk + hsel) ^ sw) * 16;
+#pragma unroll
+    for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * TL::BKB + so);
+#pragma unroll
+    for (int j = 0; j < TL::NR; ++j) bf[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * TL::BKB + so);
+  };
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) stage(s, s);
+  // Software pipeline: the fragments of substep g+1 are read from LDS while the MFMAs of substep
+  // g run.  The ring wait + barrier for K-step kt+1 sit in front of the LAST substep of kt, so the
+  // first fragments of kt+1 are already in registers when kt+1 starts.
+  wait_stages<G, NS - 2>(min(NS - 2, nk - 1));
+  wait_lgkm0();
+  raw_barrier();
+  uint4 afc[TL::MR], bfc[TL::NR];
+  read_frags(smem, 0, afc, bfc);
   int slot = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // tiles kt+1 .. min(kt+NS-2, nk-1) may stay in flight
-    wait_stages<G, NS - 2>(min(NS - 2, nk - 1 - kt));
-    wait_lgkm0();
-    raw_barrier();
-    if (kt + NS - 1 < nk) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+    // refill the slot K-step kt-1 used: every wave finished reading it before the last barrier
+    if (kt + NS - 1 < nk && !(p.probe & 1)) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
     const char* Sb = smem + slot * TL::STAGE_BYTES;
+    const int nslot = (slot == NS - 1) ? 0 : slot + 1;
 #pragma unroll
-    for (int kk = 0; kk < TL::BKB / 32; ++kk) {
-      const int so = ((2 * kk + hsel) ^ sw) * 16;
-      uint4 af[TL::MR], bfv[TL::NR];
-#pragma unroll
-      for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * TL::BKB + so);
-#pragma unroll
-      for (int j = 0; j < TL::NR; ++j) bfv[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * TL::BKB + so);
+    for (int kk = 0; kk < KSUB; ++kk) {
+      uint4 afn[TL::MR], bfn[TL::NR];
+      if (kk + 1 < KSUB) {
+        read_frags(Sb, kk + 1, afn, bfn);
+      } else if (kt + 1 < nk) {
+        wait_stages<G, NS - 2>(min(NS - 2, nk - 2 - kt));   // K-step kt+1 has landed
+        wait_lgkm0();
+        raw_barrier();
+        read_frags(smem + nslot * TL::STAGE_BYTES, 0, afn, bfn);
+      }
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], af[i], bfv[j]);
+        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
+#pragma unroll
+      for (int j = 0; j < TL::NR; ++j) bfc[j] = bfn[j];
     }
-    slot = (slot == NS - 1) ? 0 : slot + 1;
+    slot = nslot;
   }
 
+  if (p.probe & 2) {   // probe: no epilogue (keep the accumulators alive)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+      for (int j = 0; j < TL::NR; ++j) t += acc[i][j][0];
+    if (t == 1234.5f) ((float*)p.epi.C)[threadIdx.x] = t;
+    return;
+  }
   // ---- epilogue through LDS, BM/EP rows per pass ----
   wait_lgkm0();
   raw_barrier();                         // every wave is done reading the ring
@@ -474,9 +504,18 @@ int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? a
 //   7 256x256 NS4 | 8 128x128 NS8 | 9 256x128 NS5 | 10 128x256 NS5   (64-byte K-steps, 1 block / CU)
 //   11 256x256 NS2 (128-byte K-steps)
 // The fp32 parity mode instantiates 0, 1 and 5 only (other ids fall back to 0).
-int pick_tile(int M, int Nw, int epi) {
+// Automatic choice (tools/gemm_bench.py, MI355X, bf16): the implicit conv and the wide FFN-up
+// GEMM run best on 256x256 (tile 11); the N = 512 layer GEMMs on 64x128 at 3 blocks / CU (tile 5);
+// the GLU GEMM on 256x128.
+int pick_tile(int dtype, int M, int Nw, int epi, bool conv) {
   if (g_tile_override >= 0) return g_tile_override;
-  if ((long)M * Nw >= (long)32 << 20) return 1;
+  if (dtype == DT_BF16) {
+    if (conv) return 11;
+    if (Nw >= 2048 && M >= 4096) return 11;
+    if (epi == EPI_GLU_MASK) return 1;
+    return 5;
+  }
+  if (conv || (long)M * Nw >= (long)32 << 20) return 1;
   if (epi == EPI_GLU_MASK) return 0;
   return 5;
 }
@@ -513,6 +552,7 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
   p.W = (const char*)Wp;
   p.ldw_b = (long)Kpad * es;
   p.kb = (int)((long)Kpad * es);
+  p.probe = 0;
   p.Mtiles = p.Ntiles = 0;
   p.M = M;
   p.N = N;
@@ -521,6 +561,13 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
 }
 
 }  // namespace
+
+int g_gemm_probe = 0;
+int set_gemm_probe(int probe) {
+  const int prev = g_gemm_probe;
+  g_gemm_probe = probe;
+  return prev;
+}
 
 int set_gemm_tile_override(int tile) {
   const int prev = g_tile_override;
@@ -534,7 +581,8 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
-  int tile = pick_tile(M, packed_width(epi, N), epi.mode);
+  p.probe = g_gemm_probe;
+  int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
 }
@@ -546,7 +594,7 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   ConvArgs a{(const char*)g.X1, g.T1, g.F1, g.T2, g.F2, (long)g.C * es, M, (const char*)zero_page};
-  int tile = pick_tile(M, N, epi.mode);
+  int tile = pick_tile(dtype, M, N, epi.mode, true);
   if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
   else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
 }
