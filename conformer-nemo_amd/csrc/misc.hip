@@ -3,6 +3,7 @@
 // algorithmic bytes each one moves.
 #include "cfm_common.h"
 #include "cfm_kernels.h"
+#include "cfm_ln.h"
 
 namespace cfm {
 
@@ -68,85 +69,16 @@ __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x,
   }
 }
 
-// LayerNorm(d, eps=1e-5) over fp32 rows, one wave per row (torch.nn.LayerNorm semantics:
-// biased variance).  Optional fused second LayerNorm (norm_out of layer l feeding
-// norm_feed_forward1 of layer l+1) and optional Swish on the compute-type output.
+// LayerNorm(d, eps=1e-5) over fp32 rows, one wave per row (cfm_ln.h: ln_row).
 template <typename T, int E4>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows, int d,
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         float* out_x, const float* __restrict__ w2,
                                                         const float* __restrict__ b2, T* out_t, int swish_out) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
   if (row >= rows) return;
-  const int d4 = d >> 2;
-  const float4* xr = (const float4*)(x + (long)row * d);
-  float4 v[E4];
-  float s = 0.0f;
-#pragma unroll
-  for (int e = 0; e < E4; ++e) {
-    const int g = lane + 64 * e;
-    const float4 t = xr[min(g, d4 - 1)];            // unconditional (clamped) load, then select
-    v[e] = (g < d4) ? t : make_float4(0, 0, 0, 0);
-    s += v[e].x + v[e].y + v[e].z + v[e].w;
-  }
-  const float inv_d = 1.0f / (float)d;
-  auto normalize = [&](const float* ww, const float* bbp) {
-    float mean = wave_sum(s) * inv_d;
-    float q = 0.0f;
-#pragma unroll
-    for (int e = 0; e < E4; ++e) {
-      const int g = lane + 64 * e;
-      if (g < d4) {
-        const float a0 = v[e].x - mean, a1 = v[e].y - mean, a2 = v[e].z - mean, a3 = v[e].w - mean;
-        q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-      }
-    }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) * inv_d + 1e-5f);
-    s = 0.0f;
-#pragma unroll
-    for (int e = 0; e < E4; ++e) {
-      const int g = lane + 64 * e;
-      const float4 wv = ((const float4*)ww)[min(g, d4 - 1)], bv = ((const float4*)bbp)[min(g, d4 - 1)];
-      if (g < d4) {
-        v[e].x = (v[e].x - mean) * rstd * wv.x + bv.x;
-        v[e].y = (v[e].y - mean) * rstd * wv.y + bv.y;
-        v[e].z = (v[e].z - mean) * rstd * wv.z + bv.z;
-        v[e].w = (v[e].w - mean) * rstd * wv.w + bv.w;
-        s += v[e].x + v[e].y + v[e].z + v[e].w;
-      }
-    }
-  };
-  normalize(w, b);
-  if (out_x) {
-    float4* o = (float4*)(out_x + (long)row * d);
-#pragma unroll
-    for (int e = 0; e < E4; ++e) {
-      const int g = lane + 64 * e;
-      if (g < d4) o[g] = v[e];
-    }
-  }
-  if (w2) normalize(w2, b2);
-  if (out_t) {
-    T* o = out_t + (long)row * d;
-#pragma unroll
-    for (int e = 0; e < E4; ++e) {
-      const int g = lane + 64 * e;
-      if (g < d4) {
-        float f[4] = {v[e].x, v[e].y, v[e].z, v[e].w};
-        if (swish_out) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) f[i] = swishf(f[i]);
-        }
-        if constexpr (sizeof(T) == 2) {
-          *(uint2*)(o + 4 * g) = make_uint2((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
-                                            (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16));
-        } else {
-          *(float4*)(o + 4 * g) = make_float4(f[0], f[1], f[2], f[3]);
-        }
-      }
-    }
-  }
+  ln_row<T, E4>(x + (long)row * d, d, threadIdx.x & 63, w, b, out_x ? out_x + (long)row * d : nullptr, w2, b2,
+                out_t ? out_t + (long)row * d : nullptr, swish_out);
 }
 
 // Depthwise Conv1d(k, pad (k-1)/2, groups=d) + bias + BatchNorm1d(eval) + Swish
