@@ -321,7 +321,9 @@ CFM_DEV_HOST_INLINE LdsGeom lds_geom(int Tp, int dkp, int vt_rows, int nw) {
   return g;
 }
 
-template <int NS, int ND, int NW>
+// PF: prefetch the next key tile's P rows into registers (costs 8*NS VGPRs; off for NW = 8, where
+// two waves per SIMD must fit 256 registers and the second wave hides the P latency instead).
+template <int NS, int ND, int NW, bool PF>
 __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   using T = bf16_t;
   constexpr int SE = 16;
@@ -426,11 +428,15 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
         pb[s] = *(const uint4*)(prowb + d0);
       }
     };
-    uint4 pa[NS], pb[NS], na[NS], nb[NS];
-    if (jbeg < jend) load_p(jbeg, pa, pb);
+    uint4 pa[NS], pb[NS], na[PF ? NS : 1], nb[PF ? NS : 1];
+    if (PF && jbeg < jend) load_p(jbeg, pa, pb);
     for (int j0 = jbeg; j0 < jend; j0 += 32) {
       const bool more = j0 + 32 < jend;
-      if (more) load_p(j0 + 32, na, nb);
+      if constexpr (PF) {
+        if (more) load_p(j0 + 32, (uint4(&)[NS])na, (uint4(&)[NS])nb);
+      } else {
+        load_p(j0, pa, pb);
+      }
       f32x16 st = f32x16{}, bd0 = f32x16{}, bd1 = f32x16{};
       const char* krow = Ks + (j0 + col) * g.ks + hsel * 16;
 #pragma unroll
@@ -459,9 +465,11 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
       PV<T, ND>::run(o, st, v);
       __builtin_amdgcn_s_waitcnt(0xc07f);   // bd_s / row_s reads done before the next tile rewrites them
       __builtin_amdgcn_wave_barrier();
-      if (more) {
+      if constexpr (PF) {
+        if (more) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) { pa[s] = na[s]; pb[s] = nb[s]; }
+          for (int s = 0; s < NS; ++s) { pa[s] = na[s]; pb[s] = nb[s]; }
+        }
       }
     }
     if (hsel == 0) row_s[col] = l_run;
@@ -487,25 +495,30 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   }
 }
 
-// launches the LDS-resident kernel if its image fits; returns false otherwise
+// launches the LDS-resident kernel if its image fits; returns false otherwise.  8 waves per block
+// (one 32-query tile each at T' <= 256, two waves per SIMD) when the image fits, else 4.
 template <int NS>
 bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   constexpr int DKP = NS * 16;
   constexpr int ND = (DKP + 31) / 32;
-  const int nqt = (p.Tp + 31) / 32;
-  const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
-  const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
   constexpr int LDS_MAX = 160 * 1024;
   static bool attr_set = [] {
-    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 8, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return true;
   }();
   (void)attr_set;
-  (void)nqt;
-  (void)g8;
+  static const int force_nw = [] { const char* s = getenv("CFM_ATTN_NW"); return s ? atoi(s) : 0; }();
+  const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
+  const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
+  if (force_nw != 4 && g8.bytes <= LDS_MAX) {
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, false>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
+    return true;
+  }
   if (g4.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 4>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 4, true>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
     return true;
   }
   return false;
