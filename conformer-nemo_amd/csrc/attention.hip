@@ -117,7 +117,10 @@ constexpr float RESCALE_THR = 8.0f;   // log2 units: P entries may reach 2^8 bef
 // Scores of this lane's query against its 16 keys of the tile: s = ac + bd (already in log2 units,
 // Q was pre-scaled by log2(e)/sqrt(dk)); masked keys -> -inf.  Masking runs only on tiles that
 // need it (uniform branch).
-CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, int j0, int len, int iq, int lane) {
+// `rowx` XORs the BD image row (0 or 32): the LDS kernel keeps the two 32-position halves of the
+// window in a 2-slot ring and swaps their roles every key tile.
+CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, int j0, int len, int iq, int lane,
+                          int rowx = 0) {
   const int col = lane & 31;
   const bool need_mask = (j0 + 32 > len) || p.ctx_left >= 0 || p.ctx_right >= 0;
   float mloc = -INFINITY;
@@ -125,7 +128,7 @@ CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, in
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = acc_row(r, lane);
-      st[r] += bd_s[(jj - col + 31) * BDS + col];
+      st[r] += bd_s[((jj - col + 31) ^ rowx) * BDS + col];
       mloc = fmaxf(mloc, st[r]);
     }
   } else {
@@ -133,7 +136,7 @@ CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, in
     for (int r = 0; r < 16; ++r) {
       const int jj = acc_row(r, lane);
       const int jg = j0 + jj;
-      const float sc = st[r] + bd_s[(jj - col + 31) * BDS + col];
+      const float sc = st[r] + bd_s[((jj - col + 31) ^ rowx) * BDS + col];
       bool masked = jg >= len;
       if (p.ctx_left >= 0) masked |= jg < iq - p.ctx_left;
       if (p.ctx_right >= 0) masked |= jg > iq + p.ctx_right;
@@ -321,8 +324,8 @@ CFM_DEV_HOST_INLINE LdsGeom lds_geom(int Tp, int dkp, int vt_rows, int nw) {
   return g;
 }
 
-// PF: prefetch the next key tile's P rows into registers (costs 8*NS VGPRs; off for NW = 8, where
-// two waves per SIMD must fit 256 registers and the second wave hides the P latency instead).
+// PF: prefetch the next key tile's P rows into registers (8*NS VGPRs; with NW = 8, two waves per
+// SIMD must fit 256 registers: on for dk <= 64).
 template <int NS, int ND, int NW, bool PF>
 __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   using T = bf16_t;
@@ -415,46 +418,47 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
     if (p.ctx_left >= 0) jbeg = max(0, (i0 - p.ctx_left) & ~31);
     if (p.ctx_right >= 0) jend = min(jend, i0 + 31 + p.ctx_right + 1);
 
-    auto load_p = [&](int j0, uint4 (&pa)[NS], uint4 (&pb)[NS]) {
-      const int pr0 = Tp - 1 - (i0 + 31) + j0;
-      const int ra = min(max(pr0 + col, 0), 2 * Tp - 2);
-      const int rb = min(max(pr0 + 32 + col, 0), 2 * Tp - 2);
-      const T* prowa = (const T*)p.P + (long)ra * p.ldp + (long)h * p.dkp;
-      const T* prowb = (const T*)p.P + (long)rb * p.ldp + (long)h * p.dkp;
+    // BD window of key tile k = positions [j0 - i0 + T' - 32, j0 - i0 + T' + 32): its upper half is
+    // the lower half of tile k+1, so each tile computes one new 32-position block (P rows loaded
+    // one tile ahead) into the ring slot the block before last used.
+    auto load_p = [&](int prow0, uint4 (&pr)[NS]) {
+      const int ra = min(max(prow0 + col, 0), 2 * Tp - 2);
+      const T* prow = (const T*)p.P + (long)ra * p.ldp + (long)h * p.dkp;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int d0 = s * SE + hsel * (SE / 2);
-        pa[s] = *(const uint4*)(prowa + d0);
-        pb[s] = *(const uint4*)(prowb + d0);
-      }
+      for (int s = 0; s < NS; ++s) pr[s] = *(const uint4*)(prow + s * SE + hsel * (SE / 2));
     };
-    uint4 pa[NS], pb[NS], na[PF ? NS : 1], nb[PF ? NS : 1];
-    if (PF && jbeg < jend) load_p(jbeg, pa, pb);
-    for (int j0 = jbeg; j0 < jend; j0 += 32) {
+    auto bd_block = [&](const uint4 (&pr)[NS], int slot) {
+      f32x16 bd = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) mfma_slab<T>(bd, pr[s], qv[s]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bd_s[(acc_row(r, lane) + 32 * slot) * BDS + col] = bd[r];
+    };
+    // P row of position block start for key tile j0: lower = Tp - 1 - (i0 + 31) + j0, upper = +32
+    uint4 pu[NS], pn[PF ? NS : 1];
+    if (jbeg < jend) {
+      uint4 pl[NS];
+      load_p(Tp - 1 - (i0 + 31) + jbeg, pl);
+      load_p(Tp - 1 - (i0 + 31) + jbeg + 32, pu);
+      bd_block(pl, 0);
+    }
+    int k = 0;
+    for (int j0 = jbeg; j0 < jend; j0 += 32, ++k) {
       const bool more = j0 + 32 < jend;
       if constexpr (PF) {
-        if (more) load_p(j0 + 32, (uint4(&)[NS])na, (uint4(&)[NS])nb);
-      } else {
-        load_p(j0, pa, pb);
+        if (more) load_p(Tp - 1 - (i0 + 31) + j0 + 64, (uint4(&)[NS])pn);
       }
-      f32x16 st = f32x16{}, bd0 = f32x16{}, bd1 = f32x16{};
+      f32x16 st = f32x16{};
       const char* krow = Ks + (j0 + col) * g.ks + hsel * 16;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const uint4 kf = *(const uint4*)(krow + s * 32);
         mfma_slab<T>(st, kf, qu[s]);
-        mfma_slab<T>(bd0, pa[s], qv[s]);
-        mfma_slab<T>(bd1, pb[s], qv[s]);
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = acc_row(r, lane);
-        bd_s[rr * BDS + col] = bd0[r];
-        bd_s[(rr + 32) * BDS + col] = bd1[r];
-      }
+      bd_block(pu, (k + 1) & 1);
       __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
       __builtin_amdgcn_wave_barrier();
-      const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane);
+      const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane, (k & 1) << 5);
       softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
       uint2 v[ND][4];
 #pragma unroll
@@ -465,10 +469,12 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
       PV<T, ND>::run(o, st, v);
       __builtin_amdgcn_s_waitcnt(0xc07f);   // bd_s / row_s reads done before the next tile rewrites them
       __builtin_amdgcn_wave_barrier();
-      if constexpr (PF) {
-        if (more) {
+      if (more) {
+        if constexpr (PF) {
 #pragma unroll
-          for (int s = 0; s < NS; ++s) { pa[s] = na[s]; pb[s] = nb[s]; }
+          for (int s = 0; s < NS; ++s) pu[s] = pn[s];
+        } else {
+          load_p(Tp - 1 - (i0 + 31) + j0 + 64, pu);
         }
       }
     }
@@ -505,7 +511,7 @@ bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   static bool attr_set = [] {
     (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 8, false>,
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 8, (NS <= 4)>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return true;
   }();
@@ -514,7 +520,7 @@ bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
   const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
   if (force_nw != 4 && g8.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, false>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, (NS <= 4)>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
     return true;
   }
   if (g4.bytes <= LDS_MAX) {
