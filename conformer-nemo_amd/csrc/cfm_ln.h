@@ -24,6 +24,9 @@ CFM_DEV void ln_load(const float* xr_, int d, int lane, float4 (&v)[E4]) {
 template <typename T, int E4>
 CFM_DEV void ln_apply(float4 (&v)[E4], int d, int lane, const float* w, const float* b, float* out_x,
                       const float* w2, const float* b2, T* out_t, int swish_out) {
+  // no implicit FMA contraction: several rows per wave run unrolled copies of this body, and every
+  // copy must round identically (bitwise batch invariance)
+#pragma clang fp contract(off)
   const int d4 = d >> 2;
   float s = 0.0f;
 #pragma unroll
