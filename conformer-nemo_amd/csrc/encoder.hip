@@ -14,6 +14,7 @@
 
 #include "../../include/cfm_encoder.h"
 #include "cfm_common.h"
+#include "cfm_abi.h"
 #include "cfm_kernels.h"
 
 using namespace cfm;
@@ -21,48 +22,11 @@ namespace cfm {
 thread_local KernelClock* g_kclock = nullptr;
 }
 
-namespace {
-
+namespace cfm {
 thread_local std::string g_last_error;
-
-struct CfmError {
-  cfm_status code;
-  std::string msg;
-};
-
-[[noreturn]] void fail(cfm_status code, const std::string& msg) { throw CfmError{code, msg}; }
-
-#define HIP_OK(expr)                                                                          \
-  do {                                                                                        \
-    hipError_t _e = (expr);                                                                   \
-    if (_e != hipSuccess) fail(CFM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
-  } while (0)
-
-template <class F>
-cfm_status guarded(F&& f) {
-  try {
-    f();
-    return CFM_OK;
-  } catch (const CfmError& e) {
-    g_last_error = e.msg;
-    return e.code;
-  } catch (const std::exception& e) {
-    g_last_error = e.what();
-    return CFM_ERR_INVALID_ARG;
-  } catch (...) {
-    g_last_error = "unknown error";
-    return CFM_ERR_INVALID_ARG;
-  }
 }
 
-inline long round_up(long v, long m) { return (v + m - 1) / m * m; }
-inline uint16_t host_f2bf(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+namespace {
 
 // calc_length (subsampling.py:272-282) in float32 on the host.
 int host_calc_length(int len, int repeat) {

@@ -1,0 +1,2 @@
+"""Loss plugins (reference nemo/collections/asr/losses)."""
+from nemo.collections.asr.losses.ctc import CTCLoss  # noqa: F401

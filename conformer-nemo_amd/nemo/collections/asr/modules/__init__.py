@@ -1,2 +1,3 @@
 """Module plugins resolvable by yaml `_target_` (reference nemo/collections/asr/modules)."""
 from nemo.collections.asr.modules.conformer_encoder import ConformerEncoder  # noqa: F401
+from nemo.collections.asr.modules.conv_asr import ConvASRDecoder  # noqa: F401

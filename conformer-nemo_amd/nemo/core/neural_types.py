@@ -20,6 +20,18 @@ class AcousticEncodedRepresentation(ElementType):
     pass
 
 
+class LogprobsType(ElementType):
+    pass
+
+
+class LabelsType(ElementType):
+    pass
+
+
+class LossType(ElementType):
+    pass
+
+
 class NeuralType:
     def __init__(self, axes=None, elements_type=None, optional: bool = False):
         self.axes = tuple(axes) if axes is not None else None

@@ -10,8 +10,8 @@ import conformer_oracle as O
 from conftest import ROOT
 
 
-def _declared_symbols():
-    src = open(os.path.join(ROOT, "include", "cfm_encoder.h")).read()
+def _declared_symbols(header="cfm_encoder.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(cfm_[a-z0-9_]+)\s*\(", src)))
 
@@ -28,6 +28,10 @@ def test_library_loads_and_exports_header_symbols():
     out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
     for name in declared:
         assert re.search(rf"\bT {name}\b", out), name
+    ctc = _declared_symbols("cfm_ctc.h")
+    assert set(ctc) == set(_lib.CTC_SYMBOLS)
+    for name in ctc:
+        assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
 def test_encoded_length_matches_oracle():
