@@ -1,4 +1,4 @@
-"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h and include/cfm_ctc.h).
+"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h and cfm_train.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -24,6 +24,11 @@ EXPORTED_SYMBOLS = (
     "cfm_encoder_set_max_audio_length", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
     "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
     "cfm_op_rel_attention", "cfm_bench_gemm",
+)
+# every symbol include/cfm_train.h declares
+TRAIN_SYMBOLS = (
+    "cfm_op_layernorm_backward_ws_size", "cfm_op_layernorm_backward", "cfm_op_linear_backward_ws_size",
+    "cfm_op_linear_backward", "cfm_op_swish_backward",
 )
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
@@ -86,6 +91,11 @@ def load() -> ctypes.CDLL:
         "cfm_op_rel_attention_ws_size": (sz, [ci, ci, ci, ci, ci]),
         "cfm_bench_gemm": (ci, [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(ctypes.c_float)]),
         "cfm_op_rel_attention": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp]),
+        "cfm_op_layernorm_backward_ws_size": (sz, [ci, ci]),
+        "cfm_op_layernorm_backward": (ci, [vp, ci, ci, vp, vp, vp, ci, vp, vp, vp, sz, vp]),
+        "cfm_op_linear_backward_ws_size": (sz, [ci, ci, ci, ci]),
+        "cfm_op_linear_backward": (ci, [ci, vp, ci, ci, vp, ci, vp, vp, vp, vp, vp, sz, vp]),
+        "cfm_op_swish_backward": (ci, [vp, vp, vp, ctypes.c_int64, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -1,0 +1,289 @@
+// Backward building blocks of the Conformer layer (training step of BASELINE
+// config 3): operand relayouts for the gradient GEMMs, deterministic column reductions,
+// LayerNorm backward and the Swish derivative.  The gradient GEMMs themselves run on the forward
+// GEMM kernel (gemm.hip): dX = dY . W on a packed W^T, dW = dY^T . X on transposed operands.
+//
+// Reference semantics: torch.nn.LayerNorm (conformer_modules.py:66-70 via the layer, eps 1e-5,
+// biased variance), nn.Linear (y = x W^T + b), Swish (activations.py:20, x * sigmoid(x)).
+#include <algorithm>
+#include <cstring>
+
+#include "../../include/cfm_train.h"
+#include "cfm_abi.h"
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+namespace cfm {
+namespace {
+
+// dst[i][j] = transpose ? src[j][i] : src[i][j] (compute type), zero outside src; 32x32 LDS tiles.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, long src_ld, int rows, int cols,
+                                                   int transpose, T* __restrict__ dst, long dst_ld, int rows_pad,
+                                                   int cols_pad) {
+  __shared__ float tile[32][33];
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    if (transpose) {   // tile[k][tx] = src[j0 + k][i0 + tx]: coalesced along the source rows
+      const int si = j0 + k, sj = i0 + tx;
+      tile[k][tx] = (si < rows && sj < cols) ? src[(long)si * src_ld + sj] : 0.0f;
+    } else {
+      const int si = i0 + k, sj = j0 + tx;
+      tile[k][tx] = (si < rows && sj < cols) ? src[(long)si * src_ld + sj] : 0.0f;
+    }
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int di = i0 + k, dj = j0 + tx;
+    if (di < rows_pad && dj < cols_pad) st_f<T>(dst + (long)di * dst_ld + dj, transpose ? tile[tx][k] : tile[k][tx]);
+  }
+}
+
+// Column sums, stage 1: partial[chunk][n] = sum of rows [chunk*R, (chunk+1)*R) (threads = columns,
+// so every row read is coalesced); stage 2 adds the chunks in order.  Fixed order: bitwise reproducible.
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ src, long ld, int M, int N,
+                                                             int R, float* __restrict__ partial) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (n >= N) return;
+  const int r0 = chunk * R, r1 = min(M, r0 + R);
+  float s = 0.0f;
+  for (int r = r0; r < r1; ++r) s += src[(long)r * ld + n];
+  partial[(long)chunk * N + n] = s;
+}
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int nchunks, int N,
+                                                           float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.0f;
+  for (int c = 0; c < nchunks; ++c) s += partial[(long)c * N + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+// LayerNorm backward, one wave per row (E4 float4 chunks per lane, d % 4 == 0):
+//   xhat = (x - mean) * rstd, g = dy * w
+//   dx   = rstd * (g - mean(g) - xhat * mean(g * xhat))       (+= dx_acc if accumulate)
+//   prod = dy * xhat  (rows, for dw = column sums)
+template <int E4>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ dy, int M, int d,
+                                                            float* __restrict__ dx, int accumulate,
+                                                            float* __restrict__ prod) {
+#pragma clang fp contract(off)
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int d4 = d >> 2;
+  const float4* xr = (const float4*)(x + (long)row * d);
+  const float4* dr = (const float4*)(dy + (long)row * d);
+  const float4* wr = (const float4*)w;
+  float4 xv[E4], dv[E4], wv[E4];
+  float s = 0.0f;
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    const int g = min(lane + 64 * e, d4 - 1);
+    const bool ok = lane + 64 * e < d4;
+    xv[e] = ok ? xr[g] : make_float4(0, 0, 0, 0);
+    dv[e] = ok ? dr[g] : make_float4(0, 0, 0, 0);
+    wv[e] = wr[g];
+    s += xv[e].x + xv[e].y + xv[e].z + xv[e].w;
+  }
+  const float inv_d = 1.0f / (float)d;
+  const float mean = wave_sum(s) * inv_d;
+  float q = 0.0f;
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    if (lane + 64 * e < d4) {
+      const float a0 = xv[e].x - mean, a1 = xv[e].y - mean, a2 = xv[e].z - mean, a3 = xv[e].w - mean;
+      q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * inv_d + 1e-5f);
+  float sg = 0.0f, sgx = 0.0f;
+  float4 xh[E4], gv[E4];
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    xh[e] = make_float4((xv[e].x - mean) * rstd, (xv[e].y - mean) * rstd, (xv[e].z - mean) * rstd,
+                        (xv[e].w - mean) * rstd);
+    gv[e] = make_float4(dv[e].x * wv[e].x, dv[e].y * wv[e].y, dv[e].z * wv[e].z, dv[e].w * wv[e].w);
+    if (lane + 64 * e < d4) {
+      sg += gv[e].x + gv[e].y + gv[e].z + gv[e].w;
+      sgx += gv[e].x * xh[e].x + gv[e].y * xh[e].y + gv[e].z * xh[e].z + gv[e].w * xh[e].w;
+    }
+  }
+  const float mg = wave_sum(sg) * inv_d, mgx = wave_sum(sgx) * inv_d;
+  float4* dxr = (float4*)(dx + (long)row * d);
+  float4* pr = (float4*)(prod + (long)row * d);
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    const int g = lane + 64 * e;
+    if (g < d4) {
+      float4 o = make_float4(rstd * (gv[e].x - mg - xh[e].x * mgx), rstd * (gv[e].y - mg - xh[e].y * mgx),
+                             rstd * (gv[e].z - mg - xh[e].z * mgx), rstd * (gv[e].w - mg - xh[e].w * mgx));
+      if (accumulate) {
+        const float4 a = dxr[g];
+        o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+      }
+      dxr[g] = o;
+      pr[g] = make_float4(dv[e].x * xh[e].x, dv[e].y * xh[e].y, dv[e].z * xh[e].z, dv[e].w * xh[e].w);
+    }
+  }
+}
+
+// dz = du * swish'(z),  swish'(z) = s + z * s * (1 - s), s = sigmoid(z)   (exact sigmoid)
+__global__ __launch_bounds__(256) void swish_bwd_kernel(const float* __restrict__ z, const float* __restrict__ du,
+                                                        float* __restrict__ dz, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float zz = z[i];
+    const float s = 1.0f / (1.0f + expf(-zz));
+    dz[i] = du[i] * (s + zz * s * (1.0f - s));
+  }
+}
+
+}  // namespace
+
+void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, bool transpose, void* dst, long dst_ld,
+                 int rows_pad, int cols_pad, hipStream_t st) {
+  if (rows_pad <= 0 || cols_pad <= 0) return;
+  const dim3 grid((cols_pad + 31) / 32, (rows_pad + 31) / 32), block(256);
+  if (dtype == DT_F32)
+    cfm_launch(pack_kernel<float>, grid, block, 0, st, src, src_ld, rows, cols, (int)transpose, (float*)dst, dst_ld,
+               rows_pad, cols_pad);
+  else
+    cfm_launch(pack_kernel<bf16_t>, grid, block, 0, st, src, src_ld, rows, cols, (int)transpose, (bf16_t*)dst, dst_ld,
+               rows_pad, cols_pad);
+}
+
+size_t col_sums_ws(int M, int N) {
+  const int R = 64, nchunks = (M + R - 1) / R;
+  return (size_t)nchunks * N * 4;
+}
+
+void col_sums(const float* src, long ld, int M, int N, float* out, int accumulate, float* ws, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  const int R = 64, nchunks = (M + R - 1) / R;
+  cfm_launch(colsum_partial_kernel, dim3((N + 255) / 256, nchunks), dim3(256), 0, st, src, ld, M, N, R, ws);
+  cfm_launch(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, (const float*)ws, nchunks, N, out, accumulate);
+}
+
+void layernorm_backward(const float* x, const float* w, const float* dy, int M, int d, float* dx, int accumulate,
+                        float* prod, hipStream_t st) {
+  if (M <= 0) return;
+  const dim3 grid((M + 3) / 4), block(256);
+  const int d4 = d / 4;
+  if (d4 <= 64) cfm_launch(layernorm_bwd_kernel<1>, grid, block, 0, st, x, w, dy, M, d, dx, accumulate, prod);
+  else if (d4 <= 128) cfm_launch(layernorm_bwd_kernel<2>, grid, block, 0, st, x, w, dy, M, d, dx, accumulate, prod);
+  else if (d4 <= 256) cfm_launch(layernorm_bwd_kernel<4>, grid, block, 0, st, x, w, dy, M, d, dx, accumulate, prod);
+  else cfm_launch(layernorm_bwd_kernel<8>, grid, block, 0, st, x, w, dy, M, d, dx, accumulate, prod);
+}
+
+void swish_backward(const float* z, const float* du, float* dz, long n, hipStream_t st) {
+  if (n <= 0) return;
+  cfm_launch(swish_bwd_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, st, z, du, dz, n);
+}
+
+}  // namespace cfm
+
+using namespace cfm;
+
+namespace {
+
+struct LinBwdWs {
+  long a1, wt, a2, b2, cs, total;
+  long Np64, Kp256, Mp, Kp;
+};
+
+LinBwdWs lin_bwd_ws(int dt, int M, int K, int N) {
+  LinBwdWs w;
+  const int es = dtype_size(dt);
+  const long kg = GEMM_BK_BYTES / es;
+  w.Np64 = round_up(N, kg);
+  w.Kp256 = round_up(K, GEMM_BN);
+  w.Kp = round_up(K, kg);
+  w.Mp = round_up(M, kg);
+  const long Np256 = round_up(N, GEMM_BN);
+  long off = 0;
+  auto take = [&](long bytes) { const long o = off; off = round_up(off + bytes, 256); return o; };
+  w.a1 = take((long)M * w.Np64 * es);        // dy rows            [M][Np64]
+  w.wt = take(w.Kp256 * w.Np64 * es);        // W^T                [Kp256][Np64]
+  w.a2 = take(Np256 * w.Mp * es);            // dy^T               [N][Mp]
+  w.b2 = take(w.Kp256 * w.Mp * es);          // x^T                [Kp256][Mp]
+  w.cs = take((long)col_sums_ws(M, N));
+  w.total = off + 4096;                      // + zero page
+  return w;
+}
+
+GemmEpi epi_out_f32(float* X, long ldx) {
+  GemmEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = EPI_SCALE_F32;
+  e.alpha = 1.0f;
+  e.X = X;
+  e.ldx = ldx;
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t cfm_op_layernorm_backward_ws_size(int rows, int d) {
+  return (size_t)round_up((long)rows * d * 4, 256) + col_sums_ws(rows, d) + 256;
+}
+
+cfm_status cfm_op_layernorm_backward(const float* x, int rows, int d, const float* w, const float* dy, float* dx,
+                                     int accumulate, float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!x || !w || !dy || !dx) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (d % 4 || d > 2048) fail(CFM_ERR_UNSUPPORTED, "d must be a multiple of 4 and <= 2048");
+    if (!ws || ws_bytes < cfm_op_layernorm_backward_ws_size(rows, d)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    float* prod = (float*)ws;
+    float* cs = (float*)((char*)ws + round_up((long)rows * d * 4, 256));
+    layernorm_backward(x, w, dy, rows, d, dx, accumulate, prod, st);
+    if (dw) col_sums(prod, d, rows, d, dw, 0, cs, st);
+    if (db) col_sums(dy, d, rows, d, db, 0, cs, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_op_linear_backward_ws_size(int dtype, int M, int K, int N) {
+  return (size_t)lin_bwd_ws(dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, M, K, N).total;
+}
+
+cfm_status cfm_op_linear_backward(int dtype, const float* x, int M, int K, const float* w, int N, const float* dy,
+                                  float* dx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!x || !w || !dy) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (M <= 0 || K <= 0 || N <= 0 || K % 4) fail(CFM_ERR_INVALID_ARG, "bad sizes (K % 4 == 0 required)");
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16;
+    const LinBwdWs l = lin_bwd_ws(dt, M, K, N);
+    if (!ws || ws_bytes < (size_t)l.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* b = (char*)ws;
+    char* zero = b + l.total - 4096;
+    HIP_OK(hipMemsetAsync(zero, 0, 4096, st));
+    if (dx) {   // dx (M, K) = dy (M, N) . W (N, K): A = dy rows, packed operand W^T [K][N]
+      pack_matrix(dt, dy, N, M, N, false, b + l.a1, l.Np64, M, (int)l.Np64, st);
+      pack_matrix(dt, w, K, N, K, true, b + l.wt, l.Np64, (int)l.Kp256, (int)l.Np64, st);
+      gemm(dt, b + l.a1, l.Np64, M, N, b + l.wt, (int)l.Np64, K, epi_out_f32(dx, K), zero, st);
+    }
+    if (dw) {   // dw (N, K) = dy^T (N, M) . x (M, K): A = dy^T [N][Mp], packed operand x^T [K][Mp]
+      pack_matrix(dt, dy, N, M, N, true, b + l.a2, l.Mp, N, (int)l.Mp, st);
+      pack_matrix(dt, x, K, M, K, true, b + l.b2, l.Mp, (int)l.Kp256, (int)l.Mp, st);
+      gemm(dt, b + l.a2, l.Mp, N, M, b + l.b2, (int)l.Mp, K, epi_out_f32(dw, K), zero, st);
+    }
+    if (db) col_sums(dy, N, M, N, db, 0, (float*)(b + l.cs), st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int64_t n, void* stream) {
+  return guarded([&] {
+    if (!z || !du || !dz) fail(CFM_ERR_INVALID_ARG, "null argument");
+    swish_backward(z, du, dz, n, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

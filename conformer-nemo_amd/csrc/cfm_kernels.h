@@ -103,4 +103,17 @@ void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
 
+// ---- backward building blocks (backward.hip) ----
+// dst[i][j] = transpose ? src[j][i] : src[i][j] in the compute type for i < rows_pad, j < cols_pad;
+// src is fp32 [rows][cols] (ld src_ld), zero outside it.
+void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, bool transpose, void* dst, long dst_ld,
+                 int rows_pad, int cols_pad, hipStream_t st);
+// out[n] (+)= sum_m src[m][n], fixed-order (bitwise reproducible); ws >= col_sums_ws(M, N) bytes.
+size_t col_sums_ws(int M, int N);
+void col_sums(const float* src, long ld, int M, int N, float* out, int accumulate, float* ws, hipStream_t st);
+// LayerNorm backward (one wave per row): dx (+)= ..., prod = dy * xhat (for the weight gradient).
+void layernorm_backward(const float* x, const float* w, const float* dy, int M, int d, float* dx, int accumulate,
+                        float* prod, hipStream_t st);
+void swish_backward(const float* z, const float* du, float* dz, long n, hipStream_t st);
+
 }  // namespace cfm

@@ -7,6 +7,7 @@
 //                 denc    = dlogits . W       (GEMM on packed W^T)
 //                 dW      = dlogits^T . enc   (GEMM on the transposed operands, K = B*T)
 //                 dbias   = column sums of dlogits (fixed-order reduction: deterministic)
+// The operand relayouts (pack_matrix) and column sums are shared with backward.hip.
 // CTC loss:       one wave per utterance walks the 2U+1 extended states (blank, l1, blank, l2, ...,
 //                 blank), states held in registers (SPL per lane, shuffles for the s-1/s-2 links):
 //                 alpha recursion forward (alphas kept in the workspace), beta recursion backward
@@ -45,32 +46,6 @@ CFM_DEV float wave_max(float v) {
 }
 
 // ---- relayouts -------------------------------------------------------------------------------
-
-// dst[i][j] (ld dst_ld, compute type) = transpose ? src[j][i] : src[i][j] for i < rows_pad,
-// j < cols_pad; src is fp32 [rows][cols] (ld src_ld); entries outside the source are 0.  32x32 tiles.
-template <typename T>
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, int src_ld, int rows, int cols,
-                                                   int transpose, T* __restrict__ dst, long dst_ld, int rows_pad,
-                                                   int cols_pad) {
-  __shared__ float tile[32][33];
-  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int k = ty; k < 32; k += 8) {
-    // source element for destination (i0 + a, j0 + b): transposed reads walk the source rows
-    if (transpose) {
-      const int si = j0 + k, sj = i0 + tx;   // src[si][sj] -> tile[k][tx] = dst(i0+tx, j0+k)
-      tile[k][tx] = (si < rows && sj < cols) ? src[(long)si * src_ld + sj] : 0.0f;
-    } else {
-      const int si = i0 + k, sj = j0 + tx;
-      tile[k][tx] = (si < rows && sj < cols) ? src[(long)si * src_ld + sj] : 0.0f;
-    }
-  }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int di = i0 + k, dj = j0 + tx;
-    if (di < rows_pad && dj < cols_pad) st_f<T>(dst + (long)di * dst_ld + dj, transpose ? tile[tx][k] : tile[k][tx]);
-  }
-}
 
 // (B, D, T) fp32 -> rows[(b*T + t)][d] (ld) compute type (the GEMM A operand of the head).
 template <typename T>
@@ -171,21 +146,6 @@ __global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const float* __res
     const int c = lane + 64 * i;
     if (c < C) g[(long)row * C + c] = dv[i] - expf(lv[i]) * s;
   }
-}
-
-// column sums of g (M x C): one block per column, fixed-order tree (bitwise reproducible)
-__global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ g, int M, int C, float* __restrict__ out) {
-  __shared__ float red[256];
-  const int c = blockIdx.x;
-  float s = 0.0f;
-  for (int m = threadIdx.x; m < M; m += 256) s += g[(long)m * C + c];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[c] = red[0];
 }
 
 // ---- CTC ---------------------------------------------------------------------------------------
@@ -406,7 +366,7 @@ struct cfm_ctc_head {
 namespace {
 
 struct HeadWs {
-  long rows, logits, gl, glp, glt, encT, xg, total;
+  long rows, logits, gl, glp, glt, encT, xg, cs, total;
   long M, Mp, ldl;
 };
 
@@ -424,6 +384,7 @@ HeadWs head_ws(const cfm_ctc_head* h, int B, int T) {
   w.glt = take((long)h->C * w.Mp * h->es);
   w.encT = take(h->Dp256 * w.Mp * h->es);
   w.xg = take(w.M * h->D * 4);
+  w.cs = take((long)col_sums_ws((int)w.M, h->C));
   w.total = off;
   return w;
 }
@@ -432,16 +393,6 @@ template <typename F>
 void by_dtype(int dt, F&& f) {
   if (dt == DT_F32) f(float{});
   else f(bf16_t{});
-}
-
-void pack(int dt, const float* src, int src_ld, int rows, int cols, bool transpose, void* dst, long dst_ld,
-          int rows_pad, int cols_pad, hipStream_t st) {
-  const dim3 grid((cols_pad + 31) / 32, (rows_pad + 31) / 32), block(256);
-  by_dtype(dt, [&](auto tag) {
-    using T = decltype(tag);
-    cfm_launch(pack_kernel<T>, grid, block, 0, st, src, src_ld, rows, cols, (int)transpose, (T*)dst, dst_ld,
-               rows_pad, cols_pad);
-  });
 }
 
 // f(std::integral_constant<int, CPL>) with CPL = classes per lane of a one-wave-per-row kernel
@@ -506,8 +457,8 @@ cfm_status cfm_ctc_head_set_weights(cfm_ctc_head* h, const float* weight, const 
   return guarded([&] {
     if (!h || !weight) fail(CFM_ERR_INVALID_ARG, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    pack(h->dtype, weight, h->D, h->C, h->D, false, h->w, h->Dp, (int)h->Cp256, (int)h->Dp, st);
-    pack(h->dtype, weight, h->D, h->C, h->D, true, h->wt, h->Cp64, (int)h->Dp256, (int)h->Cp64, st);
+    pack_matrix(h->dtype, weight, h->D, h->C, h->D, false, h->w, h->Dp, (int)h->Cp256, (int)h->Dp, st);
+    pack_matrix(h->dtype, weight, h->D, h->C, h->D, true, h->wt, h->Cp64, (int)h->Dp256, (int)h->Cp64, st);
     if (bias) HIP_OK(hipMemcpyAsync(h->bias, bias, (size_t)h->C * 4, hipMemcpyDeviceToDevice, st));
     else HIP_OK(hipMemsetAsync(h->bias, 0, (size_t)h->C * 4, st));
     HIP_OK(hipGetLastError());
@@ -563,17 +514,17 @@ cfm_status cfm_ctc_head_backward(cfm_ctc_head* h, const float* enc_bdt, int B, i
       cfm_launch(log_softmax_bwd_kernel<decltype(cpl)::value>, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, st,
                  logprobs_btc, grad_lp_btc, M, h->C, gl);
     });
-    if (grad_bias) cfm_launch(col_sum_kernel, dim3(h->C), dim3(256), 0, st, (const float*)gl, M, h->C, grad_bias);
+    if (grad_bias) col_sums(gl, h->C, M, h->C, grad_bias, 0, (float*)(ws + w.cs), st);
     if (grad_enc_bdt) {
       // denc rows (M, D) = gl (M, C) . W (C, D): A = gl rows, packed operand W^T [D][C]
-      pack(h->dtype, gl, h->C, M, h->C, false, ws + w.glp, h->Cp64, M, (int)h->Cp64, st);
+      pack_matrix(h->dtype, gl, h->C, M, h->C, false, ws + w.glp, h->Cp64, M, (int)h->Cp64, st);
       float* xg = (float*)(ws + w.xg);
       gemm(h->dtype, ws + w.glp, h->Cp64, M, h->C, h->wt, (int)h->Cp64, h->D, epi_f32(nullptr, xg, h->D), h->zero, st);
       transpose_out(xg, B, T, h->D, grad_enc_bdt, st);
     }
     if (grad_weight) {
       // dW (C, D) = gl^T (C, M) . enc (M, D): A = gl^T [C][Mp], packed operand enc^T [D][Mp]
-      pack(h->dtype, gl, h->C, M, h->C, true, ws + w.glt, w.Mp, h->C, (int)w.Mp, st);
+      pack_matrix(h->dtype, gl, h->C, M, h->C, true, ws + w.glt, w.Mp, h->C, (int)w.Mp, st);
       by_dtype(h->dtype, [&](auto tag) {
         using Tt = decltype(tag);
         cfm_launch(bdt_dm_kernel<Tt>, dim3((unsigned)std::min<long>((w.Mp + 255) / 256, 1024), (unsigned)h->Dp256),

@@ -30,7 +30,9 @@ def test_library_loads_and_exports_header_symbols():
         assert re.search(rf"\bT {name}\b", out), name
     ctc = _declared_symbols("cfm_ctc.h")
     assert set(ctc) == set(_lib.CTC_SYMBOLS)
-    for name in ctc:
+    train = _declared_symbols("cfm_train.h")
+    assert set(train) == set(_lib.TRAIN_SYMBOLS)
+    for name in ctc + train:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
