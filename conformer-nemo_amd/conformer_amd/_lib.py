@@ -28,7 +28,9 @@ EXPORTED_SYMBOLS = (
 # every symbol include/cfm_train.h declares
 TRAIN_SYMBOLS = (
     "cfm_op_layernorm_backward_ws_size", "cfm_op_layernorm_backward", "cfm_op_linear_backward_ws_size",
-    "cfm_op_linear_backward", "cfm_op_swish_backward",
+    "cfm_op_linear_backward", "cfm_op_swish_backward", "cfm_op_glu_backward", "cfm_op_dwconv_backward_ws_size",
+    "cfm_op_dwconv_backward", "cfm_op_batchnorm_train_ws_size", "cfm_op_batchnorm_train_forward",
+    "cfm_op_batchnorm_train_backward",
 )
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
@@ -96,6 +98,12 @@ def load() -> ctypes.CDLL:
         "cfm_op_linear_backward_ws_size": (sz, [ci, ci, ci, ci]),
         "cfm_op_linear_backward": (ci, [ci, vp, ci, ci, vp, ci, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_op_swish_backward": (ci, [vp, vp, vp, ctypes.c_int64, vp]),
+        "cfm_op_glu_backward": (ci, [vp, vp, vp, ci, ci, ci, vp, vp]),
+        "cfm_op_dwconv_backward_ws_size": (sz, [ci, ci, ci, ci]),
+        "cfm_op_dwconv_backward": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, vp, sz, vp]),
+        "cfm_op_batchnorm_train_ws_size": (sz, [ci, ci]),
+        "cfm_op_batchnorm_train_forward": (ci, [vp, ci, ci, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "cfm_op_batchnorm_train_backward": (ci, [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

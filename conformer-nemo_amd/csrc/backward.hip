@@ -140,6 +140,149 @@ __global__ __launch_bounds__(256) void swish_bwd_kernel(const float* __restrict_
   }
 }
 
+// ---- convolution module (conformer_modules.py:160-180) ---------------------------------------
+
+// GLU(dim=1) + pad mask backward: pre (rows, 2d) = [a | g] (pointwise_conv1 output, channels-last),
+// dy (rows, d) = d(masked GLU output).  Padded frames (t >= len[b]) were zeroed after the GLU, so
+// their gradient is 0.  dpre = [dy * sigmoid(g) | dy * a * sigmoid(g) * (1 - sigmoid(g))].
+__global__ __launch_bounds__(256) void glu_bwd_kernel(const float* __restrict__ pre, const float* __restrict__ dy,
+                                                      const int32_t* __restrict__ lens, int Tp, int d, long rows,
+                                                      float* __restrict__ dpre) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long m = i / d;
+    const int c = (int)(i - m * d);
+    const int b = (int)(m / Tp), t = (int)(m - (long)b * Tp);
+    const float g = pre[m * 2 * d + d + c], a = pre[m * 2 * d + c];
+    const float s = 1.0f / (1.0f + expf(-g));
+    const float dv = (lens && t >= lens[b]) ? 0.0f : dy[i];
+    dpre[m * 2 * d + c] = dv * s;
+    dpre[m * 2 * d + d + c] = dv * a * s * (1.0f - s);
+  }
+}
+
+// Depthwise Conv1d(k, pad (k-1)/2, groups=d) input gradient (the forward's cross-correlation with
+// the kernel flipped): dx[b,t,c] = sum_k w[c][k] * dy[b, t - k + pad, c].  w is the reference
+// (d, 1, k) weight.  Thread = channel, 32 frames per block, register window.
+template <int K, int DT>
+__global__ __launch_bounds__(256) void dwconv_bwd_x_kernel(const float* __restrict__ dy, const float* __restrict__ w,
+                                                           int Tp, int d, float* __restrict__ dx) {
+  constexpr int PAD = (K - 1) / 2, NX = DT + K - 1;
+  const int c = blockIdx.y * 256 + threadIdx.x, b = blockIdx.z, t0 = blockIdx.x * DT;
+  if (c >= d) return;
+  const float* yc = dy + (long)b * Tp * d + c;
+  float y[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {   // y[i] = dy[t0 - PAD + i]
+    const int t = t0 - PAD + i;
+    const float v = yc[(long)min(max(t, 0), Tp - 1) * d];
+    y[i] = (t >= 0 && t < Tp) ? v : 0.0f;
+  }
+  float wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = w[(long)c * K + k];
+#pragma unroll
+  for (int j = 0; j < DT; ++j) {
+    float a = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) a = fmaf(wk[k], y[j + 2 * PAD - k], a);   // dy[t0 + j - k + PAD]
+    const int t = t0 + j;
+    if (t < Tp) dx[((long)b * Tp + t) * d + c] = a;
+  }
+}
+
+// Depthwise weight gradient, stage 1: partial[b * nt + tile][k][c] = sum over the tile's frames t of
+// x[b, t + k - pad, c] * dy[b, t, c]  (x = the conv input, zero outside [0, T')).
+template <int K, int DT>
+__global__ __launch_bounds__(256) void dwconv_bwd_w_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                           int Tp, int d, float* __restrict__ partial) {
+  constexpr int PAD = (K - 1) / 2, NX = DT + K - 1;
+  const int c = blockIdx.y * 256 + threadIdx.x, b = blockIdx.z, t0 = blockIdx.x * DT;
+  if (c >= d) return;
+  const float* xc = x + (long)b * Tp * d + c;
+  const float* yc = dy + (long)b * Tp * d + c;
+  float xv[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {   // xv[i] = x[t0 - PAD + i]
+    const int t = t0 - PAD + i;
+    const float v = xc[(long)min(max(t, 0), Tp - 1) * d];
+    xv[i] = (t >= 0 && t < Tp) ? v : 0.0f;
+  }
+  float acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < DT; ++j) {
+    const int t = t0 + j;
+    const float g = yc[(long)min(t, Tp - 1) * d];
+    const float gv = t < Tp ? g : 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = fmaf(xv[j + k], gv, acc[k]);
+  }
+  float* pc = partial + ((long)(b * gridDim.x + blockIdx.x) * K) * d + c;
+#pragma unroll
+  for (int k = 0; k < K; ++k) pc[(long)k * d] = acc[k];
+}
+
+// BatchNorm1d (train mode, statistics over every (b, t) incl. padded frames, as nn.BatchNorm1d on
+// (B, C, T)): y = (x - mean) * rstd * gamma + beta and xhat for the backward.
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, const float* __restrict__ gam,
+                                                       const float* __restrict__ bet, long rows, int d,
+                                                       float* __restrict__ y, float* __restrict__ xhat) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % d);
+    const float h = (x[i] - mean[c]) * rstd[c];
+    if (xhat) xhat[i] = h;
+    y[i] = h * gam[c] + bet[c];
+  }
+}
+// per channel: mean = s1 / n, var = s2 / n (s2 = sum (x - mean)^2), rstd, running stats update
+__global__ void bn_stats_kernel(const float* __restrict__ s1, const float* __restrict__ s2, long n, int d,
+                                float momentum, float* __restrict__ mean, float* __restrict__ rstd,
+                                float* __restrict__ run_mean, float* __restrict__ run_var, int pass) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  if (pass == 0) {
+    mean[c] = s1[c] / (float)n;
+  } else {
+    const float var = s2[c] / (float)n;
+    rstd[c] = 1.0f / sqrtf(var + 1e-5f);
+    if (run_mean) {
+      run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * mean[c];
+      run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void sq_dev_kernel(const float* __restrict__ x, const float* __restrict__ mean, long rows,
+                                                     int d, float* __restrict__ out) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float v = x[i] - mean[i % d];
+    out[i] = v * v;
+  }
+}
+// BatchNorm backward given the column sums sdy = sum dy, sdyx = sum dy * xhat over the n rows:
+//   dx = gamma * rstd * (dy - sdy / n - xhat * sdyx / n)
+__global__ __launch_bounds__(256) void bn_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                                     const float* __restrict__ gam, const float* __restrict__ rstd,
+                                                     const float* __restrict__ sdy, const float* __restrict__ sdyx,
+                                                     long rows, int d, float* __restrict__ dx) {
+  const long n = rows * d;
+  const float inv = 1.0f / (float)rows;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % d);
+    dx[i] = gam[c] * rstd[c] * (dy[i] - sdy[c] * inv - xhat[i] * sdyx[c] * inv);
+  }
+}
+__global__ __launch_bounds__(256) void mul_kernel(const float* __restrict__ a, const float* __restrict__ b, long n,
+                                                  float* __restrict__ out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = a[i] * b[i];
+}
+
+unsigned ew_grid(long n) { return (unsigned)std::min<long>((n + 255) / 256, 8192); }
+
 }  // namespace
 
 void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, bool transpose, void* dst, long dst_ld,
@@ -226,6 +369,102 @@ GemmEpi epi_out_f32(float* X, long ldx) {
 }  // namespace
 
 extern "C" {
+
+cfm_status cfm_op_glu_backward(const float* pre, const float* dy, const int32_t* lens, int B, int Tp, int d, float* dpre,
+                               void* stream) {
+  return guarded([&] {
+    if (!pre || !dy || !dpre) fail(CFM_ERR_INVALID_ARG, "null argument");
+    const long rows = (long)B * Tp;
+    cfm_launch(glu_bwd_kernel, dim3(ew_grid(rows * d)), dim3(256), 0, (hipStream_t)stream, pre, dy, lens, Tp, d, rows,
+               dpre);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_op_dwconv_backward_ws_size(int B, int Tp, int d, int K) {
+  const long nt = (Tp + 31) / 32;
+  return (size_t)round_up((long)B * nt * K * d * 4, 256) +
+         std::max(col_sums_ws((int)(B * nt), K * d), col_sums_ws(B * Tp, d)) + 256;
+}
+
+cfm_status cfm_op_dwconv_backward(const float* x, const float* w, const float* dy, int B, int Tp, int d, int K,
+                                  float* dx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!x || !w || !dy) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (K != 31) fail(CFM_ERR_UNSUPPORTED, "depthwise backward is built for kernel size 31");
+    if (!ws || ws_bytes < cfm_op_dwconv_backward_ws_size(B, Tp, d, K)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    constexpr int DT = 32;
+    const int nt = (Tp + DT - 1) / DT;
+    const dim3 grid(nt, (d + 255) / 256, B), block(256);
+    if (dx) cfm_launch(dwconv_bwd_x_kernel<31, DT>, grid, block, 0, st, dy, w, Tp, d, dx);
+    float* part = (float*)ws;
+    float* cs = (float*)((char*)ws + round_up((long)B * nt * K * d * 4, 256));
+    if (dw) {
+      cfm_launch(dwconv_bwd_w_kernel<31, DT>, grid, block, 0, st, x, dy, Tp, d, part);
+      // dw[c][k] = sum over the B * nt partial blocks of partial[blk][k][c]: column sums of a
+      // (B*nt) x (K*d) matrix, then the [k][c] result transposed to the reference (d, 1, K) layout
+      col_sums(part, (long)K * d, B * nt, K * d, part + (long)B * nt * K * d - (long)K * d, 0, cs, st);
+      pack_matrix(DT_F32, part + (long)B * nt * K * d - (long)K * d, d, K, d, true, dw, K, d, K, st);
+    }
+    if (db) col_sums(dy, d, B * Tp, d, db, 0, cs, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_op_batchnorm_train_ws_size(int rows, int d) {
+  return (size_t)round_up((long)rows * d * 4, 256) + 4 * round_up((long)d * 4, 256) + col_sums_ws(rows, d) + 256;
+}
+
+cfm_status cfm_op_batchnorm_train_forward(const float* x, int rows, int d, const float* gamma, const float* beta,
+                                          float momentum, float* run_mean, float* run_var, float* y, float* xhat,
+                                          float* mean, float* rstd, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!x || !gamma || !beta || !y || !mean || !rstd) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!ws || ws_bytes < cfm_op_batchnorm_train_ws_size(rows, d)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* b = (char*)ws;
+    float* tmp = (float*)b;
+    float* s1 = (float*)(b + round_up((long)rows * d * 4, 256));
+    float* s2 = (float*)((char*)s1 + round_up((long)d * 4, 256));
+    float* cs = (float*)((char*)s2 + round_up((long)d * 4, 256));
+    const long n = (long)rows * d;
+    col_sums(x, d, rows, d, s1, 0, cs, st);
+    cfm_launch(bn_stats_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)s1, (const float*)s2,
+               (long)rows, d, momentum, mean, rstd, run_mean, run_var, 0);
+    cfm_launch(sq_dev_kernel, dim3(ew_grid(n)), dim3(256), 0, st, x, (const float*)mean, (long)rows, d, tmp);
+    col_sums(tmp, d, rows, d, s2, 0, cs, st);
+    cfm_launch(bn_stats_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)s1, (const float*)s2,
+               (long)rows, d, momentum, mean, rstd, run_mean, run_var, 1);
+    cfm_launch(bn_apply_kernel, dim3(ew_grid(n)), dim3(256), 0, st, x, (const float*)mean, (const float*)rstd, gamma,
+               beta, (long)rows, d, y, xhat);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+cfm_status cfm_op_batchnorm_train_backward(const float* dy, const float* xhat, int rows, int d, const float* gamma,
+                                           const float* rstd, float* dx, float* dgamma, float* dbeta, void* ws,
+                                           size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!dy || !xhat || !gamma || !rstd || !dx) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!ws || ws_bytes < cfm_op_batchnorm_train_ws_size(rows, d)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* b = (char*)ws;
+    float* tmp = (float*)b;
+    float* sdy = (float*)(b + round_up((long)rows * d * 4, 256));
+    float* sdyx = (float*)((char*)sdy + round_up((long)d * 4, 256));
+    float* cs = (float*)((char*)sdyx + 3 * round_up((long)d * 4, 256));
+    const long n = (long)rows * d;
+    col_sums(dy, d, rows, d, sdy, 0, cs, st);
+    cfm_launch(mul_kernel, dim3(ew_grid(n)), dim3(256), 0, st, dy, xhat, n, tmp);
+    col_sums(tmp, d, rows, d, sdyx, 0, cs, st);
+    if (dgamma) HIP_OK(hipMemcpyAsync(dgamma, sdyx, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+    if (dbeta) HIP_OK(hipMemcpyAsync(dbeta, sdy, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+    cfm_launch(bn_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, st, dy, xhat, gamma, rstd, (const float*)sdy,
+               (const float*)sdyx, (long)rows, d, dx);
+    HIP_OK(hipGetLastError());
+  });
+}
 
 size_t cfm_op_layernorm_backward_ws_size(int rows, int d) {
   return (size_t)round_up((long)rows * d * 4, 256) + col_sums_ws(rows, d) + 256;

@@ -6,6 +6,8 @@
  *   LayerNorm  (conformer_modules.py:73-77 norm_* = nn.LayerNorm(d_model), eps 1e-5)
  *   nn.Linear  (ConformerFeedForward.linear1/2, conformer_modules.py:189-191; attention projections)
  *   Swish      (activations.py:20: x * sigmoid(x))
+ *   ConformerConvolution pieces (conformer_modules.py:160-180): GLU + pad mask, depthwise Conv1d,
+ *   BatchNorm1d in training mode
  * All tensors are fp32 device pointers; the gradient GEMMs run in `dtype` (CFM_COMPUTE_FP32 or
  * CFM_COMPUTE_BF16 operands, fp32 accumulation).  Weight/bias gradients are deterministic
  * (fixed-order reductions).  Conventions as in cfm_encoder.h.
@@ -33,6 +35,27 @@ cfm_status cfm_op_layernorm_backward(const float* x, int rows, int d, const floa
 size_t cfm_op_linear_backward_ws_size(int dtype, int M, int K, int N);
 cfm_status cfm_op_linear_backward(int dtype, const float* x, int M, int K, const float* w, int N, const float* dy,
                                   float* dx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- convolution module (ConformerConvolution.forward, conformer_modules.py:160-180) ---- */
+/* GLU(dim=1) + pad-mask backward: pre (B*T', 2d) = pointwise_conv1 output [a | g] (channels-last),
+ * dy (B*T', d); frames t >= lens[b] get zero gradient (lens may be NULL).  -> dpre (B*T', 2d). */
+cfm_status cfm_op_glu_backward(const float* pre, const float* dy, const int32_t* lens, int B, int Tp, int d, float* dpre,
+                               void* stream);
+/* Depthwise Conv1d(k=31, pad 15, groups=d) backward on channels-last (B, T', d) tensors; w is the
+ * reference (d, 1, K) weight.  dx, dw (d, 1, K), db (d) may each be NULL. */
+size_t cfm_op_dwconv_backward_ws_size(int B, int Tp, int d, int K);
+cfm_status cfm_op_dwconv_backward(const float* x, const float* w, const float* dy, int B, int Tp, int d, int K,
+                                  float* dx, float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+/* BatchNorm1d in training mode over rows = B*T' frames (padded frames included, as the reference):
+ * y = xhat * gamma + beta with batch statistics; saves xhat (rows, d), mean, rstd (d); updates
+ * run_mean / run_var (momentum, unbiased variance) unless NULL.  Backward from xhat and rstd. */
+size_t cfm_op_batchnorm_train_ws_size(int rows, int d);
+cfm_status cfm_op_batchnorm_train_forward(const float* x, int rows, int d, const float* gamma, const float* beta,
+                                          float momentum, float* run_mean, float* run_var, float* y, float* xhat,
+                                          float* mean, float* rstd, void* ws, size_t ws_bytes, void* stream);
+cfm_status cfm_op_batchnorm_train_backward(const float* dy, const float* xhat, int rows, int d, const float* gamma,
+                                           const float* rstd, float* dx, float* dgamma, float* dbeta, void* ws,
+                                           size_t ws_bytes, void* stream);
 
 /* dz = du * swish'(z) elementwise (n elements). */
 cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int64_t n, void* stream);

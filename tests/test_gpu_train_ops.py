@@ -50,7 +50,8 @@ def test_ffn_block_backward(compute):
     du, dw2, db2 = linear_backward(lib, dt, _t(z["u"]), _t(z["w2"]), dy_ffn)
     # Swish
     dzv = torch.empty_like(du)
-    _lib.check(lib.cfm_op_swish_backward(_t(z["z"]).data_ptr(), du.data_ptr(), dzv.data_ptr(), du.numel(), _st()),
+    zz = _t(z["z"])
+    _lib.check(lib.cfm_op_swish_backward(zz.data_ptr(), du.data_ptr(), dzv.data_ptr(), du.numel(), _st()),
                "swish_backward")
     # linear1
     dhn, dw1, db1 = linear_backward(lib, dt, _t(z["hn"]), _t(z["w1"]), dzv)
@@ -61,7 +62,8 @@ def test_ffn_block_backward(compute):
     dlnw, dlnb = torch.empty(d, device="cuda"), torch.empty(d, device="cuda")
     n = lib.cfm_op_layernorm_backward_ws_size(M, d)
     ws = torch.empty(n, dtype=torch.uint8, device="cuda")
-    _lib.check(lib.cfm_op_layernorm_backward(x.data_ptr(), M, d, _t(z["ln_w"]).data_ptr(), dhn.data_ptr(),
+    ln_w = _t(z["ln_w"])    # keep every tensor whose pointer is passed alive across the call
+    _lib.check(lib.cfm_op_layernorm_backward(x.data_ptr(), M, d, ln_w.data_ptr(), dhn.data_ptr(),
                                              dx.data_ptr(), 1, dlnw.data_ptr(), dlnb.data_ptr(), ws.data_ptr(), n,
                                              _st()), "layernorm_backward")
     torch.cuda.synchronize()
@@ -86,3 +88,70 @@ def test_linear_backward_deterministic_ragged():
     assert rel_l2(a[0], (dyd @ wd).numpy()) <= 1e-5
     assert rel_l2(a[1], (dyd.T @ xd).numpy()) <= 1e-5
     assert rel_l2(a[2], dyd.sum(0).numpy()) <= 1e-5
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_conv_module_backward(compute):
+    """ConformerConvolution in training mode (tests/golden/bwd_conv.npz): BatchNorm batch statistics
+    and running-stat update, then the whole backward chain pw2 -> Swish -> BN -> depthwise -> GLU+mask
+    -> pw1 from the native ops."""
+    from conformer_amd import _lib
+    lib = _lib.load()
+    z = np.load(os.path.join(GOLDEN, "bwd_conv.npz"))
+    dt = DT[compute]
+    g = GATE[compute]
+    B, T = int(z["B"]), int(z["T"])
+    M, d = z["x"].shape
+    # BatchNorm forward (train) on the depthwise output
+    h = _t(z["h"])
+    y, xhat = torch.empty_like(h), torch.empty_like(h)
+    mean, rstd = torch.empty(d, device="cuda"), torch.empty(d, device="cuda")
+    rm, rv = _t(z["bn_rm0"]), _t(z["bn_rv0"])
+    n = lib.cfm_op_batchnorm_train_ws_size(M, d)
+    ws = torch.empty(n, dtype=torch.uint8, device="cuda")
+    bn_w, bn_b = _t(z["bn_w"]), _t(z["bn_b"])
+    _lib.check(lib.cfm_op_batchnorm_train_forward(h.data_ptr(), M, d, bn_w.data_ptr(),
+                                                  bn_b.data_ptr(), float(z["bn_momentum"]), rm.data_ptr(),
+                                                  rv.data_ptr(), y.data_ptr(), xhat.data_ptr(), mean.data_ptr(),
+                                                  rstd.data_ptr(), ws.data_ptr(), n, _st()), "bn_forward")
+    torch.cuda.synchronize()
+    assert rel_l2(y.cpu().numpy(), z["bn"]) <= 1e-5
+    assert rel_l2(rm.cpu().numpy(), z["bn_rm1"]) <= 1e-5 and rel_l2(rv.cpu().numpy(), z["bn_rv1"]) <= 1e-5
+    # backward chain
+    bn = z["bn"].astype(np.float64)
+    s = (bn / (1.0 + np.exp(-bn))).astype(np.float32)
+    ds, dw2, db2 = linear_backward(lib, dt, _t(s), _t(z["pw2_w"]), _t(z["dout"]))
+    dbn = torch.empty_like(ds)
+    bn_t = _t(z["bn"])
+    _lib.check(lib.cfm_op_swish_backward(bn_t.data_ptr(), ds.data_ptr(), dbn.data_ptr(), dbn.numel(), _st()),
+               "swish_backward")
+    dh, dgam, dbet = torch.empty_like(dbn), torch.empty(d, device="cuda"), torch.empty(d, device="cuda")
+    _lib.check(lib.cfm_op_batchnorm_train_backward(dbn.data_ptr(), xhat.data_ptr(), M, d, bn_w.data_ptr(),
+                                                   rstd.data_ptr(), dh.data_ptr(), dgam.data_ptr(), dbet.data_ptr(),
+                                                   ws.data_ptr(), n, _st()), "bn_backward")
+    dglu, ddw, ddb = torch.empty_like(dh), torch.empty(d, 1, 31, device="cuda"), torch.empty(d, device="cuda")
+    n2 = lib.cfm_op_dwconv_backward_ws_size(B, T, d, 31)
+    ws2 = torch.empty(n2, dtype=torch.uint8, device="cuda")
+    glu_t, dw_w = _t(z["glu"]), _t(z["dw_w"])
+    _lib.check(lib.cfm_op_dwconv_backward(glu_t.data_ptr(), dw_w.data_ptr(), dh.data_ptr(), B, T, d,
+                                          31, dglu.data_ptr(), ddw.data_ptr(), ddb.data_ptr(), ws2.data_ptr(), n2,
+                                          _st()), "dwconv_backward")
+    dpre = torch.empty(M, 2 * d, device="cuda")
+    lens = torch.from_numpy(z["lens"]).cuda()
+    pre_t = _t(z["pre"])
+    _lib.check(lib.cfm_op_glu_backward(pre_t.data_ptr(), dglu.data_ptr(), lens.data_ptr(), B, T, d,
+                                       dpre.data_ptr(), _st()), "glu_backward")
+    dx, dw1, db1 = linear_backward(lib, dt, _t(z["x"]), _t(z["pw1_w"]), dpre)
+    torch.cuda.synchronize()
+    for name, got, gate in [("d_pw2_w", dw2, g), ("d_pw2_b", db2, 1e-4), ("d_bn", dbn, g), ("d_h", dh, g),
+                            ("d_bn_w", dgam, g), ("d_bn_b", dbet, g), ("d_dw_w", ddw, g),
+                            ("d_pre", dpre, g), ("d_x", dx, g), ("d_pw1_w", dw1, g), ("d_pw1_b", db1, g)]:
+        e = rel_l2(got.cpu().numpy(), z[name])
+        assert e <= gate, f"{name}: relL2 {e:.3e} > {gate}"
+    # d_dw_b = sum_t d_h, and train-mode BatchNorm makes every column of d_h sum to zero: the golden is
+    # rounding noise (~1e-6), so relL2 on it is meaningless.  Check it is the column sum of our d_h
+    # (fp32 accumulation bound), and that both sides are at noise level against |d_h|.
+    dh64 = dh.double().cpu().numpy()
+    scale = np.sqrt(M) * np.sqrt((dh64 ** 2).mean(0)).max()
+    np.testing.assert_allclose(ddb.cpu().numpy(), dh64.sum(0), rtol=0, atol=1e-5 * scale)
+    assert np.abs(z["d_dw_b"]).max() <= 1e-4 * scale and np.abs(ddb.cpu().numpy()).max() <= 1e-4 * scale
