@@ -30,7 +30,7 @@ TRAIN_SYMBOLS = (
     "cfm_op_layernorm_backward_ws_size", "cfm_op_layernorm_backward", "cfm_op_linear_backward_ws_size",
     "cfm_op_linear_backward", "cfm_op_swish_backward", "cfm_op_glu_backward", "cfm_op_dwconv_backward_ws_size",
     "cfm_op_dwconv_backward", "cfm_op_batchnorm_train_ws_size", "cfm_op_batchnorm_train_forward",
-    "cfm_op_batchnorm_train_backward",
+    "cfm_op_batchnorm_train_backward", "cfm_op_rel_attention_backward_ws_size", "cfm_op_rel_attention_backward",
 )
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
@@ -104,6 +104,9 @@ def load() -> ctypes.CDLL:
         "cfm_op_batchnorm_train_ws_size": (sz, [ci, ci]),
         "cfm_op_batchnorm_train_forward": (ci, [vp, ci, ci, vp, vp, ctypes.c_float, vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_op_batchnorm_train_backward": (ci, [vp, vp, ci, ci, vp, vp, vp, vp, vp, vp, sz, vp]),
+        "cfm_op_rel_attention_backward_ws_size": (sz, [ci, ci, ci, ci, ci]),
+        "cfm_op_rel_attention_backward": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp, vp,
+                                               vp, vp, vp, vp, sz, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

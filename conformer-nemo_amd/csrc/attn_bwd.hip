@@ -1,0 +1,350 @@
+// Backward of the relative-position multi-head attention (RelPositionMultiHeadAttention.forward,
+// multi_head_attention.py:172-210 with forward_attention :94-115), SURVEY §8 row a16.
+//
+// Operands are the forward's own layouts (cfm_kernels.h): qk = [(q+u)c | (q+v)c | k] per row with
+// c = log2(e)/sqrt(dk), V transposed per (b, h) in Vt, and p = linear_pos(pos_emb) per head.
+// The T' x T' score matrices are materialised per (b, h) in fp32 (B*H*T'^2*4 bytes: 64 MB at
+// BASELINE config 3) and every contraction runs on one batched MFMA GEMM (`bgemm`, LDS-staged,
+// any operand orientation):
+//   S  = (q+u)c . k^T            BD = (q+v)c . p^T          (log2 units, as the forward)
+//   P  = softmax_j(S[i][j] + BD[i][T'-1-i+j]) with the pad / context mask      (rel_shift :159-170)
+//   dP = dctx . V^T,   dS = P * (dP - rowsum(P * dP))                          (natural-log units)
+//   G[i][r] = dS[i][r - (T'-1-i)]   (rel_shift undone: the gradient on the raw BD matrix)
+//   d(q+u) = dS . k / sqrt(dk)      dk = dS^T . (q+u)c * ln2      dv = P^T . dctx
+//   d(q+v) = G . p / sqrt(dk)       dp = sum_b G^T . (q+v)c * ln2
+//   dq = d(q+u) + d(q+v);  d pos_bias_u = sum_rows d(q+u);  d pos_bias_v = sum_rows d(q+v)
+// Masked scores get zero gradient: the reference fills them with -10000 before the softmax and
+// zeroes their probabilities after it (:106-107), so both paths into them carry no gradient.
+#include <cmath>
+
+#include "../../include/cfm_train.h"
+#include "cfm_abi.h"
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+namespace cfm {
+namespace {
+
+struct BgArgs {
+  const void* A; long am, ak, az1, az2;   // A(m, k) at A + z1*az1 + z2*az2 + m*am + k*ak
+  const void* B; long bk, bn, bz1, bz2;   // B(k, n)
+  float* C; long cm, cn, cz1, cz2;        // C(m, n) fp32
+  int M, N, K, Z2;                        // batch z = blockIdx.z = z1 * Z2 + z2
+  float alpha; int accumulate;
+};
+
+// C = alpha * A.B (+ C).  64x64 output tile per 4-wave block (2x2 waves of 32x32 MFMA tiles), K in
+// steps of 32 staged through LDS as [row][k] images in the compute type T, so either operand
+// orientation is read coalesced from HBM (consecutive threads walk whichever stride is 1).  The
+// next K-step's global loads are in flight while the current step's MFMAs run.
+template <typename TA, typename TB, typename T>
+__global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
+  constexpr int RB = 32 * (int)sizeof(T) + 16;   // LDS row: 32 k values + 16 B pad
+  __shared__ __attribute__((aligned(16))) char As[64 * RB];
+  __shared__ __attribute__((aligned(16))) char Bs[64 * RB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int z = blockIdx.z, z1 = z / a.Z2, z2 = z - z1 * a.Z2;
+  const TA* A = (const TA*)a.A + z1 * a.az1 + z2 * a.az2;
+  const TB* Bm = (const TB*)a.B + z1 * a.bz1 + z2 * a.bz2;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const bool a_kc = a.ak == 1, b_kc = a.bk == 1;
+  float ra[8], rb[8];
+  auto coord = [&](bool kc, int e, int& r, int& k) {
+    const int idx = e * 256 + tid;
+    if (kc) { k = idx & 31; r = idx >> 5; } else { r = idx & 63; k = idx >> 6; }
+  };
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int r, k;
+      coord(a_kc, e, r, k);
+      const int gm = m0 + r, gk = k0 + k;
+      ra[e] = (gm < a.M && gk < a.K) ? ld_f<TA>(A + gm * a.am + gk * a.ak) : 0.0f;
+      coord(b_kc, e, r, k);
+      const int gn = n0 + r, gk2 = k0 + k;
+      rb[e] = (gn < a.N && gk2 < a.K) ? ld_f<TB>(Bm + gk2 * a.bk + gn * a.bn) : 0.0f;
+    }
+  };
+  f32x16 acc = {};
+  const int wm = w & 1, wn = w >> 1;
+  const char* ap = As + (wm * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
+  const char* bp = Bs + (wn * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
+  load(0);
+  for (int k0 = 0; k0 < a.K; k0 += 32) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int r, k;
+      coord(a_kc, e, r, k);
+      st_f<T>((T*)(As + r * RB) + k, ra[e]);
+      coord(b_kc, e, r, k);
+      st_f<T>((T*)(Bs + r * RB) + k, rb[e]);
+    }
+    __syncthreads();
+    if (k0 + 32 < a.K) load(k0 + 32);
+#pragma unroll
+    for (int s = 0; s < (int)sizeof(T); ++s)
+      mfma_slab<T>(acc, *(const uint4*)(ap + 32 * s), *(const uint4*)(bp + 32 * s));
+  }
+  float* C = a.C + z1 * a.cz1 + z2 * a.cz2;
+  const int n = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + acc_row(r, lane);
+    if (m < a.M && n < a.N) {
+      float* c = C + m * a.cm + n * a.cn;
+      const float v = a.alpha * acc[r];
+      *c = a.accumulate ? *c + v : v;
+    }
+  }
+}
+
+enum { OP_F32 = 0, OP_CT = 1 };   // operand storage: fp32, or the compute type
+
+template <typename T>
+void bgemm_t(const BgArgs& a, int ta, int tb, int Z, hipStream_t st) {
+  const dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, Z), block(256);
+  if (ta == OP_F32 && tb == OP_F32) cfm_launch((bgemm_kernel<float, float, T>), grid, block, 0, st, a);
+  else if (ta == OP_F32) cfm_launch((bgemm_kernel<float, T, T>), grid, block, 0, st, a);
+  else if (tb == OP_F32) cfm_launch((bgemm_kernel<T, float, T>), grid, block, 0, st, a);
+  else cfm_launch((bgemm_kernel<T, T, T>), grid, block, 0, st, a);
+}
+
+void bgemm(int dt, const BgArgs& a, int ta, int tb, int Z, hipStream_t st) {
+  if (a.M <= 0 || a.N <= 0 || Z <= 0) return;
+  if (dt == DT_F32) bgemm_t<float>(a, ta, tb, Z, st);
+  else bgemm_t<bf16_t>(a, ta, tb, Z, st);
+}
+
+CFM_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+CFM_DEV bool key_valid(int i, int j, int len, int cl, int cr) {
+  return i < len && j < len && (cl < 0 || j >= i - cl) && (cr < 0 || j <= i + cr);
+}
+
+// One wave per score row (b, h, i): S[i][j] + BD[i][T'-1-i+j] (log2 units) -> P in place.
+__global__ __launch_bounds__(256) void attn_probs_kernel(float* __restrict__ S, long sld, const float* __restrict__ BD,
+                                                         long bdld, const int32_t* __restrict__ lens, int B, int H,
+                                                         int Tp, int cl, int cr) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= (long)B * H * Tp) return;
+  const int i = (int)(row % Tp);
+  const int b = (int)(row / ((long)H * Tp));
+  const int len = lens ? min(lens[b], Tp) : Tp;
+  float* s = S + row * sld;
+  const float* bd = BD + row * bdld + (Tp - 1 - i);
+  float m = -INFINITY;
+  for (int j = lane; j < Tp; j += 64) {
+    if (!key_valid(i, j, len, cl, cr)) continue;
+    const float v = s[j] + bd[j];
+    s[j] = v;
+    m = fmaxf(m, v);
+  }
+  m = wave_max(m);
+  float sum = 0.0f;
+  for (int j = lane; j < Tp; j += 64) {
+    if (!key_valid(i, j, len, cl, cr)) continue;
+    const float e = exp2f(s[j] - m);
+    s[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  const float inv = sum > 0.0f ? 1.0f / sum : 0.0f;
+  for (int j = lane; j < Tp; j += 64) s[j] = key_valid(i, j, len, cl, cr) ? s[j] * inv : 0.0f;
+}
+
+// One wave per row: dS = P * (dP - sum_j P dP) into dP; the skewed copy G (layout [h][b][i][r],
+// all r < gld written) gets dS at r = T'-1-i+j and zero elsewhere.
+__global__ __launch_bounds__(256) void attn_dscore_kernel(const float* __restrict__ P, float* __restrict__ dP,
+                                                          long sld, float* __restrict__ G, long gld, int B, int H,
+                                                          int Tp) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= (long)B * H * Tp) return;
+  const int i = (int)(row % Tp);
+  const long bh = row / Tp;
+  const int h = (int)(bh % H), b = (int)(bh / H);
+  const float* p = P + row * sld;
+  float* dp = dP + row * sld;
+  float D = 0.0f;
+  for (int j = lane; j < Tp; j += 64) D += p[j] * dp[j];
+  D = wave_sum(D);
+  float* g = G + (((long)h * B + b) * Tp + i) * gld;
+  const int sh = Tp - 1 - i;
+  for (int r = lane; r < gld; r += 64) {
+    const int j = r - sh;
+    g[r] = (j >= 0 && j < Tp) ? p[j] * (dp[j] - D) : 0.0f;
+  }
+  for (int j = lane; j < Tp; j += 64) dp[j] = p[j] * (dp[j] - D);
+}
+
+__global__ void add_rows_kernel(float* __restrict__ dst, long ldd, const float* __restrict__ src, long lds, long rows,
+                                int cols) {
+  const long n = rows * cols;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const long r = e / cols;
+    const int c = (int)(e - r * cols);
+    dst[r * ldd + c] += src[r * lds + c];
+  }
+}
+
+struct BwdGeom {
+  long sld, gld, s_bytes, g_bytes, t_bytes, cs_bytes;
+  BwdGeom(int B, int Tp, int H, int dk) {
+    sld = round_up(Tp, 4);
+    gld = round_up(2L * Tp - 1, 4);
+    const long BH = (long)B * H;
+    s_bytes = round_up(BH * Tp * sld * 4, 256);
+    g_bytes = round_up(BH * Tp * gld * 4, 256);
+    t_bytes = round_up((long)B * Tp * H * dk * 4, 256);
+    cs_bytes = round_up((long)col_sums_ws(B * Tp, H * dk), 256);
+  }
+  size_t total() const { return (size_t)(2 * s_bytes + g_bytes + t_bytes + cs_bytes); }
+};
+
+}  // namespace
+
+size_t rel_pos_attention_backward_ws(int B, int Tp, int H, int dk) { return BwdGeom(B, Tp, H, dk).total(); }
+
+void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad,
+                                const void* P, long ldp, const int32_t* lens, int B, int Tp, int H, int dk, int dkp,
+                                int ctx_left, int ctx_right, const float* dctx, long ld_dctx, float* dq, float* dk_,
+                                float* dv, long ld_dqkv, float* dpos, long ld_dpos, float* du, float* dvb, char* ws,
+                                hipStream_t st) {
+  if (B <= 0 || Tp <= 0) return;
+  const BwdGeom g(B, Tp, H, dk);
+  float* S = (float*)ws;                          // scores -> P
+  float* dP = (float*)(ws + g.s_bytes);           // dP -> dS
+  float* BD = (float*)(ws + 2 * g.s_bytes);       // raw BD -> G
+  float* tmp = (float*)(ws + 2 * g.s_bytes + g.g_bytes);
+  float* cs = (float*)(ws + 2 * g.s_bytes + g.g_bytes + g.t_bytes);
+  const int es = dtype_size(dt);
+  const char* qkc = (const char*)qk;
+  const long BT = (long)B * Tp;
+  const float rs = (float)(1.0 / std::sqrt((double)dk));
+  const float ln2 = 0.69314718055994531f;
+  const long szs = (long)Tp * g.sld, szg = (long)Tp * g.gld;   // one (b, h) score / G image
+  auto A0 = [](const void* p, long am, long ak, long az1, long az2) { BgArgs a{}; a.A = p; a.am = am; a.ak = ak; a.az1 = az1; a.az2 = az2; return a; };
+  auto setB = [](BgArgs& a, const void* p, long bk, long bn, long bz1, long bz2) { a.B = p; a.bk = bk; a.bn = bn; a.bz1 = bz1; a.bz2 = bz2; };
+  auto setC = [](BgArgs& a, float* p, long cm, long cn, long cz1, long cz2) { a.C = p; a.cm = cm; a.cn = cn; a.cz1 = cz1; a.cz2 = cz2; };
+  const int Z = B * H;
+  (void)es;
+  // S[b,h] = (q+u)c . k^T
+  {
+    BgArgs a = A0(qkc, ldqk, 1, (long)Tp * ldqk, dkp);
+    setB(a, (const void*)nullptr, 1, ldqk, (long)Tp * ldqk, dkp);
+    a.B = (const void*)(qkc + 2L * H * dkp * es);
+    setC(a, S, g.sld, 1, (long)H * szs, szs);
+    a.M = Tp; a.N = Tp; a.K = dk; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
+    bgemm(dt, a, OP_CT, OP_CT, Z, st);
+  }
+  // BD[b,h] = (q+v)c . p^T   (2T'-1 positions)
+  {
+    BgArgs a = A0(qkc + (long)H * dkp * es, ldqk, 1, (long)Tp * ldqk, dkp);
+    setB(a, P, 1, ldp, 0, dkp);
+    setC(a, BD, g.gld, 1, (long)H * szg, szg);
+    a.M = Tp; a.N = 2 * Tp - 1; a.K = dk; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
+    bgemm(dt, a, OP_CT, OP_CT, Z, st);
+  }
+  const unsigned rows_blocks = (unsigned)((BT * H + 3) / 4);
+  cfm_launch(attn_probs_kernel, dim3(rows_blocks), dim3(256), 0, st, S, g.sld, (const float*)BD, g.gld, lens, B, H, Tp,
+             ctx_left, ctx_right);
+  // dP[b,h] = dctx . V^T
+  {
+    BgArgs a = A0(dctx, ld_dctx, 1, (long)Tp * ld_dctx, dk);
+    setB(a, Vt, (long)Tpad, 1, (long)H * vt_rows * Tpad, (long)vt_rows * Tpad);
+    setC(a, dP, g.sld, 1, (long)H * szs, szs);
+    a.M = Tp; a.N = Tp; a.K = dk; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+  }
+  cfm_launch(attn_dscore_kernel, dim3(rows_blocks), dim3(256), 0, st, (const float*)S, dP, g.sld, BD, g.gld, B, H, Tp);
+  float* G = BD;
+  // d(q+u) = dS . k / sqrt(dk) -> dq
+  {
+    BgArgs a = A0(dP, g.sld, 1, (long)H * szs, szs);
+    setB(a, qkc + 2L * H * dkp * es, ldqk, 1, (long)Tp * ldqk, dkp);
+    setC(a, dq, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
+    a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = rs; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+  }
+  if (du) col_sums(dq, ld_dqkv, (int)BT, H * dk, du, 0, cs, st);
+  // d(q+v) = G . p / sqrt(dk) -> tmp;  dq += tmp
+  {
+    BgArgs a = A0(G, g.gld, 1, (long)Tp * g.gld, (long)B * szg);   // G is [h][b][i][r]
+    setB(a, P, ldp, 1, 0, dkp);
+    setC(a, tmp, (long)H * dk, 1, (long)Tp * H * dk, dk);
+    a.M = Tp; a.N = dk; a.K = 2 * Tp - 1; a.Z2 = H; a.alpha = rs; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+  }
+  if (dvb) col_sums(tmp, (long)H * dk, (int)BT, H * dk, dvb, 0, cs, st);
+  cfm_launch(add_rows_kernel, dim3(1024), dim3(256), 0, st, dq, ld_dqkv, (const float*)tmp, (long)H * dk, BT, H * dk);
+  // dk = dS^T . (q+u)c * ln2
+  {
+    BgArgs a = A0(dP, 1, g.sld, (long)H * szs, szs);
+    setB(a, qkc, ldqk, 1, (long)Tp * ldqk, dkp);
+    setC(a, dk_, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
+    a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = ln2; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+  }
+  // dv = P^T . dctx
+  {
+    BgArgs a = A0(S, 1, g.sld, (long)H * szs, szs);
+    setB(a, dctx, ld_dctx, 1, (long)Tp * ld_dctx, dk);
+    setC(a, dv, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
+    a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_F32, Z, st);
+  }
+  // dp[h] = sum_(b,i) G^T . (q+v)c * ln2: one GEMM per head with K = B*T' ((b, i) rows are uniform in G and qk)
+  if (dpos) {
+    BgArgs a = A0(G, 1, g.gld, (long)B * szg, 0);
+    setB(a, qkc + (long)H * dkp * es, ldqk, 1, dkp, 0);
+    setC(a, dpos, ld_dpos, 1, dk, 0);
+    a.M = 2 * Tp - 1; a.N = dk; a.K = (int)BT; a.Z2 = 1; a.alpha = ln2; a.accumulate = 0;
+    bgemm(dt, a, OP_F32, OP_CT, H, st);
+  }
+}
+
+}  // namespace cfm
+
+using namespace cfm;
+
+extern "C" {
+
+size_t cfm_op_rel_attention_backward_ws_size(int dtype, int B, int Tp, int H, int dk) {
+  return cfm_op_rel_attention_ws_size(dtype, B, Tp, H, dk) + rel_pos_attention_backward_ws(B, Tp, H, dk) + 256;
+}
+
+cfm_status cfm_op_rel_attention_backward(int dtype, const void* q, const void* k, const void* v, const void* p,
+                                         const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp,
+                                         int H, int dk, int ctx_left, int ctx_right, const float* dctx, float* dq,
+                                         float* dk_, float* dv, float* dp, float* du, float* dvb, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (B <= 0 || Tp <= 0 || H <= 0 || dk <= 0) fail(CFM_ERR_INVALID_ARG, "bad shape");
+    if (dk > 128) fail(CFM_ERR_UNSUPPORTED, "head dim > 128");
+    if (!q || !k || !v || !p || !pos_u || !pos_v || !dctx || !dq || !dk_ || !dv || !ws)
+      fail(CFM_ERR_INVALID_ARG, "null pointer");
+    if (ws_bytes < cfm_op_rel_attention_backward_ws_size(dtype, B, Tp, H, dk))
+      fail(CFM_ERR_INVALID_ARG, "workspace too small");
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    const int dkp = (int)round_up(dk, 16), vt_rows = (int)round_up(dkp, 32), Tpad = (int)round_up(Tp, 32);
+    const long M = (long)B * Tp;
+    const long qk_bytes = round_up(M * 3 * H * dkp * es, 256);
+    const long vt_bytes = round_up((long)B * H * vt_rows * Tpad * es, 256);
+    hipStream_t st = (hipStream_t)stream;
+    char* w = (char*)ws;
+    attn_relayout(dt, q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, w, qk_bytes, vt_bytes, st);
+    char* bw = w + round_up((long)cfm_op_rel_attention_ws_size(dtype, B, Tp, H, dk), 256);
+    rel_pos_attention_backward(dt, w, 3L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes,
+                               (long)H * dkp, lens, B, Tp, H, dk, dkp, ctx_left, ctx_right, dctx, (long)H * dk, dq,
+                               dk_, dv, (long)H * dk, dp, (long)H * dk, du, dvb, bw, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

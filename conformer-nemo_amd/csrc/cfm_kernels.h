@@ -101,6 +101,20 @@ void transpose_out(const float* X, int B, int Tp, int d, float* y_bdt, hipStream
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
                        long ldp, const int32_t* lens, int B, int Tp, int H,
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
+// q, k, v (M, H*dk), p (2T'-1, H*dk) in the compute type -> the qk / Vt / P layouts above, at ws,
+// ws + qk_bytes, ws + qk_bytes + vt_bytes (what the QKV and pos GEMM epilogues write in the encoder).
+void attn_relayout(int dt, const void* q, const void* k, const void* v, const void* p, const float* pos_u,
+                   const float* pos_v, int B, int Tp, int H, int dk, int dkp, int vt_rows, int Tpad, char* ws,
+                   long qk_bytes, long vt_bytes, hipStream_t st);
+// Backward of rel_pos_attention from the same qk / Vt / P operands (attn_bwd.hip).  dctx (M, H*dk)
+// fp32 = gradient of the attention output before linear_out; outputs fp32: dq, dk, dv (M, H*dk, ld
+// ld_dqkv), dpos (2T'-1, H*dk, ld ld_dpos), du, dvb (H*dk) = pos_bias_u / pos_bias_v gradients.
+size_t rel_pos_attention_backward_ws(int B, int Tp, int H, int dk);
+void rel_pos_attention_backward(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad,
+                                const void* P, long ldp, const int32_t* lens, int B, int Tp, int H, int dk, int dkp,
+                                int ctx_left, int ctx_right, const float* dctx, long ld_dctx, float* dq, float* dk_,
+                                float* dv, long ld_dqkv, float* dpos, long ld_dpos, float* du, float* dvb, char* ws,
+                                hipStream_t st);
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
 
 // ---- backward building blocks (backward.hip) ----

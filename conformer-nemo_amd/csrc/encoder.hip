@@ -911,6 +911,17 @@ void relayout(const void* q, const void* k, const void* v, const void* p, const 
 }
 }  // namespace
 
+namespace cfm {
+void attn_relayout(int dt, const void* q, const void* k, const void* v, const void* p, const float* pos_u,
+                   const float* pos_v, int B, int Tp, int H, int dk, int dkp, int vt_rows, int Tpad, char* ws,
+                   long qk_bytes, long vt_bytes, hipStream_t st) {
+  if (dt == DT_F32)
+    relayout<float>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, ws, qk_bytes, vt_bytes, st);
+  else
+    relayout<bf16_t>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, ws, qk_bytes, vt_bytes, st);
+}
+}  // namespace cfm
+
 extern "C" cfm_status cfm_op_rel_attention(int dtype, const void* q, const void* k, const void* v, const void* p,
                                            const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp,
                                            int H, int dk, int ctx_left, int ctx_right, void* out, void* ws,
@@ -923,10 +934,7 @@ extern "C" cfm_status cfm_op_rel_attention(int dtype, const void* q, const void*
     const long qk_bytes = round_up(M * 3 * H * dkp * es, 256);
     const long vt_bytes = round_up((long)B * H * vt_rows * Tpad * es, 256);
     hipStream_t st = (hipStream_t)stream;
-    if (dt == DT_F32)
-      relayout<float>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
-    else
-      relayout<bf16_t>(q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
+    attn_relayout(dt, q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
     char* w = (char*)ws;
     rel_pos_attention(dt, w, 3L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes, (long)H * dkp, lens,
                       B, Tp, H, dk, dkp, ctx_left, ctx_right, out, (long)H * dk, st);

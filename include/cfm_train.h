@@ -57,6 +57,18 @@ cfm_status cfm_op_batchnorm_train_backward(const float* dy, const float* xhat, i
                                            const float* rstd, float* dx, float* dgamma, float* dbeta, void* ws,
                                            size_t ws_bytes, void* stream);
 
+/* RelPositionMultiHeadAttention backward (multi_head_attention.py:172-210, dropout off), from the
+ * same operands as cfm_op_rel_attention (cfm_encoder.h): q, k, v (B*T', H*dk) and p = linear_pos(pos_emb)
+ * (2T'-1, H*dk) in the compute type, pos_u / pos_v (H*dk) fp32, pad lengths and context window.
+ * dctx (B*T', H*dk) fp32 is the gradient of the attention context (the input of linear_out).
+ * Outputs fp32: dq, dkey, dv (B*T', H*dk), dp (2T'-1, H*dk), du, dvb (H*dk; dp/du/dvb may be NULL). */
+size_t cfm_op_rel_attention_backward_ws_size(int dtype, int B, int Tp, int H, int dk);
+cfm_status cfm_op_rel_attention_backward(int dtype, const void* q, const void* k, const void* v, const void* p,
+                                         const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp,
+                                         int H, int dk, int ctx_left, int ctx_right, const float* dctx, float* dq,
+                                         float* dkey, float* dv, float* dp, float* du, float* dvb, void* ws,
+                                         size_t ws_bytes, void* stream);
+
 /* dz = du * swish'(z) elementwise (n elements). */
 cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int64_t n, void* stream);
 

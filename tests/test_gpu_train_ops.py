@@ -1,6 +1,8 @@
-"""GPU parity of the backward building blocks (include/cfm_train.h) against the reference under
-torch autograd (tests/golden/bwd_ffn.npz, from tests/golden/gen_bwd_goldens.py): the macaron FFN
-sub-block x + 0.5 * FFN(LayerNorm(x)) of ConformerLayer, backward composed from the native ops.
+"""GPU parity of the backward building blocks (include/cfm_train.h) against the reference modules
+under torch autograd, composed from the native ops:
+  * bwd_ffn.npz  (gen_bwd_goldens.py): macaron FFN sub-block x + 0.5 * FFN(LayerNorm(x));
+  * bwd_conv.npz (gen_conv_bwd_goldens.py): ConformerConvolution in training mode;
+  * bwd_attn.npz (gen_attn_bwd_goldens.py): RelPositionMultiHeadAttention, full and windowed context.
 
 Gates: fp32 GEMM operands rel-L2 <= 1e-4 per gradient; bf16 operands rel-L2 <= 2e-2.
 """
@@ -155,3 +157,58 @@ def test_conv_module_backward(compute):
     scale = np.sqrt(M) * np.sqrt((dh64 ** 2).mean(0)).max()
     np.testing.assert_allclose(ddb.cpu().numpy(), dh64.sum(0), rtol=0, atol=1e-5 * scale)
     assert np.abs(z["d_dw_b"]).max() <= 1e-4 * scale and np.abs(ddb.cpu().numpy()).max() <= 1e-4 * scale
+
+
+@pytest.mark.parametrize("case", ["full", "ctx"])
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_rel_attention_backward(compute, case):
+    """RelPositionMultiHeadAttention backward (tests/golden/bwd_attn.npz, the reference module under
+    float64 autograd with the encoder's pad / context-window mask): the native attention backward,
+    then the projections' backward (linear_q/k/v into d_x, linear_pos weight) from linear_backward."""
+    from conformer_amd import _lib
+    lib = _lib.load()
+    z = {k.split(".", 1)[1]: v for k, v in np.load(os.path.join(GOLDEN, "bwd_attn.npz")).items()
+         if k.startswith(case + ".")}
+    dt = DT[compute]
+    g = GATE[compute]
+    B, T, H = int(z["B"]), int(z["T"]), int(z["H"])
+    M, d = z["q"].shape
+    dk = d // H
+    ct = torch.float32 if compute == "fp32" else torch.bfloat16
+    q, k, v, p = (_t(z[n]).to(ct).contiguous() for n in ("q", "k", "v", "p"))
+    u, vb, dctx = _t(z["u"]), _t(z["vb"]), _t(z["d_ctx"])
+    lens = torch.from_numpy(z["lens"]).cuda()
+    cl, cr = int(z["ctx_left"]), int(z["ctx_right"])
+    # forward context first (same operands, checks the window mask)
+    ctx = torch.empty(M, d, dtype=ct, device="cuda")
+    wsf = torch.empty(lib.cfm_op_rel_attention_ws_size(dt, B, T, H, dk), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.cfm_op_rel_attention(dt, q.data_ptr(), k.data_ptr(), v.data_ptr(), p.data_ptr(), u.data_ptr(),
+                                        vb.data_ptr(), lens.data_ptr(), B, T, H, dk, cl, cr, ctx.data_ptr(),
+                                        wsf.data_ptr(), _st()), "rel_attention")
+    dq, dkey, dv = (torch.empty(M, d, device="cuda") for _ in range(3))
+    dp = torch.empty(2 * T - 1, d, device="cuda")
+    du, dvb = torch.empty(d, device="cuda"), torch.empty(d, device="cuda")
+    n = lib.cfm_op_rel_attention_backward_ws_size(dt, B, T, H, dk)
+    ws = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.cfm_op_rel_attention_backward(dt, q.data_ptr(), k.data_ptr(), v.data_ptr(), p.data_ptr(),
+                                                 u.data_ptr(), vb.data_ptr(), lens.data_ptr(), B, T, H, dk, cl, cr,
+                                                 dctx.data_ptr(), dq.data_ptr(), dkey.data_ptr(), dv.data_ptr(),
+                                                 dp.data_ptr(), du.data_ptr(), dvb.data_ptr(), ws.data_ptr(), n,
+                                                 _st()), "rel_attention_backward")
+    # projections: d_x = dq W_q + dk W_k + dv W_v ; d W_pos = dp^T pos_emb
+    x = _t(z["x"])
+    dxq, dwq, dbq = linear_backward(lib, dt, x, _t(z["w_q"]), dq)
+    dxk, _, _ = linear_backward(lib, dt, x, _t(z["w_k"]), dkey)
+    dxv, _, _ = linear_backward(lib, dt, x, _t(z["w_v"]), dv)
+    _, dwpos, _ = linear_backward(lib, dt, _t(z["pos_emb"]), _t(z["w_pos"]), dp)
+    torch.cuda.synchronize()
+    fwd_gate = 1e-5 if compute == "fp32" else 2e-2
+    assert rel_l2(ctx.float().cpu().numpy(), z["ctx"]) <= fwd_gate
+    for name, got in [("d_q", dq), ("d_k", dkey), ("d_v", dv), ("d_p", dp), ("d_u", du), ("d_vb", dvb),
+                      ("d_w_q", dwq), ("d_b_q", dbq), ("d_x", dxq + dxk + dxv), ("d_w_pos", dwpos)]:
+        e = rel_l2(got.cpu().numpy(), z[name])
+        assert e <= g, f"{name}: relL2 {e:.3e} > {g}"
+    # padded query rows / keys carry no gradient
+    for b, L in enumerate(z["lens"]):
+        assert float(dq[b * T + L:(b + 1) * T].abs().max() if L < T else 0) == 0.0
+        assert float(dkey[b * T + L:(b + 1) * T].abs().max() if L < T else 0) == 0.0
