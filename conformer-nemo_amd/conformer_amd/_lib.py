@@ -31,6 +31,7 @@ TRAIN_SYMBOLS = (
     "cfm_op_linear_backward", "cfm_op_swish_backward", "cfm_op_glu_backward", "cfm_op_dwconv_backward_ws_size",
     "cfm_op_dwconv_backward", "cfm_op_batchnorm_train_ws_size", "cfm_op_batchnorm_train_forward",
     "cfm_op_batchnorm_train_backward", "cfm_op_rel_attention_backward_ws_size", "cfm_op_rel_attention_backward",
+    "cfm_train_tape_size", "cfm_train_workspace_size", "cfm_train_forward", "cfm_train_backward",
 )
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (

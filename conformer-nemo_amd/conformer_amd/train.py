@@ -1,0 +1,191 @@
+"""Host runtime of the native training step (include/cfm_train.h, csrc/train.hip).
+
+`EncoderTrainer` drives `cfm_train_forward` / `cfm_train_backward` on one GPU: the train-mode
+encoder forward records an activation tape (a torch-owned device buffer), the backward replays it
+and writes every parameter gradient in the reference state_dict layout.  `encoder_train_forward`
+wraps the pair as one torch.autograd.Function, so the drop-in `ConformerEncoder` in `.train()` mode
+behaves like the reference module under autograd (EncDecCTCModel.training_step -> loss.backward(),
+ctc_models.py:485-514): gradients land in each nn.Parameter's `.grad`.
+
+Multi-GPU: SyncBatchNorm statistics are summed across ranks by a host callback that runs a
+torch.distributed (RCCL) all-reduce on a view of the library's workspace; the gradient exchange
+itself is `conformer_amd.dist.allreduce_gradients` (one flat all-reduce per step).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+
+
+class CfmTrainOpts(ctypes.Structure):
+    _fields_ = [("dropout", ctypes.c_float), ("dropout_emb", ctypes.c_float), ("dropout_att", ctypes.c_float),
+                ("bn_momentum", ctypes.c_float), ("update_running_stats", ctypes.c_int), ("world", ctypes.c_int),
+                ("seed", ctypes.c_uint64), ("allreduce", ALLREDUCE_FN), ("allreduce_user", ctypes.c_void_p)]
+
+
+def _bind(lib) -> None:
+    if getattr(lib, "_cfm_train_bound", False):
+        return
+    vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    for name, res, args in (
+            ("cfm_train_tape_size", sz, [vp, ci, ci]),
+            ("cfm_train_workspace_size", sz, [vp, ci, ci]),
+            ("cfm_train_forward", ci, [vp, pp, ci, vp, vp, ci, ci, ctypes.POINTER(CfmTrainOpts), vp, vp, vp, sz, vp,
+                                       sz, vp]),
+            ("cfm_train_backward", ci, [vp, pp, ci, vp, ci, ci, ctypes.POINTER(CfmTrainOpts), pp, vp, sz, vp, sz,
+                                        vp])):
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    lib._cfm_train_bound = True
+
+
+class EncoderTrainer:
+    """Training step of one encoder handle (a `NativeEncoder`) on one GPU."""
+
+    def __init__(self, native):
+        self.native = native
+        self.lib = native.lib
+        _bind(self.lib)
+        self.device = torch.device("cuda", native.device)
+        self.names: List[str] = list(native.param_names().keys())
+        self._ws: Optional[torch.Tensor] = None
+        self._cb = None          # keep the ctypes callback alive
+        self._group = None
+        self.world = 1
+
+    # ---- SyncBatchNorm plumbing ---------------------------------------------------------------
+    def set_sync_group(self, group=None, world: Optional[int] = None) -> None:
+        """Share BatchNorm statistics over `group` (torch.distributed, RCCL on ROCm)."""
+        import torch.distributed as dist
+        self._group = group
+        self.world = int(world if world is not None else dist.get_world_size(group))
+
+    def _make_callback(self):
+        if self.world <= 1:
+            return None
+
+        def cb(user, buf, n, stream):
+            try:
+                import torch.distributed as dist
+                ws = self._ws
+                off = int(buf) - ws.data_ptr()
+                if off < 0 or off % 4 or off + 4 * n > ws.numel():
+                    return 1
+                view = ws[off:off + 4 * n].view(torch.float32)
+                dist.all_reduce(view, group=self._group)
+                return 0
+            except Exception:   # noqa: BLE001  (no exception may cross the C boundary)
+                return 1
+        return ALLREDUCE_FN(cb)
+
+    # ---- step ------------------------------------------------------------------------------------
+    def _opts(self, dropout: float, seed: int, update_running_stats: bool, bn_momentum: float) -> CfmTrainOpts:
+        o = CfmTrainOpts()
+        o.dropout = float(dropout)
+        o.dropout_emb = 0.0
+        o.dropout_att = 0.0
+        o.bn_momentum = float(bn_momentum)
+        o.update_running_stats = 1 if update_running_stats else 0
+        o.world = self.world
+        o.seed = int(seed) & ((1 << 64) - 1)
+        self._cb = self._make_callback()
+        if self._cb is not None:
+            o.allreduce = self._cb
+        o.allreduce_user = None
+        return o
+
+    def _workspace(self, B: int, T: int) -> torch.Tensor:
+        n = int(self.lib.cfm_train_workspace_size(self.native.handle, B, T))
+        if self._ws is None or self._ws.numel() < n:
+            self._ws = None
+            self._ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _ptrs(self, tensors: Sequence[Optional[torch.Tensor]]):
+        arr = (ctypes.c_void_p * len(tensors))()
+        for i, t in enumerate(tensors):
+            arr[i] = None if t is None else t.data_ptr()
+        return arr
+
+    def check_params(self, params: Sequence[torch.Tensor]) -> None:
+        if len(params) != len(self.names):
+            raise ValueError(f"expected {len(self.names)} parameter tensors, got {len(params)}")
+        for n, p in zip(self.names, params):
+            if p.device != self.device or p.dtype != torch.float32 or not p.is_contiguous():
+                raise ValueError(f"{n}: parameters must be contiguous fp32 tensors on {self.device}")
+
+    def forward(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor], params: Sequence[torch.Tensor],
+                dropout: float = 0.0, seed: int = 0, update_running_stats: bool = True, bn_momentum: float = 0.1):
+        from .runtime import encoded_length
+        self.check_params(params)
+        x = x_bft.detach().to(self.device, torch.float32).contiguous()
+        B, F, T = x.shape
+        Tp = encoded_length(T)
+        d = self.native.cfg.d_model
+        y = torch.empty((B, d, Tp), dtype=torch.float32, device=self.device)
+        ylen = torch.empty((B,), dtype=torch.int32, device=self.device)
+        ln = None
+        if lengths is not None:
+            ln = lengths.to(device=self.device, dtype=torch.int32).contiguous()
+        tape = torch.empty(int(self.lib.cfm_train_tape_size(self.native.handle, B, T)), dtype=torch.uint8,
+                           device=self.device)
+        ws = self._workspace(B, T)
+        o = self._opts(dropout, seed, update_running_stats, bn_momentum)
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(self.lib.cfm_train_forward(self.native.handle, self._ptrs(params), len(params), x.data_ptr(),
+                                              None if ln is None else ln.data_ptr(), B, T, ctypes.byref(o),
+                                              y.data_ptr(), ylen.data_ptr(), tape.data_ptr(), tape.numel(),
+                                              ws.data_ptr(), ws.numel(), st), "cfm_train_forward")
+        state = dict(tape=tape, B=B, T=T, dropout=dropout, seed=seed, bn_momentum=bn_momentum, x=x, ln=ln)
+        return y, ylen, state
+
+    def backward(self, dy_bdt: torch.Tensor, state: Dict, params: Sequence[torch.Tensor],
+                 want: Sequence[bool]) -> List[Optional[torch.Tensor]]:
+        dy = dy_bdt.detach().to(self.device, torch.float32).contiguous()
+        grads = [torch.empty_like(p) if w else None for p, w in zip(params, want)]
+        ws = self._workspace(state["B"], state["T"])
+        o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"])
+        tape = state["tape"]
+        st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
+                                               state["B"], state["T"], ctypes.byref(o), self._ptrs(grads),
+                                               tape.data_ptr(), tape.numel(), ws.data_ptr(), ws.numel(), st),
+                   "cfm_train_backward")
+        return grads
+
+
+class _EncoderTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, trainer: EncoderTrainer, x, lengths, cfg: Tuple, *params):
+        dropout, seed, update_stats, momentum = cfg
+        y, ylen, state = trainer.forward(x, lengths, params, dropout, seed, update_stats, momentum)
+        ctx.trainer = trainer
+        ctx.state = state
+        ctx.params = params
+        ctx.mark_non_differentiable(ylen)
+        return y, ylen
+
+    @staticmethod
+    def backward(ctx, dy, _dylen):
+        want = [bool(ctx.needs_input_grad[4 + i]) for i in range(len(ctx.params))]
+        if dy is None:
+            dy = torch.zeros((ctx.state["B"], ctx.trainer.native.cfg.d_model, 1), device=ctx.trainer.device)
+        grads = ctx.trainer.backward(dy, ctx.state, ctx.params, want)
+        ctx.state = None
+        return (None, None, None, None, *grads)
+
+
+def encoder_train_forward(trainer: EncoderTrainer, x: torch.Tensor, lengths: Optional[torch.Tensor],
+                          params: Sequence[torch.Tensor], dropout: float, seed: int,
+                          update_running_stats: bool = True, bn_momentum: float = 0.1):
+    """Differentiable native train-mode encoder forward: returns (y (B, d, T'), lengths (B,) int32)."""
+    return _EncoderTrainFn.apply(trainer, x, lengths, (float(dropout), int(seed), bool(update_running_stats),
+                                                       float(bn_momentum)), *params)

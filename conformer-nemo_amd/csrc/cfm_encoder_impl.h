@@ -1,0 +1,49 @@
+// Encoder handle layout shared by the forward (encoder.hip) and the training step (train.hip).
+// Internal: not part of the C-ABI (include/cfm_encoder.h declares the opaque handle).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/cfm_encoder.h"
+#include "cfm_abi.h"
+
+namespace cfm {
+struct LayerW {
+  long ff1_w1, ff1_b1, ff1_w2, ff1_b2, ff2_w1, ff2_b1, ff2_w2, ff2_b2;
+  long qkv_w, qkv_b, out_w, out_b, uv;   // uv: pos_bias_u | pos_bias_v, [H][dkp] each, zero-padded
+  long pw1_w, pw1_b, dw_w, dw_b, bn_mean, bn_inv, bn_w, bn_b, pw2_w, pw2_b;
+  long ln_w[5], ln_b[5];   // ff1, self_att, conv, ff2, out
+};
+
+}  // namespace cfm
+
+struct cfm_encoder {
+  cfm_encoder_cfg cfg;
+  int device, dtype, es;
+  int d, H, dk, dkp, dff, C, F, F1, F2, K, L, dout, vt_rows;
+  int bke;                   // K padding granule in elements (GEMM_BK_BYTES / es)
+  bool has_out_proj;
+  // packed weights (one device allocation)
+  char* wbuf = nullptr;
+  size_t wbytes = 0;
+  bool weights_set = false;
+  long conv1_w, conv1_b, conv2_w, conv2_b, sub_w, sub_b, pos_w, outp_w, outp_b;
+  std::vector<cfm::LayerW> layers;
+  // relative positional table (compute type), rows = 2*max_len - 1
+  char* pe = nullptr;
+  int max_len = 0;
+  // micro-batch concurrency: the batch is split into `microbatches` parts run on their own streams
+  int microbatches = 2;
+  std::vector<hipStream_t> sub_streams;
+  std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
+  void* zero_page = nullptr;
+  std::vector<std::pair<std::string, int64_t>> params;
+
+  template <typename P = char>
+  P* w(long off) const { return (P*)(wbuf + off); }
+  long kpad(int k) const { return cfm::round_up(k, bke); }
+};
+

@@ -587,6 +587,20 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
 }
 
+// As gemm(), with the packed operand's row stride `ldw` (elements) decoupled from its K extent:
+// the main loop covers round_up(K, 128 bytes) only.  Used for split-K slices of wide operands.
+void gemm_ldw(int dtype, const void* A, long lda, int M, int K, const void* Wp, long ldw, int N, const GemmEpi& epi,
+              const void* zero_page, hipStream_t st) {
+  if (M <= 0 || K <= 0) return;
+  const int es = dtype_size(dtype);
+  GemmParams p = make_params(es, M, Wp, (int)ldw, N, epi);
+  p.kb = round_up_int(K * es, GEMM_BK_BYTES);
+  DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
+  int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
+  if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
+  else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
+}
+
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                const void* zero_page, hipStream_t st) {
   const int M = B * g.T2 * g.F2;

@@ -1,0 +1,1226 @@
+// Whole-encoder training step (SURVEY §8 rows a16 + e; BASELINE config 3): a stream-ordered
+// train-mode forward that records an activation tape, and the backward that replays it in reverse
+// and writes every parameter gradient in the reference's state_dict layout.
+//
+// Reference semantics followed (conformer_modules.py:88-200, multi_head_attention.py:69-316,
+// subsampling.py:99-176, conformer_encoder.py:236-281) in training mode:
+//   * dropout p = `dropout` on the embedding (RelPositionalEncoding.forward :316), inside both
+//     feed-forwards (ConformerFeedForward :198) and on the four residual branches (:101-118);
+//     masks come from a counter-based hash of (seed, site, element) so the backward regenerates
+//     them instead of storing them;
+//   * BatchNorm1d with batch statistics over all B*T' frames (padding included) and the momentum
+//     update of running_mean / running_var (unbiased variance); optionally synchronised across
+//     ranks (SyncBatchNorm, conformer_ctc_bpe.yaml:175) through a host-called sum-allreduce;
+//   * everything else exactly as the eval forward (encoder.hip), from the same kernels.
+// Weights are read from the caller's fp32 parameter tensors each step (packed into the workspace
+// per layer), so an optimizer can update them in place between steps with no re-registration.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/cfm_train.h"
+#include "cfm_abi.h"
+#include "cfm_common.h"
+#include "cfm_encoder_impl.h"
+#include "cfm_kernels.h"
+
+using namespace cfm;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// dropout masks: keep(e) iff hash(seed, site, e) >= thr, thr = p * 2^32; kept values * 1/(1-p)
+// ---------------------------------------------------------------------------------------------
+struct Drop {
+  uint32_t thr;    // 0 = no dropout
+  uint32_t key;    // per (step, site)
+  float scale;     // 1 / (1 - p)
+};
+CFM_DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+CFM_DEV float drop_mul(const Drop& d, uint64_t e) {
+  if (d.thr == 0) return 1.0f;
+  const uint32_t h = mix32((uint32_t)e ^ mix32(d.key ^ (uint32_t)(e >> 32) * 0x9e3779b9u));
+  return h >= d.thr ? d.scale : 0.0f;
+}
+inline uint32_t host_mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+Drop make_drop(float p, uint64_t seed, int site) {
+  Drop d{0u, 0u, 1.0f};
+  if (p <= 0.0f) return d;
+  const double t = std::min(1.0, (double)p) * 4294967296.0;
+  d.thr = (uint32_t)std::min(4294967295.0, std::max(1.0, t));
+  d.key = host_mix32((uint32_t)seed ^ host_mix32((uint32_t)(seed >> 32) + 0x632be5abu * (uint32_t)site));
+  d.scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
+  return d;
+}
+
+unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+
+// ---------------------------------------------------------------------------------------------
+// operand packing
+// ---------------------------------------------------------------------------------------------
+// dst[i][j] = scale * fn(src)[transpose ? (j, i) : (i, j)] in the compute type, zero outside src.
+// fn 0 = identity, 1 = dropout(swish(.)) (the FFN hidden recomputed from its pre-activation; the
+// mask index is the source element (row * cols + col)).  32x32 LDS tiles.
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src, long src_ld, int rows, int cols,
+                                                    int transpose, float scale, int fn, Drop drop,
+                                                    Tout* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad) {
+  __shared__ float tile[32][33];
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int si = transpose ? j0 + k : i0 + k;
+    const int sj = transpose ? i0 + tx : j0 + tx;
+    float v = 0.0f;
+    if (si < rows && sj < cols) {
+      v = ld_f<Tin>(src + (long)si * src_ld + sj);
+      if (fn == 1) v = swishf(v) * drop_mul(drop, (uint64_t)si * cols + sj);
+      v *= scale;
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int di = i0 + k, dj = j0 + tx;
+    if (di < rows_pad && dj < cols_pad) st_f<Tout>(dst + (long)di * dst_ld + dj, transpose ? tile[tx][k] : tile[k][tx]);
+  }
+}
+
+// Head-padded row gather: dst row n = (part, head, dd) of `parts` stacked (H*dk, K) fp32 sources,
+// head dims padded dk -> dkp (the layout the QKV epilogue and attention kernels consume); K = 1
+// packs bias vectors (fp32 out).
+template <typename T>
+__global__ __launch_bounds__(256) void pack_heads_kernel(const float* __restrict__ s0, const float* __restrict__ s1,
+                                                         const float* __restrict__ s2, int parts, int H, int dk,
+                                                         int dkp, int K, T* __restrict__ dst, long Kp, int rows_pad) {
+  const long n = (long)rows_pad * Kp;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / Kp), k = (int)(i - (long)r * Kp);
+    float v = 0.0f;
+    if (r < parts * H * dkp && k < K) {
+      const int part = r / (H * dkp), rr = r % (H * dkp), hh = rr / dkp, dd = rr % dkp;
+      const float* s = part == 0 ? s0 : (part == 1 ? s1 : s2);
+      if (dd < dk && s) v = s[(long)(hh * dk + dd) * K + k];
+    }
+    st_f<T>(dst + i, v);
+  }
+}
+
+// Index-permuting packs of the subsampling weights (rows_pad x cols_pad destination):
+//   0  Linear W (d, C*F2) [n][c*F2+f]  -> [n][f*C+c]          (channels-last flatten of conv2's output)
+//   1  its transpose                   -> [f*C+c][n]
+//   2  conv2 W (C, C, 3, 3)            -> [co][tap*C+ci]       (implicit-GEMM K order)
+//   3  its transpose                   -> [tap*C+ci][co]
+//   4  gradient un-permute, fp32: dst (d, C*F2) [n][c*F2+f] <- src [n][f*C+c]
+//   5  gradient un-permute, fp32: dst (C, C, 3, 3)         <- src [co][tap*C+ci]
+template <typename T>
+__global__ __launch_bounds__(256) void perm_pack_kernel(const float* __restrict__ src, int mode, int C, int F2, int d,
+                                                        T* __restrict__ dst, long ld, int rows_pad, int cols_pad) {
+  const long n = (long)rows_pad * cols_pad;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / cols_pad), q = (int)(i - (long)r * cols_pad);
+    float v = 0.0f;
+    switch (mode) {
+      case 0: if (r < d && q < C * F2) { const int f = q / C, c = q % C; v = src[(long)r * C * F2 + (long)c * F2 + f]; } break;
+      case 1: if (q < d && r < C * F2) { const int f = r / C, c = r % C; v = src[(long)q * C * F2 + (long)c * F2 + f]; } break;
+      case 2: if (r < C && q < 9 * C) { const int tap = q / C, ci = q % C; v = src[((long)r * C + ci) * 9 + tap]; } break;
+      case 3: if (q < C && r < 9 * C) { const int tap = r / C, ci = r % C; v = src[((long)q * C + ci) * 9 + tap]; } break;
+      case 4: { const int c = q / F2, f = q % F2; v = src[(long)r * C * F2 + (long)f * C + c]; } break;
+      case 5: { const int ci = q / 9, tap = q % 9; v = src[(long)r * 9 * C + (long)tap * C + ci]; } break;
+    }
+    st_f<T>(dst + (long)r * ld + q, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// elementwise forward pieces
+// ---------------------------------------------------------------------------------------------
+// u = dropout(swish(z)) in the compute type (FFN hidden, conformer_modules.py:196-198)
+template <typename T>
+__global__ __launch_bounds__(256) void swish_drop_kernel(const T* __restrict__ z, long n, Drop drop,
+                                                         T* __restrict__ u) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    st_f<T>(u + i, swishf(ld_f<T>(z + i)) * drop_mul(drop, (uint64_t)i));
+}
+// xout = xin + alpha * dropout(br) (residual update, conformer_modules.py:101-118); xout may alias xin
+__global__ __launch_bounds__(256) void resid_drop_kernel(const float* xin, const float* __restrict__ br, float alpha,
+                                                         long n, Drop drop, float* xout) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    xout[i] = xin[i] + alpha * br[i] * drop_mul(drop, (uint64_t)i);
+}
+// y = alpha * dropout(x) (in place allowed)
+__global__ __launch_bounds__(256) void scale_drop_kernel(const float* x, float alpha, long n, Drop drop, float* y) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] = alpha * x[i] * drop_mul(drop, (uint64_t)i);
+}
+// GLU(dim=1) + pad mask (conformer_modules.py:162-167): g = a * sigmoid(gate), 0 on padded frames;
+// fp32 for the tape and the compute type for the depthwise conv.
+template <typename T>
+__global__ __launch_bounds__(256) void glu_fwd_kernel(const float* __restrict__ pre, const int32_t* __restrict__ lens,
+                                                      int Tp, int d, long rows, float* __restrict__ g,
+                                                      T* __restrict__ gt) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long m = i / d;
+    const int c = (int)(i - m * d);
+    const int b = (int)(m / Tp), t = (int)(m - (long)b * Tp);
+    const float a = pre[m * 2 * d + c], gg = pre[m * 2 * d + d + c];
+    const float v = (t < lens[b]) ? a * (1.0f / (1.0f + expf(-gg))) : 0.0f;
+    g[i] = v;
+    st_f<T>(gt + i, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// reductions (fixed order: bitwise reproducible)
+// ---------------------------------------------------------------------------------------------
+// partial[chunk][n] = sum of rows [chunk*R, ...) of f(src) with f 0: x, 1: x*y, 2: (x - mean[n])^2
+__global__ __launch_bounds__(256) void colred_partial_kernel(const float* __restrict__ src, const float* __restrict__ y,
+                                                             const float* __restrict__ mean, long ld, int M, int N,
+                                                             int R, int f, float* __restrict__ partial) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * R, r1 = min(M, r0 + R);
+  const float mu = f == 2 ? mean[n] : 0.0f;
+  float s = 0.0f;
+  for (int r = r0; r < r1; ++r) {
+    const float v = src[(long)r * ld + n];
+    s += f == 0 ? v : (f == 1 ? v * y[(long)r * ld + n] : (v - mu) * (v - mu));
+  }
+  partial[(long)blockIdx.y * N + n] = s;
+}
+__global__ __launch_bounds__(256) void colred_final_kernel(const float* __restrict__ partial, int nchunks, int N,
+                                                           float alpha, float* __restrict__ out, int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.0f;
+  for (int c = 0; c < nchunks; ++c) s += partial[(long)c * N + n];
+  s *= alpha;
+  out[n] = accumulate ? out[n] + s : s;
+}
+constexpr int kRedRows = 64;
+size_t colred_ws(long M, long N) { return (size_t)((M + kRedRows - 1) / kRedRows) * N * 4; }
+void colred(const float* src, const float* y, const float* mean, long ld, int M, int N, int f, float alpha, float* out,
+            int accumulate, float* ws, hipStream_t st) {
+  if (N <= 0) return;
+  if (M <= 0) {
+    if (!accumulate) HIP_OK(hipMemsetAsync(out, 0, (size_t)N * 4, st));
+    return;
+  }
+  const int nch = (M + kRedRows - 1) / kRedRows;
+  cfm_launch(colred_partial_kernel, dim3((N + 255) / 256, nch), dim3(256), 0, st, src, y, mean, ld, M, N, kRedRows, f,
+             ws);
+  cfm_launch(colred_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, (const float*)ws, nch, N, alpha, out,
+             accumulate);
+}
+
+// ---------------------------------------------------------------------------------------------
+// BatchNorm (train) + Swish, and their backward
+// ---------------------------------------------------------------------------------------------
+// pass 0: mean = s1 / n; pass 1: rstd from s2 / n and the running-stat update (momentum, unbiased)
+__global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2, double n, int d,
+                                   float momentum, float* __restrict__ mean, float* __restrict__ rstd,
+                                   float* __restrict__ run_mean, float* __restrict__ run_var, int pass) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  if (pass == 0) {
+    mean[c] = (float)((double)s1[c] / n);
+  } else {
+    const float var = (float)((double)s2[c] / n);
+    rstd[c] = 1.0f / sqrtf(var + 1e-5f);
+    if (run_mean) {
+      const float unb = n > 1.0 ? (float)((double)s2[c] / (n - 1.0)) : var;
+      run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * mean[c];
+      run_var[c] = (1.0f - momentum) * run_var[c] + momentum * unb;
+    }
+  }
+}
+// xhat = (x - mean) * rstd (fp32 tape); s = swish(xhat * gamma + beta) in the compute type
+template <typename T>
+__global__ __launch_bounds__(256) void bn_swish_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, const float* __restrict__ gam,
+                                                       const float* __restrict__ bet, long rows, int d,
+                                                       float* __restrict__ xhat, T* __restrict__ s) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % d);
+    const float h = (x[i] - mean[c]) * rstd[c];
+    xhat[i] = h;
+    st_f<T>(s + i, swishf(h * gam[c] + bet[c]));
+  }
+}
+// dz = ds * swish'(xhat * gamma + beta)
+__global__ __launch_bounds__(256) void bn_swish_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ xhat,
+                                                           const float* __restrict__ gam, const float* __restrict__ bet,
+                                                           long rows, int d, float* __restrict__ dz) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % d);
+    const float z = xhat[i] * gam[c] + bet[c];
+    const float s = 1.0f / (1.0f + expf(-z));
+    dz[i] = ds[i] * (s + z * s * (1.0f - s));
+  }
+}
+// dx = gamma * rstd * (dy - sdy / n - xhat * sdyx / n)   (sdy, sdyx: global sums over n frames)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ xhat,
+                                                           const float* __restrict__ gam, const float* __restrict__ rstd,
+                                                           const float* __restrict__ sdy, const float* __restrict__ sdyx,
+                                                           float inv_n, long rows, int d, float* __restrict__ dx) {
+  const long n = rows * d;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % d);
+    dx[i] = gam[c] * rstd[c] * (dy[i] - sdy[c] * inv_n - xhat[i] * sdyx[c] * inv_n);
+  }
+}
+// dz = dropout'(du) * swish'(z), z in the compute type (FFN hidden pre-activation)
+template <typename T>
+__global__ __launch_bounds__(256) void swish_drop_bwd_kernel(const T* __restrict__ z, const float* __restrict__ du,
+                                                             long n, Drop drop, float* __restrict__ dz) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float zz = ld_f<T>(z + i);
+    const float s = 1.0f / (1.0f + expf(-zz));
+    dz[i] = du[i] * drop_mul(drop, (uint64_t)i) * (s + zz * s * (1.0f - s));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// subsampling backward
+// ---------------------------------------------------------------------------------------------
+// g *= (y > 0) (ReLU backward from the saved output)
+template <typename T>
+__global__ __launch_bounds__(256) void relu_mask_kernel(float* g, const T* __restrict__ y, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    if (!(ld_f<T>(y + i) > 0.0f)) g[i] = 0.0f;
+}
+// col2im of conv2's input gradient, masked by conv1's ReLU:
+//   dY1[b,t1,f1,c] = [X1 > 0] * sum over taps (kt, kf) with t1 = 2*t2 - 1 + kt, f1 = 2*f2 - 1 + kf of
+//                    dCol[(b, t2, f2)][(3*kt + kf) * C + c]
+template <typename T>
+__global__ __launch_bounds__(256) void col2im_relu_kernel(const T* __restrict__ dcol, const T* __restrict__ x1, int B,
+                                                          int T1, int F1, int T2, int F2, int C,
+                                                          float* __restrict__ dy1) {
+  const long n = (long)B * T1 * F1 * C;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long p = i / C;
+    const int f1 = (int)(p % F1);
+    const long bt = p / F1;
+    const int t1 = (int)(bt % T1), b = (int)(bt / T1);
+    float s = 0.0f;
+    if (ld_f<T>(x1 + i) > 0.0f) {
+      for (int kt = 0; kt < 3; ++kt) {
+        const int tt = t1 + 1 - kt;
+        if (tt < 0 || (tt & 1) || (tt >> 1) >= T2) continue;
+        for (int kf = 0; kf < 3; ++kf) {
+          const int ff = f1 + 1 - kf;
+          if (ff < 0 || (ff & 1) || (ff >> 1) >= F2) continue;
+          const long m = ((long)b * T2 + (tt >> 1)) * F2 + (ff >> 1);
+          s += ld_f<T>(dcol + m * 9 * C + (long)(3 * kt + kf) * C + c);
+        }
+      }
+    }
+    dy1[i] = s;
+  }
+}
+// im2col of conv2's input, transposed (the weight-gradient GEMM operand):
+//   dst[tap*C + ci][m] = X1[b, 2*t2 - 1 + kt, 2*f2 - 1 + kf, ci] (zero outside), m = (b, t2, f2)
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_t_kernel(const T* __restrict__ x1, int T1, int F1, int T2, int F2, int C,
+                                                       int M2, T* __restrict__ dst, long ld, int rows_pad) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, m0 = blockIdx.x * 32;   // r = tap*C + ci (rows of dst), m (columns)
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {      // tile[k][tx] = src(m0 + k, r0 + tx): coalesced along ci
+    const int m = m0 + k, r = r0 + tx;
+    float v = 0.0f;
+    if (m < M2 && r < 9 * C) {
+      const int tap = r / C, ci = r - tap * C, kt = tap / 3, kf = tap - kt * 3;
+      const int f2 = m % F2, bt = m / F2, t2 = bt % T2, b = bt / T2;
+      const int ti = 2 * t2 - 1 + kt, fi = 2 * f2 - 1 + kf;
+      if (ti >= 0 && ti < T1 && fi >= 0 && fi < F1) v = ld_f<T>(x1 + (((long)b * T1 + ti) * F1 + fi) * C + ci);
+    }
+    tile[k][tx] = v;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, m = m0 + tx;
+    if (r < rows_pad && m < ld) st_f<T>(dst + (long)r * ld + m, tile[tx][k]);
+  }
+}
+// conv1 weight gradient, stage 1: partial[chunk][c][tap] = sum over the chunk's (b, t1) rows and all
+// f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T))
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int F, int T, int T1, int F1,
+                                                          int C, const float* __restrict__ dy1, int B, int R,
+                                                          float* __restrict__ partial) {
+  __shared__ float xs[3][264];
+  const int chunk = blockIdx.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  float acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
+  const int r0 = chunk * R, r1 = min(B * T1, r0 + R);
+  for (int bt = r0; bt < r1; ++bt) {
+    const int b = bt / T1, t1 = bt - b * T1;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * (F + 2); i += 256) {
+      const int kt = i / (F + 2), fp = i - kt * (F + 2), f = fp - 1, t = 2 * t1 - 1 + kt;
+      xs[kt][fp] = (f >= 0 && f < F && t >= 0 && t < T) ? x[((long)b * F + f) * T + t] : 0.0f;
+    }
+    __syncthreads();
+    if (c < C) {
+      const float* g = dy1 + ((long)bt * F1) * C + c;
+      for (int f1 = 0; f1 < F1; ++f1) {
+        const float gv = g[(long)f1 * C];
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int kf = 0; kf < 3; ++kf) acc[kt * 3 + kf] = fmaf(gv, xs[kt][2 * f1 + kf], acc[kt * 3 + kf]);
+      }
+    }
+  }
+  if (c < C) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) partial[((long)chunk * C + c) * 9 + k] = acc[k];
+  }
+}
+
+// (B, T', d) fp32 rows <-> (B, d, T') fp32
+__global__ __launch_bounds__(256) void btd_transpose_kernel(const float* __restrict__ src, int Tp, int d, int to_bdt,
+                                                            float* __restrict__ dst) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, t0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* s = src + (long)b * Tp * d;
+  float* o = dst + (long)b * Tp * d;
+  for (int k = ty; k < 32; k += 8) {
+    if (to_bdt) {   // src (T', d): tile[t][c]
+      const int t = t0 + k, c = c0 + tx;
+      tile[k][tx] = (t < Tp && c < d) ? s[(long)t * d + c] : 0.0f;
+    } else {        // src (d, T'): tile[c][t]
+      const int c = c0 + k, t = t0 + tx;
+      tile[k][tx] = (t < Tp && c < d) ? s[(long)c * Tp + t] : 0.0f;
+    }
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    if (to_bdt) {
+      const int c = c0 + k, t = t0 + tx;
+      if (t < Tp && c < d) o[(long)c * Tp + t] = tile[tx][k];
+    } else {
+      const int t = t0 + k, c = c0 + tx;
+      if (t < Tp && c < d) o[(long)t * d + c] = tile[tx][k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// geometry, tape and workspace layouts
+// ---------------------------------------------------------------------------------------------
+int calc_len_host(int len, int repeat) {
+  float L = (float)len;
+  for (int i = 0; i < repeat; ++i) L = std::floor((L + (2.0f * 1 - 3.0f)) / 2.0f + 1.0f);
+  return (int)L;
+}
+
+struct Geo {
+  int B, T, T1, T2, Tp, M, Tpad, NP;   // NP = 2T' - 1 position rows
+  int d, dff, H, dk, dkp, C, F, F1, F2, K, L, es, dt, kg;
+  long Mp, M2, M2p, Mq;                 // Mq: padded row count covering M and NP (wgrad K extent)
+};
+Geo make_geo(const cfm_encoder* h, int B, int T) {
+  Geo g;
+  g.B = B; g.T = T;
+  g.T1 = calc_len_host(T, 1);
+  g.T2 = calc_len_host(T, 2);
+  g.Tp = g.T2;
+  g.M = B * g.Tp;
+  g.Tpad = (int)round_up(std::max(g.Tp, 1), 32);
+  g.NP = 2 * g.Tp - 1;
+  g.d = h->d; g.dff = h->dff; g.H = h->H; g.dk = h->dk; g.dkp = h->dkp; g.C = h->C; g.F = h->F; g.F1 = h->F1;
+  g.F2 = h->F2; g.K = h->K; g.L = h->L; g.es = h->es; g.dt = h->dtype; g.kg = GEMM_BK_BYTES / h->es;
+  g.Mp = round_up(std::max(g.M, 1), g.kg);
+  g.Mq = round_up(std::max(g.M, g.NP), g.kg);
+  g.M2 = (long)B * g.T2 * g.F2;
+  g.M2p = round_up(std::max<long>(g.M2, 1), g.kg);
+  return g;
+}
+
+struct Alloc {
+  long off = 0;
+  long take(long bytes) { const long o = round_up(off, 256); off = o + round_up(std::max(bytes, 1L), 256); return o; }
+};
+
+struct TapeLayer { long x[5], hn[4], z1, z2, qk, vt, P, ctx, pre, g, xhat, mean, rstd, s; };
+struct Tape { long xin, lens, X1, X2; std::vector<TapeLayer> lay; long xfin, total; };
+
+Tape tape_layout(const cfm_encoder* h, const Geo& g) {
+  Tape t;
+  Alloc a;
+  const long es = g.es, M = g.M, d = g.d;
+  t.xin = a.take((long)g.B * g.F * g.T * 4);
+  t.lens = a.take((long)g.B * 4);
+  t.X1 = a.take((long)g.B * g.T1 * g.F1 * g.C * es);
+  t.X2 = a.take((long)g.M2 * g.C * es);
+  t.lay.resize(g.L);
+  for (auto& l : t.lay) {
+    for (long& v : l.x) v = a.take(M * d * 4);
+    for (long& v : l.hn) v = a.take(M * d * es);
+    l.z1 = a.take(M * g.dff * es);
+    l.z2 = a.take(M * g.dff * es);
+    l.qk = a.take(M * 3 * g.H * g.dkp * es);
+    l.vt = a.take((long)g.B * g.H * h->vt_rows * g.Tpad * es);
+    l.P = a.take((long)g.NP * g.H * g.dkp * es + 64);
+    l.ctx = a.take(M * d * es);
+    l.pre = a.take(M * 2 * d * 4);
+    l.g = a.take(M * d * 4);
+    l.xhat = a.take(M * d * 4);
+    l.mean = a.take(d * 4);
+    l.rstd = a.take(d * 4);
+    l.s = a.take(M * d * es);
+  }
+  t.xfin = a.take(M * d * 4);
+  t.total = round_up(a.off, 256);
+  return t;
+}
+
+// split-K factor of a weight-gradient GEMM (N x K outputs, reduction over `rows`)
+int wgrad_splits(int N, int K, long rows) {
+  const long tiles = (long)((N + 63) / 64) * ((K + 127) / 128);
+  long s = (1024 + tiles - 1) / tiles;
+  s = std::min<long>(s, std::max<long>(1, rows / 512));
+  return (int)std::max<long>(1, std::min<long>(s, 16));
+}
+
+struct Ws {
+  // forward
+  long w1, b1, w2, b2, wqkv, bqkv, uv, wout, bout, wpos, wpw1, bpw1, dww, wpw2, bpw2, wc2, bc2, wsub, bsub;
+  long u, br, dwo, gt, s1, s2, sync;
+  // backward
+  long gA, gB, dbr, dU, pa, pat, pbt, wt, part, dqkv, dctx, dP, dpre, dG, dD, red;
+  long dX2, dcol, i2c, dy1, c1part, gtmp, attws;
+  long total;
+};
+
+Ws ws_layout(const cfm_encoder* h, const Geo& g) {
+  Ws w;
+  Alloc a;
+  const long es = g.es, M = g.M, d = g.d, dff = g.dff, kg = g.kg;
+  auto kp = [&](long k) { return round_up(k, kg); };
+  auto np = [&](long n) { return round_up(n, GEMM_BN); };
+  const long HP = (long)g.H * g.dkp;
+  w.w1 = a.take(np(dff) * kp(d) * es);
+  w.b1 = a.take(np(dff) * 4);
+  w.w2 = a.take(np(d) * kp(dff) * es);
+  w.b2 = a.take(np(d) * 4);
+  w.wqkv = a.take(np(3 * HP) * kp(d) * es);
+  w.bqkv = a.take(np(3 * HP) * 4);
+  w.uv = a.take(2 * HP * 4);
+  w.wout = a.take(np(d) * kp(d) * es);
+  w.bout = a.take(np(d) * 4);
+  w.wpos = a.take(np(HP) * kp(d) * es);
+  w.wpw1 = a.take(np(2 * d) * kp(d) * es);
+  w.bpw1 = a.take(np(2 * d) * 4);
+  w.dww = a.take((long)g.K * d * 4);
+  w.wpw2 = a.take(np(d) * kp(d) * es);
+  w.bpw2 = a.take(np(d) * 4);
+  w.wc2 = a.take(np(g.C) * kp(9L * g.C) * es);
+  w.bc2 = a.take(np(g.C) * 4);
+  w.wsub = a.take(np(d) * kp((long)g.F2 * g.C) * es);
+  w.bsub = a.take(np(d) * 4);
+  w.u = a.take(M * dff * es);
+  w.br = a.take(M * d * 4);
+  w.dwo = a.take(M * d * 4);
+  w.gt = a.take(M * d * es);
+  w.s1 = a.take(d * 4);
+  w.s2 = a.take(d * 4);
+  w.sync = a.take(2 * d * 4);
+  // backward
+  const long Kmax = std::max({dff, 3 * d, 2 * d, (long)g.F2 * g.C});
+  w.gA = a.take(M * d * 4);
+  w.gB = a.take(M * d * 4);
+  w.dbr = a.take(M * d * 4);
+  w.dU = a.take(M * std::max(dff, 3 * d) * 4);
+  w.pa = a.take(M * kp(Kmax) * es);                                   // dgrad A operand [M][N]
+  const long NT = std::max({dff, 3 * d, 2 * d, (long)g.C});
+  w.pat = a.take(std::max(NT * g.Mq, (long)g.C * g.M2p) * es);       // dy^T [N][Mp]
+  const long KT = np(std::max({dff, d, (long)g.F2 * g.C}));
+  w.pbt = a.take(KT * g.Mq * es);                                      // x^T [Kpad][Mp]
+  w.wt = a.take(std::max({np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(3 * d), np(d) * kp(2 * d),
+                          np((long)g.F2 * g.C) * kp(d), np(9L * g.C) * kp(g.C)}) * es);
+  long part = 0;
+  auto upd = [&](long N, long K, long rows) { part = std::max(part, (long)wgrad_splits((int)N, (int)K, rows) * N * K); };
+  upd(dff, d, M); upd(d, dff, M); upd(3 * d, d, M); upd(d, d, M); upd(2 * d, d, M); upd(d, d, g.NP);
+  upd(d, (long)g.F2 * g.C, M); upd(g.C, 9L * g.C, g.M2);
+  w.part = a.take(part * 4);
+  w.dqkv = a.take(M * 3 * d * 4);
+  w.dctx = a.take(M * d * 4);
+  w.dP = a.take((long)g.NP * d * 4);
+  w.dpre = a.take(M * 2 * d * 4);
+  w.dG = a.take(M * d * 4);
+  w.dD = a.take(M * d * 4);
+  const long red_rows = std::max({(long)M, g.M2, (long)g.B * g.T1, 64L});
+  w.red = a.take(std::max({(long)colred_ws(red_rows, std::max(dff, 3 * d)), (long)colred_ws(16, 9L * g.C * g.C),
+                           (long)cfm_op_dwconv_backward_ws_size(g.B, g.Tp, (int)d, g.K),
+                           (long)colred_ws(g.B * g.T1, 9L * g.C)}) + 1024);
+  w.dX2 = a.take(M * (long)g.F2 * g.C * 4);
+  w.dcol = a.take(g.M2 * 9L * g.C * es);
+  w.i2c = a.take(np(9L * g.C) * g.M2p * es);
+  w.dy1 = a.take((long)g.B * g.T1 * g.F1 * g.C * 4);
+  const long c1ch = ((long)g.B * g.T1 + 7) / 8;
+  w.c1part = a.take(c1ch * 9L * g.C * 4 + 4096);
+  w.gtmp = a.take(std::max({d * (long)g.F2 * g.C, 9L * g.C * g.C, 3 * d * d}) * 4);
+  w.attws = a.take((long)rel_pos_attention_backward_ws(g.B, g.Tp, g.H, g.dk) + 256);
+  w.total = round_up(a.off, 256);
+  return w;
+}
+
+// ---------------------------------------------------------------------------------------------
+// step context
+// ---------------------------------------------------------------------------------------------
+enum LnIdx { LN_FF1 = 0, LN_ATT = 1, LN_CONV = 2, LN_FF2 = 3, LN_OUT = 4 };
+
+struct LayerP {   // indices into the parameter table
+  int ln_w[5], ln_b[5];
+  int ff_w1[2], ff_b1[2], ff_w2[2], ff_b2[2];
+  int pw1_w, pw1_b, dw_w, dw_b, bn_w, bn_b, bn_rm, bn_rv, pw2_w, pw2_b;
+  int q_w, q_b, k_w, k_b, v_w, v_b, o_w, o_b, pos_w, pu, pv;
+};
+
+struct Step {
+  cfm_encoder* h;
+  Geo g;
+  Tape tp;
+  Ws wl;
+  char* tape;
+  char* ws;
+  hipStream_t st;
+  const float* const* P;
+  const cfm_train_opts* o;
+  int i_c1w, i_c1b, i_c2w, i_c2b, i_sw, i_sb;
+  std::vector<LayerP> lp;
+
+  const float* prm(int i) const { return P[i]; }
+  template <typename T = char> T* T_(long off) const { return (T*)(tape + off); }
+  template <typename T = char> T* W_(long off) const { return (T*)(ws + off); }
+  int kpad(long k) const { return (int)round_up(k, g.kg); }
+  int npad(long n) const { return (int)round_up(n, GEMM_BN); }
+  Drop drop(int site) const { return make_drop(o->dropout, o->seed, site); }
+
+  void pack(const void* src, bool src_ct, long ld, int rows, int cols, bool tr, float scale, void* dst, long dld,
+            int rp, int cp, int fn = 0, Drop dr = Drop{0, 0, 1.0f}) const {
+    if (rp <= 0 || cp <= 0) return;
+    const dim3 grid((cp + 31) / 32, (rp + 31) / 32), block(256);
+    if (g.dt == DT_F32) {
+      cfm_launch(tpack_kernel<float, float>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale, fn,
+                 dr, (float*)dst, dld, rp, cp);
+    } else if (src_ct) {
+      cfm_launch(tpack_kernel<bf16_t, bf16_t>, grid, block, 0, st, (const bf16_t*)src, ld, rows, cols, (int)tr, scale,
+                 fn, dr, (bf16_t*)dst, dld, rp, cp);
+    } else {
+      cfm_launch(tpack_kernel<float, bf16_t>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
+                 fn, dr, (bf16_t*)dst, dld, rp, cp);
+    }
+  }
+  // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
+  void packW(const float* w, int N, int K, void* dst) const {
+    pack(w, false, K, N, K, false, 1.0f, dst, kpad(K), npad(N), kpad(K));
+  }
+  void packWt(const float* w, int N, int K, void* dst) const {
+    pack(w, false, K, N, K, true, 1.0f, dst, kpad(N), npad(K), kpad(N));
+  }
+  void bias(const float* b, int N, float* dst) const {
+    HIP_OK(hipMemsetAsync(dst, 0, (size_t)npad(N) * 4, st));
+    if (b) HIP_OK(hipMemcpyAsync(dst, b, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+  }
+  void heads(const float* s0, const float* s1, const float* s2, int parts, int K, void* dst, bool f32, long Kp,
+             int rows_pad) const {
+    const long n = (long)rows_pad * Kp;
+    if (f32 || g.dt == DT_F32)
+      cfm_launch(pack_heads_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, s0, s1, s2, parts, g.H, g.dk, g.dkp, K,
+                 (float*)dst, Kp, rows_pad);
+    else
+      cfm_launch(pack_heads_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, s0, s1, s2, parts, g.H, g.dk, g.dkp,
+                 K, (bf16_t*)dst, Kp, rows_pad);
+  }
+  void perm(const float* src, int mode, void* dst, bool f32, long ld, int rp, int cp) const {
+    const long n = (long)rp * cp;
+    if (f32 || g.dt == DT_F32)
+      cfm_launch(perm_pack_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, src, mode, g.C, g.F2, g.d, (float*)dst,
+                 ld, rp, cp);
+    else
+      cfm_launch(perm_pack_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, src, mode, g.C, g.F2, g.d,
+                 (bf16_t*)dst, ld, rp, cp);
+  }
+  GemmEpi epi(int mode, const float* b, float alpha = 1.0f) const {
+    GemmEpi e;
+    std::memset(&e, 0, sizeof(e));
+    e.mode = mode;
+    e.bias = b;
+    e.alpha = alpha;
+    return e;
+  }
+  void gemm_f32out(const void* A, long lda, int M, int K, const void* Wp, int N, const float* b, float alpha,
+                   float* X, long ldx, bool accumulate) const {
+    GemmEpi e = epi(accumulate ? EPI_RESID : EPI_SCALE_F32, b, alpha);
+    e.X = X;
+    e.ldx = ldx;
+    gemm(g.dt, A, lda, M, K, Wp, kpad(K), N, e, h->zero_page, st);
+  }
+  // out (N, K) fp32 (ld ldo) = At[N][Mp] . Bt[K][Mp]^T over `rows` (split-K + fixed-order reduction)
+  void wgrad(const void* At, const void* Bt, long ldm, int N, int K, long rows, float* out, long ldo) const {
+    const int S = wgrad_splits(N, K, rows);
+    float* part = W_<float>(wl.part);
+    if (S == 1) {
+      GemmEpi e = epi(EPI_SCALE_F32, nullptr);
+      e.X = out;
+      e.ldx = ldo;
+      gemm_ldw(g.dt, At, ldm, N, (int)rows, Bt, ldm, K, e, h->zero_page, st);
+      return;
+    }
+    const long chunk = round_up((rows + S - 1) / S, g.kg);
+    int used = 0;
+    for (int s = 0; s < S; ++s) {
+      const long k0 = (long)s * chunk;
+      const long kk = std::min(chunk, rows - k0);
+      if (kk <= 0) break;
+      GemmEpi e = epi(EPI_SCALE_F32, nullptr);
+      e.X = part + (long)s * N * K;
+      e.ldx = K;
+      gemm_ldw(g.dt, (const char*)At + k0 * g.es, ldm, N, (int)kk, (const char*)Bt + k0 * g.es, ldm, K, e,
+               h->zero_page, st);
+      ++used;
+    }
+    float* red = W_<float>(wl.red);
+    if (ldo == K) {
+      colred(part, nullptr, nullptr, (long)N * K, used, N * K, 0, 1.0f, out, 0, red, st);
+    } else {
+      for (int n = 0; n < N; ++n)   // (not used on the current paths: every gradient is dense)
+        colred(part + (long)n * K, nullptr, nullptr, (long)N * K, used, K, 0, 1.0f, out + (long)n * ldo, 0, red, st);
+    }
+  }
+  void sync(float* buf, long n) const {
+    if (o->world > 1 && o->allreduce) {
+      if (o->allreduce(o->allreduce_user, buf, (int64_t)n, (void*)st) != 0) fail(CFM_ERR_HIP, "allreduce callback failed");
+    }
+  }
+};
+
+void build_index(Step& S) {
+  std::map<std::string, int> idx;
+  const auto& pl = S.h->params;
+  for (int i = 0; i < (int)pl.size(); ++i) idx[pl[i].first] = i;
+  auto I = [&](const std::string& k) {
+    auto it = idx.find(k);
+    if (it == idx.end()) fail(CFM_ERR_WEIGHTS, "no parameter " + k);
+    return it->second;
+  };
+  S.i_c1w = I("pre_encode.conv.0.weight"); S.i_c1b = I("pre_encode.conv.0.bias");
+  S.i_c2w = I("pre_encode.conv.2.weight"); S.i_c2b = I("pre_encode.conv.2.bias");
+  S.i_sw = I("pre_encode.out.weight"); S.i_sb = I("pre_encode.out.bias");
+  S.lp.resize(S.g.L);
+  const char* lnn[5] = {"norm_feed_forward1", "norm_self_att", "norm_conv", "norm_feed_forward2", "norm_out"};
+  for (int l = 0; l < S.g.L; ++l) {
+    LayerP& q = S.lp[l];
+    const std::string p = "layers." + std::to_string(l) + ".";
+    for (int i = 0; i < 5; ++i) { q.ln_w[i] = I(p + lnn[i] + ".weight"); q.ln_b[i] = I(p + lnn[i] + ".bias"); }
+    for (int f = 0; f < 2; ++f) {
+      const std::string ff = p + (f ? "feed_forward2" : "feed_forward1");
+      q.ff_w1[f] = I(ff + ".linear1.weight"); q.ff_b1[f] = I(ff + ".linear1.bias");
+      q.ff_w2[f] = I(ff + ".linear2.weight"); q.ff_b2[f] = I(ff + ".linear2.bias");
+    }
+    q.pw1_w = I(p + "conv.pointwise_conv1.weight"); q.pw1_b = I(p + "conv.pointwise_conv1.bias");
+    q.dw_w = I(p + "conv.depthwise_conv.weight"); q.dw_b = I(p + "conv.depthwise_conv.bias");
+    q.bn_w = I(p + "conv.batch_norm.weight"); q.bn_b = I(p + "conv.batch_norm.bias");
+    q.bn_rm = I(p + "conv.batch_norm.running_mean"); q.bn_rv = I(p + "conv.batch_norm.running_var");
+    q.pw2_w = I(p + "conv.pointwise_conv2.weight"); q.pw2_b = I(p + "conv.pointwise_conv2.bias");
+    q.q_w = I(p + "self_attn.linear_q.weight"); q.q_b = I(p + "self_attn.linear_q.bias");
+    q.k_w = I(p + "self_attn.linear_k.weight"); q.k_b = I(p + "self_attn.linear_k.bias");
+    q.v_w = I(p + "self_attn.linear_v.weight"); q.v_b = I(p + "self_attn.linear_v.bias");
+    q.o_w = I(p + "self_attn.linear_out.weight"); q.o_b = I(p + "self_attn.linear_out.bias");
+    q.pos_w = I(p + "self_attn.linear_pos.weight");
+    q.pu = I(p + "self_attn.pos_bias_u"); q.pv = I(p + "self_attn.pos_bias_v");
+  }
+}
+
+// dropout sites: 0 embedding; per layer l: 1 + 8l + {0 ff1 inner, 1 ff1 resid, 2 att resid,
+// 3 conv resid, 4 ff2 inner, 5 ff2 resid}
+int site(int l, int j) { return 1 + 8 * l + j; }
+
+void check_common(cfm_encoder* h, const float* const* params, int n_params, int B, int T, const cfm_train_opts* o) {
+  if (!h || !params || !o) fail(CFM_ERR_INVALID_ARG, "null argument");
+  if (n_params != (int)h->params.size()) fail(CFM_ERR_INVALID_ARG, "parameter table size mismatch");
+  for (int i = 0; i < n_params; ++i)
+    if (!params[i]) fail(CFM_ERR_INVALID_ARG, "null parameter pointer: " + h->params[i].first);
+  if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
+  if (T > h->max_len) fail(CFM_ERR_INVALID_ARG, "T exceeds max_audio_length");
+  if (h->cfg.conv_norm_type != 0) fail(CFM_ERR_UNSUPPORTED, "training supports conv_norm_type='batch_norm' only");
+  if (h->has_out_proj) fail(CFM_ERR_UNSUPPORTED, "training with feat_out projection is not built");
+  if (h->K != 31) fail(CFM_ERR_UNSUPPORTED, "training is built for conv_kernel_size 31");
+  if (o->dropout < 0.0f || o->dropout >= 1.0f) fail(CFM_ERR_INVALID_ARG, "dropout must be in [0, 1)");
+  if (o->dropout_att != 0.0f) fail(CFM_ERR_UNSUPPORTED, "attention-probability dropout is not built (dropout_att must be 0)");
+  if (o->dropout_emb != 0.0f) fail(CFM_ERR_UNSUPPORTED, "positional-embedding dropout is not built (dropout_emb must be 0)");
+  if (o->world < 1) fail(CFM_ERR_INVALID_ARG, "world must be >= 1");
+  if (h->d % 8 || h->C % 8) fail(CFM_ERR_UNSUPPORTED, "d_model and conv channels must be multiples of 8");
+}
+
+// =============================================================================================
+// forward
+// =============================================================================================
+void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_bdt, int32_t* out_len_b) {
+  const Geo& g = S.g;
+  cfm_encoder* h = S.h;
+  hipStream_t st = S.st;
+  const int dt = g.dt, d = g.d, M = g.M, H = g.H, dkp = g.dkp, es = g.es;
+  const long HP = (long)H * dkp;
+  int32_t* lens = S.T_<int32_t>(S.tp.lens);
+  calc_length(len_b, lens, g.B, g.T, 2, st);
+  HIP_OK(hipMemcpyAsync(S.T_(S.tp.xin), x_bft, (size_t)g.B * g.F * g.T * 4, hipMemcpyDeviceToDevice, st));
+
+  // ---- ConvSubsampling (subsampling.py:163-176) + xscale + embedding dropout ----
+  conv1_subsample(dt, x_bft, g.B, g.F, g.T, S.prm(S.i_c1w), S.prm(S.i_c1b), g.C, S.T_(S.tp.X1), st);
+  S.perm(S.prm(S.i_c2w), 2, S.W_(S.wl.wc2), false, S.kpad(9L * g.C), S.npad(g.C), S.kpad(9L * g.C));
+  S.bias(S.prm(S.i_c2b), g.C, S.W_<float>(S.wl.bc2));
+  {
+    ConvGeom cg{S.T_(S.tp.X1), g.T1, g.F1, g.T2, g.F2, g.C};
+    GemmEpi e = S.epi(EPI_RELU, S.W_<float>(S.wl.bc2));
+    e.C = S.T_(S.tp.X2);
+    e.ldc = g.C;
+    gemm_conv(dt, cg, g.B, S.W_(S.wl.wc2), S.kpad(9L * g.C), g.C, e, h->zero_page, st);
+  }
+  S.perm(S.prm(S.i_sw), 0, S.W_(S.wl.wsub), false, S.kpad((long)g.F2 * g.C), S.npad(d), S.kpad((long)g.F2 * g.C));
+  S.bias(S.prm(S.i_sb), d, S.W_<float>(S.wl.bsub));
+  const float xs = h->cfg.xscaling ? (float)std::sqrt((double)d) : 1.0f;
+  float* xcur = g.L > 0 ? S.T_<float>(S.tp.lay[0].x[0]) : S.T_<float>(S.tp.xfin);
+  S.gemm_f32out(S.T_(S.tp.X2), (long)g.F2 * g.C, M, g.F2 * g.C, S.W_(S.wl.wsub), d, S.W_<float>(S.wl.bsub), xs, xcur,
+                d, false);
+  {
+    const Drop dr = S.drop(0);
+    if (dr.thr) cfm_launch(scale_drop_kernel, dim3(ew_grid((long)M * d)), dim3(256), 0, st, (const float*)xcur, 1.0f,
+                           (long)M * d, dr, xcur);
+  }
+  const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
+  float* br = S.W_<float>(S.wl.br);
+  const long n_md = (long)M * d;
+
+  for (int l = 0; l < g.L; ++l) {
+    const LayerP& q = S.lp[l];
+    const TapeLayer& t = S.tp.lay[l];
+    float* X[5];
+    for (int i = 0; i < 5; ++i) X[i] = S.T_<float>(t.x[i]);
+    // ---- FFN1 / FFN2 (conformer_modules.py:99-101, 116-118, 183-200) ----
+    auto ffn = [&](int f, float* xin, void* hn, long z, float* xout) {
+      S.packW(S.prm(q.ff_w1[f]), g.dff, d, S.W_(S.wl.w1));
+      S.bias(S.prm(q.ff_b1[f]), g.dff, S.W_<float>(S.wl.b1));
+      S.packW(S.prm(q.ff_w2[f]), d, g.dff, S.W_(S.wl.w2));
+      S.bias(S.prm(q.ff_b2[f]), d, S.W_<float>(S.wl.b2));
+      GemmEpi e = S.epi(EPI_STORE, S.W_<float>(S.wl.b1));
+      e.C = S.T_(z);
+      e.ldc = g.dff;
+      gemm(dt, hn, d, M, d, S.W_(S.wl.w1), S.kpad(d), g.dff, e, h->zero_page, st);
+      const long n = (long)M * g.dff;
+      const Drop di = S.drop(site(l, f ? 4 : 0));
+      if (dt == DT_F32)
+        cfm_launch(swish_drop_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z), n, di,
+                   S.W_<float>(S.wl.u));
+      else
+        cfm_launch(swish_drop_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z), n, di,
+                   S.W_<bf16_t>(S.wl.u));
+      S.gemm_f32out(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(S.wl.w2), d, S.W_<float>(S.wl.b2), 1.0f, br, d, false);
+      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)xin, (const float*)br, 0.5f,
+                 n_md, S.drop(site(l, f ? 5 : 1)), xout);
+    };
+    layernorm(dt, X[0], M, d, S.prm(q.ln_w[LN_FF1]), S.prm(q.ln_b[LN_FF1]), nullptr, nullptr, nullptr, S.T_(t.hn[0]),
+              0, st);
+    ffn(0, X[0], S.T_(t.hn[0]), t.z1, X[1]);
+
+    // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
+    layernorm(dt, X[1], M, d, S.prm(q.ln_w[LN_ATT]), S.prm(q.ln_b[LN_ATT]), nullptr, nullptr, nullptr, S.T_(t.hn[1]),
+              0, st);
+    {
+      S.heads(S.prm(q.pos_w), nullptr, nullptr, 1, d, S.W_(S.wl.wpos), false, S.kpad(d), S.npad(HP));
+      GemmEpi ep = S.epi(EPI_STORE, nullptr);
+      ep.C = S.T_(t.P);
+      ep.ldc = HP;
+      gemm(dt, pe_slice, d, g.NP, d, S.W_(S.wl.wpos), S.kpad(d), (int)HP, ep, h->zero_page, st);
+      S.heads(S.prm(q.q_w), S.prm(q.k_w), S.prm(q.v_w), 3, d, S.W_(S.wl.wqkv), false, S.kpad(d), S.npad(3 * HP));
+      S.heads(S.prm(q.q_b), S.prm(q.k_b), S.prm(q.v_b), 3, 1, S.W_(S.wl.bqkv), true, 1, S.npad(3 * HP));
+      S.heads(S.prm(q.pu), S.prm(q.pv), nullptr, 2, 1, S.W_(S.wl.uv), true, 1, (int)(2 * HP));
+      GemmEpi e = S.epi(EPI_QKV, S.W_<float>(S.wl.bqkv));
+      e.C = S.T_(t.qk); e.ldc = 3 * HP; e.qk_cols = (int)(2 * HP); e.uv = S.W_<float>(S.wl.uv);
+      e.qscale = (float)(1.4426950408889634 / std::sqrt((double)g.dk));
+      e.Vt = S.T_(t.vt); e.H = H; e.dkp = dkp; e.vt_rows = h->vt_rows; e.Tpad = g.Tpad; e.Tp = g.Tp;
+      gemm(dt, S.T_(t.hn[1]), d, M, d, S.W_(S.wl.wqkv), S.kpad(d), (int)(3 * HP), e, h->zero_page, st);
+      rel_pos_attention(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B, g.Tp, H,
+                        g.dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, S.T_(t.ctx), d, st);
+      S.packW(S.prm(q.o_w), d, d, S.W_(S.wl.wout));
+      S.bias(S.prm(q.o_b), d, S.W_<float>(S.wl.bout));
+      S.gemm_f32out(S.T_(t.ctx), d, M, d, S.W_(S.wl.wout), d, S.W_<float>(S.wl.bout), 1.0f, br, d, false);
+      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[1], (const float*)br, 1.0f,
+                 n_md, S.drop(site(l, 2)), X[2]);
+    }
+
+    // ---- convolution module (conformer_modules.py:112-114, 160-180) ----
+    layernorm(dt, X[2], M, d, S.prm(q.ln_w[LN_CONV]), S.prm(q.ln_b[LN_CONV]), nullptr, nullptr, nullptr,
+              S.T_(t.hn[2]), 0, st);
+    {
+      S.packW(S.prm(q.pw1_w), 2 * d, d, S.W_(S.wl.wpw1));
+      S.bias(S.prm(q.pw1_b), 2 * d, S.W_<float>(S.wl.bpw1));
+      float* pre = S.T_<float>(t.pre);
+      S.gemm_f32out(S.T_(t.hn[2]), d, M, d, S.W_(S.wl.wpw1), 2 * d, S.W_<float>(S.wl.bpw1), 1.0f, pre, 2 * d, false);
+      if (dt == DT_F32)
+        cfm_launch(glu_fwd_kernel<float>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)pre,
+                   (const int32_t*)lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<float>(S.wl.gt));
+      else
+        cfm_launch(glu_fwd_kernel<bf16_t>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)pre,
+                   (const int32_t*)lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<bf16_t>(S.wl.gt));
+      // depthwise conv + bias (fp32 pre-norm output; [K][d] weight layout of the forward kernel)
+      pack_matrix(DT_F32, S.prm(q.dw_w), g.K, d, g.K, true, S.W_(S.wl.dww), d, g.K, d, st);
+      float* dwo = S.W_<float>(S.wl.dwo);
+      dwconv_norm_swish(dt, S.W_(S.wl.gt), g.B, g.Tp, d, g.K, S.W_<float>(S.wl.dww), S.prm(q.dw_b), nullptr, nullptr,
+                        nullptr, nullptr, nullptr, dwo, st);
+      // BatchNorm1d, training statistics (SyncBatchNorm over `world` ranks when a callback is given)
+      float* red = S.W_<float>(S.wl.red);
+      float* sy = S.W_<float>(S.wl.sync);
+      float* mean = S.T_<float>(t.mean);
+      float* rstd = S.T_<float>(t.rstd);
+      const double ntot = (double)M * S.o->world;
+      colred(dwo, nullptr, nullptr, d, M, d, 0, 1.0f, sy, 0, red, st);
+      S.sync(sy, d);
+      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)sy, ntot,
+                 d, 0.0f, mean, rstd, (float*)nullptr, (float*)nullptr, 0);
+      colred(dwo, nullptr, mean, d, M, d, 2, 1.0f, sy + d, 0, red, st);
+      S.sync(sy + d, d);
+      const bool upd = S.o->update_running_stats != 0;
+      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)(sy + d),
+                 ntot, d, S.o->bn_momentum, mean, rstd, upd ? (float*)S.prm(q.bn_rm) : (float*)nullptr,
+                 upd ? (float*)S.prm(q.bn_rv) : (float*)nullptr, 1);
+      if (dt == DT_F32)
+        cfm_launch(bn_swish_kernel<float>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dwo, (const float*)mean,
+                   (const float*)rstd, S.prm(q.bn_w), S.prm(q.bn_b), (long)M, d, S.T_<float>(t.xhat),
+                   S.T_<float>(t.s));
+      else
+        cfm_launch(bn_swish_kernel<bf16_t>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dwo,
+                   (const float*)mean, (const float*)rstd, S.prm(q.bn_w), S.prm(q.bn_b), (long)M, d,
+                   S.T_<float>(t.xhat), S.T_<bf16_t>(t.s));
+      S.packW(S.prm(q.pw2_w), d, d, S.W_(S.wl.wpw2));
+      S.bias(S.prm(q.pw2_b), d, S.W_<float>(S.wl.bpw2));
+      S.gemm_f32out(S.T_(t.s), d, M, d, S.W_(S.wl.wpw2), d, S.W_<float>(S.wl.bpw2), 1.0f, br, d, false);
+      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[2], (const float*)br, 1.0f,
+                 n_md, S.drop(site(l, 3)), X[3]);
+    }
+    layernorm(dt, X[3], M, d, S.prm(q.ln_w[LN_FF2]), S.prm(q.ln_b[LN_FF2]), nullptr, nullptr, nullptr, S.T_(t.hn[3]),
+              0, st);
+    ffn(1, X[3], S.T_(t.hn[3]), t.z2, X[4]);
+    // ---- norm_out (conformer_modules.py:120) -> next layer's input (fp32) ----
+    float* nxt = l + 1 < g.L ? S.T_<float>(S.tp.lay[l + 1].x[0]) : S.T_<float>(S.tp.xfin);
+    layernorm(dt, X[4], M, d, S.prm(q.ln_w[LN_OUT]), S.prm(q.ln_b[LN_OUT]), nxt, nullptr, nullptr, nullptr, 0, st);
+  }
+  // (B, T', d) -> (B, d, T') (conformer_encoder.py:280) and the encoded lengths
+  {
+    const dim3 grid((g.Tp + 31) / 32, (d + 31) / 32, g.B);
+    cfm_launch(btd_transpose_kernel, grid, dim3(256), 0, st, (const float*)S.T_<float>(S.tp.xfin), g.Tp, d, 1, y_bdt);
+    HIP_OK(hipMemcpyAsync(out_len_b, lens, (size_t)g.B * 4, hipMemcpyDeviceToDevice, st));
+  }
+}
+
+// =============================================================================================
+// backward
+// =============================================================================================
+void train_backward(Step& S, const float* dy_bdt, float* const* G) {
+  const Geo& g = S.g;
+  cfm_encoder* h = S.h;
+  hipStream_t st = S.st;
+  const int dt = g.dt, d = g.d, M = g.M, H = g.H, dkp = g.dkp, es = g.es;
+  const long HP = (long)H * dkp, n_md = (long)M * d;
+  const int32_t* lens = S.T_<const int32_t>(S.tp.lens);
+  float* gA = S.W_<float>(S.wl.gA);
+  float* gB = S.W_<float>(S.wl.gB);
+  float* dbr = S.W_<float>(S.wl.dbr);
+  float* red = S.W_<float>(S.wl.red);
+  void* pa = S.W_(S.wl.pa);
+  void* pat = S.W_(S.wl.pat);
+  void* pbt = S.W_(S.wl.pbt);
+  void* wt = S.W_(S.wl.wt);
+  const long Mq = g.Mq;
+  auto Gp = [&](int i) -> float* { return G ? G[i] : nullptr; };
+  // column sums of an fp32 (rows, n) gradient into a parameter gradient (if requested)
+  auto bias_grad = [&](const float* src, long ld, int rows, int n, int gi, float alpha = 1.0f) {
+    if (Gp(gi)) colred(src, nullptr, nullptr, ld, rows, n, 0, alpha, Gp(gi), 0, red, st);
+  };
+  // Linear y = x W^T + b backward for a dense fp32 output gradient dy (M, N):
+  //   dx (M, K) fp32 (ldx; accumulate or overwrite), dW (N, K) -> G[gw], db -> G[gb]
+  //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
+  auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
+                        float* dx, long ldx, bool acc, int gw, int gb) {
+    if (gb >= 0) bias_grad(dy, N, M, N, gb);
+    S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
+    if (dx) {
+      S.packWt(w, N, K, wt);
+      S.gemm_f32out(pa, S.kpad(N), M, N, wt, K, nullptr, 1.0f, dx, ldx, acc);
+    }
+    if (gw >= 0 && Gp(gw)) {
+      S.pack(dy, false, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
+      S.pack(xin, true, ldxin, M, K, true, 1.0f, pbt, Mq, S.npad(K), (int)Mq, xfn, xdr);
+      S.wgrad(pat, pbt, Mq, N, K, M, Gp(gw), K);
+    }
+  };
+  auto ln_bwd = [&](const float* x, int wi, int bi, const float* dy, float* dx, bool acc) {
+    // dx (+)= LN backward; prod (dy * xhat) reuses dbr
+    layernorm_backward(x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, dbr, st);
+    if (Gp(wi)) colred(dbr, nullptr, nullptr, d, M, d, 0, 1.0f, Gp(wi), 0, red, st);
+    bias_grad(dy, d, M, d, bi);
+  };
+
+  // dy (B, d, T') -> gA (B*T', d)
+  {
+    const dim3 grid((g.Tp + 31) / 32, (d + 31) / 32, g.B);
+    cfm_launch(btd_transpose_kernel, grid, dim3(256), 0, st, dy_bdt, g.Tp, d, 0, gA);
+  }
+  for (int l = g.L - 1; l >= 0; --l) {
+    const LayerP& q = S.lp[l];
+    const TapeLayer& t = S.tp.lay[l];
+    const float* X[5];
+    for (int i = 0; i < 5; ++i) X[i] = S.T_<const float>(t.x[i]);
+    // norm_out: gB = d x4
+    ln_bwd(X[4], q.ln_w[LN_OUT], q.ln_b[LN_OUT], gA, gB, false);
+
+    // FFN block backward: residual grad g (d xout) -> += d xin through the branch
+    auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, float* gres) {
+      float* dU = S.W_<float>(S.wl.dU);
+      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gres, 0.5f, n_md,
+                 S.drop(site(l, f ? 5 : 1)), dbr);
+      const Drop di = S.drop(site(l, f ? 4 : 0));
+      // linear2 (input u = dropout(swish(z)) recomputed from z)
+      linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f]);
+      const long n = (long)M * g.dff;
+      if (dt == DT_F32)
+        cfm_launch(swish_drop_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z),
+                   (const float*)dU, n, di, dU);
+      else
+        cfm_launch(swish_drop_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z),
+                   (const float*)dU, n, di, dU);
+      float* dhn = S.W_<float>(S.wl.dctx);
+      linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f], q.ff_b1[f]);
+      ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true);
+    };
+    ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, gB);   // gB = d x3
+
+    // ---- convolution module ----
+    {
+      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
+                 S.drop(site(l, 3)), dbr);
+      float* dS = S.W_<float>(S.wl.dD);
+      linear_bwd(dbr, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b);
+      float* dZ = S.W_<float>(S.wl.dG);
+      const float* xhat = S.T_<const float>(t.xhat);
+      cfm_launch(bn_swish_bwd_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dS, xhat, S.prm(q.bn_w),
+                 S.prm(q.bn_b), (long)M, d, dZ);
+      // BatchNorm backward: local sums -> dgamma/dbeta, global sums (SyncBN) -> dx
+      float* sy = S.W_<float>(S.wl.sync);
+      colred(dZ, nullptr, nullptr, d, M, d, 0, 1.0f, sy, 0, red, st);
+      colred(dZ, xhat, nullptr, d, M, d, 1, 1.0f, sy + d, 0, red, st);
+      if (Gp(q.bn_b)) HIP_OK(hipMemcpyAsync(Gp(q.bn_b), sy, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+      if (Gp(q.bn_w)) HIP_OK(hipMemcpyAsync(Gp(q.bn_w), sy + d, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+      S.sync(sy, 2L * d);
+      float* dD = dS;   // dS is dead after dZ
+      cfm_launch(bn_bwd_apply_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dZ, xhat, S.prm(q.bn_w),
+                 S.T_<const float>(t.rstd), (const float*)sy, (const float*)(sy + d),
+                 (float)(1.0 / ((double)M * S.o->world)), (long)M, d, dD);
+      // depthwise conv backward (dx, dw, db) from the fp32 GLU output
+      float* dG = dZ;   // dZ is dead after dD
+      const size_t dwws = cfm_op_dwconv_backward_ws_size(g.B, g.Tp, d, g.K);
+      const cfm_status s = cfm_op_dwconv_backward(S.T_<const float>(t.g), S.prm(q.dw_w), dD, g.B, g.Tp, d, g.K, dG,
+                                                  Gp(q.dw_w), Gp(q.dw_b), red, dwws, st);
+      if (s != CFM_OK) fail(s, std::string("dwconv backward: ") + g_last_error);
+      float* dpre = S.W_<float>(S.wl.dpre);
+      const cfm_status s2 = cfm_op_glu_backward(S.T_<const float>(t.pre), dG, lens, g.B, g.Tp, d, dpre, st);
+      if (s2 != CFM_OK) fail(s2, std::string("glu backward: ") + g_last_error);
+      float* dhn = S.W_<float>(S.wl.dctx);
+      linear_bwd(dpre, 2 * d, S.prm(q.pw1_w), d, S.T_(t.hn[2]), d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.pw1_w,
+                 q.pw1_b);
+      ln_bwd(X[2], q.ln_w[LN_CONV], q.ln_b[LN_CONV], dhn, gB, true);   // gB = d x2
+    }
+
+    // ---- attention ----
+    {
+      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
+                 S.drop(site(l, 2)), dbr);
+      float* dctx = S.W_<float>(S.wl.dctx);
+      linear_bwd(dbr, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b);
+      float* dqkv = S.W_<float>(S.wl.dqkv);
+      float* dP = S.W_<float>(S.wl.dP);
+      const int dk = g.dk;
+      rel_pos_attention_backward(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B,
+                                 g.Tp, H, dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, dctx, d, dqkv,
+                                 dqkv + d, dqkv + 2 * d, 3L * d, dP, d, Gp(q.pu), Gp(q.pv), S.W_(S.wl.attws), st);
+      // linear_pos (no bias): dWpos = dP^T . pos_emb   (pos_emb rows = the PE window, compute type)
+      if (Gp(q.pos_w)) {
+        const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
+        S.pack(dP, false, d, g.NP, d, true, 1.0f, pat, Mq, d, (int)Mq);
+        S.pack(pe_slice, true, d, g.NP, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
+        S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), d);
+      }
+      // q/k/v: biases, input gradient through [Wq; Wk; Wv], stacked weight gradient
+      bias_grad(dqkv, 3L * d, M, d, q.q_b);
+      bias_grad(dqkv + d, 3L * d, M, d, q.k_b);
+      bias_grad(dqkv + 2 * d, 3L * d, M, d, q.v_b);
+      S.pack(dqkv, false, 3L * d, M, 3 * d, false, 1.0f, pa, S.kpad(3L * d), M, S.kpad(3L * d));
+      {
+        const long ldw = S.kpad(3L * d);
+        const int wi[3] = {q.q_w, q.k_w, q.v_w};
+        for (int p = 0; p < 3; ++p)   // Wt[i][p*d + o] = W_p[o][i]
+          S.pack(S.prm(wi[p]), false, d, d, d, true, 1.0f, (char*)wt + (long)p * d * es, ldw, S.npad(d),
+                 p == 2 ? (int)(ldw - 2L * d) : d);
+        float* dhn = dctx;   // dctx consumed
+        S.gemm_f32out(pa, S.kpad(3L * d), M, 3 * d, wt, d, nullptr, 1.0f, dhn, d, false);
+        if (Gp(q.q_w) || Gp(q.k_w) || Gp(q.v_w)) {
+          S.pack(dqkv, false, 3L * d, M, 3 * d, true, 1.0f, pat, Mq, 3 * d, (int)Mq);
+          S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
+          float* tmp = S.W_<float>(S.wl.gtmp);   // (3d, d) stacked gradient
+          S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, d);
+          for (int p = 0; p < 3; ++p)
+            if (Gp(wi[p]))
+              HIP_OK(hipMemcpyAsync(Gp(wi[p]), tmp + (long)p * d * d, (size_t)d * d * 4, hipMemcpyDeviceToDevice, st));
+        }
+        ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true);   // gB = d x1
+      }
+    }
+    ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, gB);   // gB = d x0
+    std::swap(gA, gB);
+  }
+
+  // ---- subsampling backward: gA = d(layer-0 input) ----
+  const float xs = h->cfg.xscaling ? (float)std::sqrt((double)d) : 1.0f;
+  cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gA, xs, n_md, S.drop(0), dbr);
+  const int KS = g.F2 * g.C;
+  float* dX2 = S.W_<float>(S.wl.dX2);
+  bias_grad(dbr, d, M, d, S.i_sb);
+  S.pack(dbr, false, d, M, d, false, 1.0f, pa, S.kpad(d), M, S.kpad(d));
+  S.perm(S.prm(S.i_sw), 1, wt, false, S.kpad(d), S.npad(KS), S.kpad(d));
+  S.gemm_f32out(pa, S.kpad(d), M, d, wt, KS, nullptr, 1.0f, dX2, KS, false);
+  if (Gp(S.i_sw)) {
+    S.pack(dbr, false, d, M, d, true, 1.0f, pat, Mq, d, (int)Mq);
+    S.pack(S.T_(S.tp.X2), true, KS, M, KS, true, 1.0f, pbt, Mq, S.npad(KS), (int)Mq);
+    float* tmp = S.W_<float>(S.wl.gtmp);   // (d, KS) permuted gradient
+    S.wgrad(pat, pbt, Mq, d, KS, M, tmp, KS);
+    S.perm(tmp, 4, Gp(S.i_sw), true, KS, d, KS);
+  }
+  // conv2 + ReLU: dY2 = dX2 * [X2 > 0], rows (b, t2, f2) x C
+  const long n2 = g.M2 * g.C;
+  if (dt == DT_F32)
+    cfm_launch(relu_mask_kernel<float>, dim3(ew_grid(n2)), dim3(256), 0, st, dX2, S.T_<const float>(S.tp.X2), n2);
+  else
+    cfm_launch(relu_mask_kernel<bf16_t>, dim3(ew_grid(n2)), dim3(256), 0, st, dX2, S.T_<const bf16_t>(S.tp.X2), n2);
+  bias_grad(dX2, g.C, (int)g.M2, g.C, S.i_c2b);
+  const bool need_c1 = Gp(S.i_c1w) || Gp(S.i_c1b);
+  if (Gp(S.i_c2w)) {   // dW2 = dY2^T . im2col(X1)
+    S.pack(dX2, false, g.C, (int)g.M2, g.C, true, 1.0f, pat, g.M2p, g.C, (int)g.M2p);
+    const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C) + 31) / 32));
+    if (dt == DT_F32)
+      cfm_launch(im2col_t_kernel<float>, grid, dim3(256), 0, st, S.T_<const float>(S.tp.X1), g.T1, g.F1, g.T2, g.F2,
+                 g.C, (int)g.M2, S.W_<float>(S.wl.i2c), g.M2p, S.npad(9L * g.C));
+    else
+      cfm_launch(im2col_t_kernel<bf16_t>, grid, dim3(256), 0, st, S.T_<const bf16_t>(S.tp.X1), g.T1, g.F1, g.T2, g.F2,
+                 g.C, (int)g.M2, S.W_<bf16_t>(S.wl.i2c), g.M2p, S.npad(9L * g.C));
+    float* tmp = S.W_<float>(S.wl.gtmp);   // (C, 9C) permuted gradient
+    S.wgrad(pat, S.W_(S.wl.i2c), g.M2p, g.C, 9 * g.C, g.M2, tmp, 9L * g.C);
+    S.perm(tmp, 5, Gp(S.i_c2w), true, 9L * g.C, g.C, 9 * g.C);
+  }
+  if (need_c1) {   // dCol = dY2 . W2mat, col2im + conv1 ReLU mask, then conv1's weight/bias gradient
+    S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
+    S.perm(S.prm(S.i_c2w), 3, wt, false, S.kpad(g.C), S.npad(9L * g.C), S.kpad(g.C));
+    GemmEpi e = S.epi(EPI_STORE, nullptr);
+    e.C = S.W_(S.wl.dcol);
+    e.ldc = 9L * g.C;
+    gemm(dt, pa, S.kpad(g.C), (int)g.M2, g.C, wt, S.kpad(g.C), 9 * g.C, e, h->zero_page, st);
+    const long n1 = (long)g.B * g.T1 * g.F1 * g.C;
+    float* dy1 = S.W_<float>(S.wl.dy1);
+    if (dt == DT_F32)
+      cfm_launch(col2im_relu_kernel<float>, dim3(ew_grid(n1)), dim3(256), 0, st, S.W_<const float>(S.wl.dcol),
+                 S.T_<const float>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
+    else
+      cfm_launch(col2im_relu_kernel<bf16_t>, dim3(ew_grid(n1)), dim3(256), 0, st, S.W_<const bf16_t>(S.wl.dcol),
+                 S.T_<const bf16_t>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
+    bias_grad(dy1, g.C, g.B * g.T1 * g.F1, g.C, S.i_c1b);
+    if (Gp(S.i_c1w)) {
+      const int rows = g.B * g.T1, R = 8, nch = (rows + R - 1) / R;
+      float* part = S.W_<float>(S.wl.c1part);
+      cfm_launch(conv1_wgrad_kernel, dim3(nch, (g.C + 255) / 256), dim3(256), 0, st, S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1,
+                 g.C, (const float*)dy1, g.B, R, part);
+      colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
+    }
+  }
+}
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+size_t cfm_train_tape_size(const cfm_encoder* h, int B, int T) {
+  if (!h || B <= 0 || T <= 0) return 0;
+  return (size_t)tape_layout(h, make_geo(h, B, T)).total;
+}
+
+size_t cfm_train_workspace_size(const cfm_encoder* h, int B, int T) {
+  if (!h || B <= 0 || T <= 0) return 0;
+  return (size_t)ws_layout(h, make_geo(h, B, T)).total;
+}
+
+static void make_step(Step& S, cfm_encoder* h, const float* const* params, int n_params, int B, int T,
+                      const cfm_train_opts* opts, void* tape, size_t tape_bytes, void* ws, size_t ws_bytes,
+                      void* stream) {
+  check_common(h, params, n_params, B, T, opts);
+  S.h = h;
+  S.g = make_geo(h, B, T);
+  S.tp = tape_layout(h, S.g);
+  S.wl = ws_layout(h, S.g);
+  if (!tape || tape_bytes < (size_t)S.tp.total) fail(CFM_ERR_WORKSPACE, "tape too small");
+  if (!ws || ws_bytes < (size_t)S.wl.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+  S.tape = (char*)tape;
+  S.ws = (char*)ws;
+  S.st = (hipStream_t)stream;
+  S.P = params;
+  S.o = opts;
+  build_index(S);
+}
+
+cfm_status cfm_train_forward(cfm_encoder* h, const float* const* params, int n_params, const float* x_bft,
+                             const int32_t* len_b, int B, int T, const cfm_train_opts* opts, float* y_bdt,
+                             int32_t* out_len_b, void* tape, size_t tape_bytes, void* ws, size_t ws_bytes,
+                             void* stream) {
+  return guarded([&] {
+    if (!x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
+    Step S;
+    make_step(S, h, params, n_params, B, T, opts, tape, tape_bytes, ws, ws_bytes, stream);
+    train_forward(S, x_bft, len_b, y_bdt, out_len_b);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+cfm_status cfm_train_backward(cfm_encoder* h, const float* const* params, int n_params, const float* dy_bdt, int B,
+                              int T, const cfm_train_opts* opts, float* const* grads, const void* tape,
+                              size_t tape_bytes, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!dy_bdt) fail(CFM_ERR_INVALID_ARG, "null argument");
+    Step S;
+    make_step(S, h, params, n_params, B, T, opts, (void*)tape, tape_bytes, ws, ws_bytes, stream);
+    train_backward(S, dy_bdt, grads);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

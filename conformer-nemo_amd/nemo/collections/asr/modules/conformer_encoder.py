@@ -5,8 +5,14 @@ Same constructor kwargs (reference conformer_encoder.py:111-132), same module tr
 (outputs (B, d_model | feat_out, T') fp32, encoded_lengths (B,) int32).  The forward runs entirely in
 libcfm.so (include/cfm_encoder.h): one stream-ordered C call per forward on torch's current stream.
 
+Training mode (`.train()`) runs the native training step (include/cfm_train.h): a train-mode
+forward with dropout (embedding, FFN inner, residual branches) and batch-statistics BatchNorm
+(SyncBatchNorm across ranks after `set_sync_batchnorm(group)`), differentiable through
+torch.autograd — gradients land in each parameter's `.grad`, running stats update in place.
+
 Differences from the reference, by design:
-  * eval-mode forward only (dropout identities, BatchNorm running stats); `training=True` raises;
+  * training mode requires dropout_att == 0 and dropout_emb == 0 (attention-probability and
+    positional-embedding dropout are not built) and conv_norm_type='batch_norm';
   * update_max_seq_length's distributed MAX all_reduce (:283-294) is dropped: it only decides
     whether to regrow the positional table, which is regrown per process on demand instead;
   * compute precision is selectable: 'bf16' (default, MFMA bf16 operands / fp32 accumulation and
@@ -103,6 +109,10 @@ class ConformerEncoder(NeuralModule, Exportable):
         self._native_versions = {}  # (device, compute) -> weight version snapshot
         self.max_audio_length = pos_emb_max_len
         self.use_pad_mask = True
+        self._dropout, self._dropout_emb, self._dropout_att = float(dropout), float(dropout_emb), float(dropout_att)
+        self._trainers = {}         # (device, compute) -> EncoderTrainer
+        self._sync_bn_group = None
+        self._sync_bn = False
 
     # ---- reference API ---------------------------------------------------------------------
     def set_max_audio_length(self, max_audio_length):
@@ -123,6 +133,11 @@ class ConformerEncoder(NeuralModule, Exportable):
         mask = self.use_pad_mask
         self.use_pad_mask = on
         return mask
+
+    def set_sync_batchnorm(self, group=None):
+        """SyncBatchNorm over `group` (torch.distributed; RCCL on ROCm) in training mode."""
+        self._sync_bn = True
+        self._sync_bn_group = group
 
     def set_compute_mode(self, compute: str):
         if compute not in ("bf16", "fp32"):
@@ -156,6 +171,43 @@ class ConformerEncoder(NeuralModule, Exportable):
             self._native_versions[key] = version
         return enc
 
+    def _trainer_for(self, device: torch.device):
+        from conformer_amd import NativeEncoder, make_cfg
+        from conformer_amd.train import EncoderTrainer
+
+        key = (device.index if device.index is not None else torch.cuda.current_device(), self.compute)
+        tr = self._trainers.get(key)
+        if tr is None:
+            with torch.cuda.device(key[0]):
+                native = NativeEncoder(make_cfg(**self._native_cfg), device=key[0], compute=self.compute)
+                if self.max_audio_length > native.max_audio_length:
+                    native.set_max_audio_length(self.max_audio_length)
+            tr = EncoderTrainer(native)
+            self._trainers[key] = tr
+        if self._sync_bn:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size(self._sync_bn_group) > 1:
+                tr.set_sync_group(self._sync_bn_group)
+        return tr
+
+    def _train_forward(self, audio_signal, length):
+        from conformer_amd.train import encoder_train_forward
+
+        if self._dropout_att != 0.0 or self._dropout_emb != 0.0:
+            raise NotImplementedError("native training needs dropout_att == 0 and dropout_emb == 0")
+        tr = self._trainer_for(audio_signal.device)
+        if audio_signal.size(2) > tr.native.max_audio_length:
+            tr.native.set_max_audio_length(audio_signal.size(2))
+        sd = self.state_dict(keep_vars=True)
+        params = [sd[n] for n in tr.names]
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if self._dropout > 0 else 0
+        y, ylen = encoder_train_forward(tr, audio_signal, length, params, self._dropout, seed, True, 0.1)
+        for m in self.modules():   # BatchNorm1d bookkeeping done by the reference module in train mode
+            if isinstance(m, nn.BatchNorm1d) and m.num_batches_tracked is not None:
+                m.num_batches_tracked.add_(1)
+        self._native_versions = {}   # running stats changed in place: repack before the next eval forward
+        return y, ylen
+
     def _apply(self, fn, *args, **kwargs):
         self._native_versions = {}
         return super()._apply(fn, *args, **kwargs)
@@ -168,11 +220,11 @@ class ConformerEncoder(NeuralModule, Exportable):
 
     @typecheck()
     def forward_for_export(self, audio_signal, length=None):
-        if self.training:
-            raise NotImplementedError("the native Conformer encoder implements the eval-mode forward; call .eval()")
         if not self.use_pad_mask:
             raise NotImplementedError("enable_pad_mask(False) is not supported by the native path")
         if not audio_signal.is_cuda:
             raise RuntimeError("ConformerEncoder (MI355X-native) expects audio_signal on a ROCm GPU")
+        if self.training:
+            return self._train_forward(audio_signal, length)
         enc = self._native_for(audio_signal.device)
         return enc.forward(audio_signal, length)

@@ -72,6 +72,56 @@ cfm_status cfm_op_rel_attention_backward(int dtype, const void* q, const void* k
 /* dz = du * swish'(z) elementwise (n elements). */
 cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int64_t n, void* stream);
 
+/* ---- whole-encoder training step (csrc/train.hip) -------------------------------------------
+ * Replaces the autograd graph of ConformerEncoder.forward() in training mode
+ * (conformer_encoder.py:236-281 -> ConformerLayer.forward conformer_modules.py:88-121 with
+ * nn.Dropout active and BatchNorm1d on batch statistics) and its backward, as driven by
+ * EncDecCTCModel.training_step (ctc_models.py:485-514) through Lightning's loss.backward().
+ *
+ * `params` / `grads` are host arrays of DEVICE pointers with one entry per parameter-table row
+ * (cfm_encoder_param_name order, fp32, reference layouts).  Weights are read from `params` on
+ * every call (nothing is cached: update them in place between steps freely).  The train forward
+ * updates the batch_norm running_mean / running_var entries in place (momentum, unbiased variance,
+ * like nn.BatchNorm1d) when opts->update_running_stats != 0.  grads[i] may be NULL (gradient not
+ * wanted); non-NULL entries are overwritten (not accumulated); running-stat rows are ignored.
+ *
+ * The tape (caller-owned, cfm_train_tape_size bytes) carries the activations from the forward to
+ * the backward; it must be passed unmodified to cfm_train_backward with the same B, T and opts.
+ * The workspace (cfm_train_workspace_size) is scratch for either call.  Both calls are
+ * stream-ordered and host-sync free.
+ *
+ * SyncBatchNorm (conformer_ctc_bpe.yaml:175 sync_batchnorm: true): with world > 1 the library calls
+ * `allreduce(user, buf, n, stream)` on the host while enqueueing, to SUM n floats at `buf` (device,
+ * inside the workspace) over all ranks, stream-ordered on `stream` (e.g. an RCCL all-reduce); every
+ * rank must hold the same B and T.  Return 0 on success.
+ */
+typedef int (*cfm_allreduce_fn)(void* user, float* buf, int64_t n, void* stream);
+
+typedef struct cfm_train_opts {
+  float dropout;               /* ConformerEncoder(dropout=): embedding, FFN inner and residual-branch dropout */
+  float dropout_emb;           /* must be 0 (positional-embedding dropout not built; yaml default 0.0)      */
+  float dropout_att;           /* must be 0 (attention-probability dropout not built)                        */
+  float bn_momentum;           /* nn.BatchNorm1d momentum (0.1)                                               */
+  int update_running_stats;    /* 1: update running_mean / running_var in place                              */
+  int world;                   /* ranks sharing the BatchNorm statistics (1 = plain BatchNorm1d)             */
+  uint64_t seed;               /* dropout mask seed; use a fresh one per step                                */
+  cfm_allreduce_fn allreduce;  /* required when world > 1                                                    */
+  void* allreduce_user;
+} cfm_train_opts;
+
+size_t cfm_train_tape_size(const cfm_encoder* h, int B, int T);
+size_t cfm_train_workspace_size(const cfm_encoder* h, int B, int T);
+/* x_bft (B, feat_in, T) fp32, len_b (B,) int32 or NULL -> y_bdt (B, d_model, T') fp32, out_len_b (B,) int32 */
+cfm_status cfm_train_forward(cfm_encoder* h, const float* const* params, int n_params, const float* x_bft,
+                             const int32_t* len_b, int B, int T, const cfm_train_opts* opts, float* y_bdt,
+                             int32_t* out_len_b, void* tape, size_t tape_bytes, void* ws, size_t ws_bytes,
+                             void* stream);
+/* dy_bdt (B, d_model, T') fp32 = dLoss/dy -> grads (see above).  No input gradient (audio_signal
+ * is a leaf without grad in every reference training path). */
+cfm_status cfm_train_backward(cfm_encoder* h, const float* const* params, int n_params, const float* dy_bdt, int B,
+                              int T, const cfm_train_opts* opts, float* const* grads, const void* tape,
+                              size_t tape_bytes, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

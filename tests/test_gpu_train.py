@@ -1,0 +1,124 @@
+"""GPU parity of the whole-encoder training step (include/cfm_train.h) against the REFERENCE
+ConformerEncoder in training mode under torch autograd (tests/golden/train_*.npz, written by
+gen_train_goldens.py): encoder output, every parameter gradient (loss = sum(y * R)) and the
+BatchNorm running statistics after one step, through the drop-in module in `.train()` mode.
+
+Gates: fp32 compute mode rel-L2 <= 1e-3 on the output and on every gradient (the north-star fp32
+tolerance); bf16 operands rel-L2 <= 2e-2 on the output and <= 6e-2 per gradient (bf16 GEMM
+operands through two layers of backward).  Gradients are compared relative to
+max(|ref|, 1e-2 x the step's largest gradient norm).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_l2
+
+pytestmark = pytest.mark.gpu
+CASES = ["train_tiny", "train_tiny_dk10", "train_tiny_ctx"]
+GATE_Y = {"fp32": 1e-3, "bf16": 2e-2}
+GATE_G = {"fp32": 1e-3, "bf16": 6e-2}
+
+
+def _encoder(z, compute, dropout=0.0):
+    from nemo.collections.asr.modules import ConformerEncoder
+    from recipe import make_state_dict
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(**cfg, dropout=dropout, dropout_emb=0.0, dropout_att=0.0)
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
+    enc.set_compute_mode(compute)
+    return enc.cuda().train()
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES)
+def test_train_step_matches_reference(case, compute):
+    z = np.load(os.path.join(GOLDEN, case + ".npz"))
+    enc = _encoder(z, compute)
+    x = torch.from_numpy(z["x"]).cuda()
+    ln = torch.from_numpy(z["lengths"]).cuda()
+    y, ylen = enc(audio_signal=x, length=ln)
+    (y * torch.from_numpy(z["dy"]).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    assert (ylen.cpu().numpy() == z["ylen"]).all()
+    e = rel_l2(y.detach().cpu().numpy(), z["y"])
+    assert e <= GATE_Y[compute], f"output relL2 {e:.3e}"
+    params = dict(enc.named_parameters())
+    worst = (0.0, "")
+    # some gradients are analytically ~0 (depthwise-conv bias: train-mode BatchNorm removes any
+    # per-channel shift), so the relative error is taken against a floor of 1e-2 x the largest
+    # gradient norm of the step
+    floor = 1e-2 * max(float(np.linalg.norm(z[k])) for k in z.files if k.startswith("grad__"))
+    for k in z.files:
+        if not k.startswith("grad__"):
+            continue
+        name = k[len("grad__"):]
+        g = params[name].grad
+        assert g is not None, f"no gradient for {name}"
+        err = float(np.linalg.norm(g.cpu().numpy().astype(np.float64) - z[k]) / max(np.linalg.norm(z[k]), floor))
+        worst = max(worst, (err, name))
+        assert err <= GATE_G[compute], f"{name}: grad relL2 {err:.3e} > {GATE_G[compute]}"
+    bufs = dict(enc.named_buffers())
+    for k in z.files:
+        if k.startswith("buf__"):
+            err = rel_l2(bufs[k[len("buf__"):]].cpu().numpy(), z[k])
+            assert err <= GATE_G[compute], f"{k}: relL2 {err:.3e}"
+    print(f"{case}/{compute}: y relL2 {e:.2e}, worst grad {worst[1]} {worst[0]:.2e}")
+
+
+def test_train_step_deterministic_and_dropout():
+    """Same seed -> bitwise-identical gradients; dropout > 0 changes the output, keeps it finite,
+    and its masks are regenerated consistently in the backward (directional derivative check)."""
+    z = np.load(os.path.join(GOLDEN, "train_tiny.npz"))
+    x = torch.from_numpy(z["x"]).cuda()
+    ln = torch.from_numpy(z["lengths"]).cuda()
+    dy = torch.from_numpy(z["dy"]).cuda()
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(123)
+        enc = _encoder(z, "fp32", dropout=0.1)
+        y, _ = enc(audio_signal=x, length=ln)
+        (y * dy).sum().backward()
+        runs.append((y.detach().clone(), [p.grad.clone() for p in enc.parameters()]))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
+    assert torch.isfinite(runs[0][0]).all()
+    assert rel_l2(runs[0][0].cpu().numpy(), z["y"]) > 1e-3      # dropout did something
+    # directional derivative along one weight, same dropout masks (same seed): (L(w+h v) - L(w-h v)) / 2h
+    torch.manual_seed(123)
+    enc = _encoder(z, "fp32", dropout=0.1)
+    w = enc.layers[0].feed_forward1.linear1.weight
+    v = torch.randn_like(w)
+    g_dir = float((runs[0][1][[n for n, _ in enc.named_parameters()].index("layers.0.feed_forward1.linear1.weight")]
+                   * v).sum())
+    h = 1e-3
+    vals = []
+    for s in (1.0, -1.0):
+        torch.manual_seed(123)
+        e2 = _encoder(z, "fp32", dropout=0.1)
+        with torch.no_grad():
+            e2.layers[0].feed_forward1.linear1.weight.add_(s * h * v)
+        y2, _ = e2(audio_signal=x, length=ln)
+        vals.append(float((y2.double() * dy.double()).sum()))
+    fd = (vals[0] - vals[1]) / (2 * h)
+    assert abs(fd - g_dir) <= 2e-2 * max(abs(g_dir), 1.0), (fd, g_dir)
+
+
+def test_train_then_eval_uses_updated_running_stats():
+    z = np.load(os.path.join(GOLDEN, "train_tiny.npz"))
+    enc = _encoder(z, "fp32")
+    x = torch.from_numpy(z["x"]).cuda()
+    ln = torch.from_numpy(z["lengths"]).cuda()
+    with torch.no_grad():
+        y0, _ = enc.eval()(audio_signal=x, length=ln)
+        enc.train()
+        enc(audio_signal=x, length=ln)
+        y1, _ = enc.eval()(audio_signal=x, length=ln)
+    assert int(enc.layers[0].conv.batch_norm.num_batches_tracked) == 1
+    assert not torch.equal(y0, y1)   # eval repacked the in-place-updated running statistics

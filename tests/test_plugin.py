@@ -38,16 +38,18 @@ def test_state_dict_layout_matches_reference():
         assert tuple(sd[k].shape) == tuple(shp), k
 
 
-def test_forward_is_keyword_only_and_training_is_refused():
+def test_forward_is_keyword_only_and_cpu_is_refused():
+    """No CPU fallback: eval and train forwards on CPU tensors raise (the product path is HIP only)."""
     from nemo.collections.asr.modules import ConformerEncoder
     enc = ConformerEncoder(feat_in=80, n_layers=1, d_model=64, n_heads=4)
     x = torch.zeros(1, 80, 16)
     ln = torch.tensor([16])
     with pytest.raises(TypeError):
         enc(x, ln)
-    enc.train()
-    with pytest.raises(NotImplementedError):
-        enc(audio_signal=x, length=ln)
+    for mode in (enc.eval, enc.train):
+        mode()
+        with pytest.raises(RuntimeError):
+            enc(audio_signal=x, length=ln)
 
 
 def test_neural_types_and_input_example():
