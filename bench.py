@@ -123,6 +123,10 @@ def main():
     ap.add_argument("--layers", type=int, default=17)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
     ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--mode", default="forward", choices=["forward", "train"],
+                    help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
+                         "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW)")
+    ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,6 +145,8 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    if args.mode == "train":
+        return run_train(args, world, rank, dev, dist, barrier)
     from nemo.collections.asr.modules import ConformerEncoder
     torch.manual_seed(0)
     d, H, L, B, T = 512, 8, args.layers, args.batch, args.seq
@@ -224,6 +230,86 @@ def main():
                             "frac_of_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
             "cpu_baseline": cpu,
             "breakdown": breakdown,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+TRAIN_METRIC = "training-step audio-frames/sec, Conformer-CTC-Large B=32/GPU T=1000 (BASELINE config 3)"
+
+
+def run_train(args, world, rank, dev, dist, barrier):
+    """BASELINE config 3: one step = encoder train-mode forward (dropout 0.1, batch-statistics BatchNorm,
+    SyncBatchNorm across ranks) + ConvASRDecoder + CTCLoss(mean_batch) + backward + ONE flat RCCL
+    gradient all-reduce + AdamW (conformer_ctc_bpe.yaml optim: betas 0.9/0.98, wd 1e-3).
+    Synthetic targets U=60 uniform in [0, V)."""
+    from conformer_amd import dist as cdist
+    from nemo.collections.asr.losses import CTCLoss
+    from nemo.collections.asr.modules import ConformerEncoder, ConvASRDecoder
+    torch.manual_seed(0)
+    d, H, L, B, T, V, U = 512, 8, args.layers, args.batch, args.seq, args.vocab, 60
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H, dropout=0.1, dropout_emb=0.0,
+                           dropout_att=0.0).to(dev).train()
+    dec = ConvASRDecoder(feat_in=d, num_classes=V).to(dev).train()
+    for m in (enc, dec):
+        m.set_compute_mode(args.compute)
+    if dist:
+        cdist.convert_sync_batchnorm(enc)
+    loss_fn = CTCLoss(num_classes=V, zero_infinity=True, reduction="mean_batch")
+    params = [p for m in (enc, dec) for p in m.parameters()]
+    try:
+        opt = torch.optim.AdamW(params, lr=1e-4, betas=(0.9, 0.98), weight_decay=1e-3, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.AdamW(params, lr=1e-4, betas=(0.9, 0.98), weight_decay=1e-3, foreach=True)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, 80, T, device=dev, generator=g)
+    lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
+    targets = torch.randint(0, V, (B, U), device=dev, generator=g)
+    tlen = torch.full((B,), U, dtype=torch.int64, device=dev)
+    bucket = [None]
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        y, yl = enc(audio_signal=x, length=lengths)
+        lp = dec(encoder_output=y)
+        loss = loss_fn(log_probs=lp, targets=targets, input_lengths=yl, target_lengths=tlen)
+        loss.backward()
+        if dist:
+            bucket[0] = cdist.allreduce_gradients(params, bucket=bucket[0])
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    assert torch.isfinite(loss).item()
+    t_max = max_over_ranks(elapsed, dev, dist)
+    value = job_throughput(t_max, world, B, T, args.steps)
+    ms_step = 1000.0 * t_max / args.steps
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from conformer_oracle import encoder_flops
+        fwd = encoder_flops(B, T, d, L)
+        n_par = sum(p.numel() for p in params)
+        out = {
+            "metric": TRAIN_METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
+            "config": {"workload": f"Conformer-CTC-Large training step (encoder d512/8 heads/{L} layers, dropout 0.1, "
+                                   f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss "
+                                   f"U={U}, AdamW), B={B}/GPU, T={T}",
+                       "global_batch": B * world, "seq_len": T,
+                       "parallelism": f"dp{world}" + (" (1 flat RCCL gradient all-reduce per step)" if dist else "")},
+            "model_flops": {"GFLOP_per_step_per_gpu_(3x_fwd)": round(3 * fwd / 1e9, 1),
+                            "TFLOP/s_per_gpu": round(3 * fwd / (ms_step * 1e-3) / 1e12, 1),
+                            "frac_of_peak": round(3 * fwd / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+            "params": n_par, "loss": round(float(loss), 4),
         }
         print(json.dumps(out), flush=True)
     if dist:

@@ -50,3 +50,53 @@ def test_single_rank_is_identity():
     import bench
     assert bench.max_over_ranks(0.25, torch.device("cpu"), False) == 0.25
     assert bench.job_throughput(2.0, 1, 32, 1000, 4) == 32 * 1000 * 4 / 2.0
+
+
+# ---- training-step data parallelism (conformer_amd.dist, conformer_amd.train) on CPU tensors ----
+
+def _dp_worker(rank, world, port, q):
+    import ctypes
+
+    sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
+    from conformer_amd import dist as cdist
+    from conformer_amd.train import EncoderTrainer
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        # one flat all-reduce averages every .grad (shared parameters counted once)
+        ps = [torch.nn.Parameter(torch.zeros(3, 2)), torch.nn.Parameter(torch.zeros(5))]
+        ps[0].grad = torch.full((3, 2), float(rank + 1))
+        ps[1].grad = torch.arange(5, dtype=torch.float32) * (rank + 1)
+        bucket = cdist.allreduce_gradients(ps + [ps[0]])
+        assert bucket is not None and bucket.numel() >= 11
+        # SyncBatchNorm statistics callback: sums a float view of the (here CPU) workspace in place
+        tr = EncoderTrainer.__new__(EncoderTrainer)
+        tr._group, tr.world = None, world
+        tr._ws = torch.zeros(64, dtype=torch.uint8)
+        view = tr._ws[16:32].view(torch.float32)
+        view.copy_(torch.tensor([1.0, 2.0, 3.0, 4.0]) * (rank + 1))
+        cb = tr._make_callback()
+        rc = cb(None, ctypes.c_void_p(tr._ws.data_ptr() + 16), 4, None)
+        rc_bad = cb(None, ctypes.c_void_p(tr._ws.data_ptr() + 60), 4, None)   # outside the workspace
+        q.put((rank, ps[0].grad.tolist(), ps[1].grad.tolist(), rc, rc_bad, view.tolist(),
+               cdist.shard_batch(torch.arange(8), rank, world).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_allreduce_and_syncbn_callback_gloo_ws2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    for rank, g0, g1, rc, rc_bad, view, shard in res:
+        assert g0 == [[1.5, 1.5]] * 3                          # (1 + 2) / 2
+        assert g1 == [1.5 * i for i in range(5)]
+        assert rc == 0 and rc_bad != 0
+        assert view == [3.0, 6.0, 9.0, 12.0]                   # summed, not averaged
+        assert shard == list(range(4 * rank, 4 * rank + 4))

@@ -1,0 +1,87 @@
+"""Data-parallel training step on the GPU: two ranks, each holding half of the global
+batch, SyncBatchNorm statistics summed across ranks (the cfm_train.h all-reduce callback) and one
+flat gradient all-reduce (conformer_amd.dist.allreduce_gradients), must reproduce the REFERENCE's
+single-process global-batch gradients (tests/golden/train_tiny_ctx.npz) averaged over ranks, and
+the global-batch BatchNorm running statistics.
+
+The box has one GPU, so both ranks share cuda:0 and talk over gloo (RCCL refuses two ranks on one
+device); the collective calls are the same torch.distributed calls the RCCL path makes.
+"""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    for p in (os.path.join(ROOT, "conformer-nemo_amd"), os.path.join(ROOT, "tests", "golden")):
+        sys.path.insert(0, p)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from conformer_amd import dist as cdist
+        from nemo.collections.asr.modules import ConformerEncoder
+        from recipe import make_state_dict
+        torch.cuda.set_device(0)
+        z = np.load(os.path.join(GOLDEN, "train_tiny_ctx.npz"))
+        cfg = json.loads(str(z["cfg_json"]))
+        enc = ConformerEncoder(**cfg, dropout=0.0, dropout_emb=0.0, dropout_att=0.0)
+        sd = make_state_dict(cfg, int(z["seed"]))
+        ref = enc.state_dict()
+        enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
+        enc.set_compute_mode("fp32")
+        enc = enc.cuda().train()
+        cdist.convert_sync_batchnorm(enc)
+        x = cdist.shard_batch(torch.from_numpy(z["x"]), rank, world).cuda()
+        ln = cdist.shard_batch(torch.from_numpy(z["lengths"]), rank, world).cuda()
+        dy = cdist.shard_batch(torch.from_numpy(z["dy"]), rank, world).cuda()
+        y, _ = enc(audio_signal=x, length=ln)
+        (y * dy).sum().backward()
+        cdist.allreduce_gradients(enc.parameters())
+        torch.cuda.synchronize()
+        worst = 0.0
+        floor = 1e-2 * max(float(np.linalg.norm(z[k])) for k in z.files if k.startswith("grad__"))
+        params = dict(enc.named_parameters())
+        for k in z.files:
+            if k.startswith("grad__"):
+                ref_g = z[k] / world
+                got = params[k[len("grad__"):]].grad.cpu().numpy()
+                worst = max(worst, float(np.linalg.norm(got - ref_g) / max(np.linalg.norm(ref_g), floor / world)))
+        bufs = dict(enc.named_buffers())
+        wb = max(float(np.linalg.norm(bufs[k[5:]].cpu().numpy() - z[k]) / np.linalg.norm(z[k]))
+                 for k in z.files if k.startswith("buf__"))
+        yl = float(np.linalg.norm(y.detach().cpu().numpy() - cdist.shard_batch(torch.from_numpy(z["y"]), rank,
+                                                                               world).numpy()))
+        q.put((rank, worst, wb, yl))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp2_syncbn_gradients_match_global_batch():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(150)
+        assert p.exitcode == 0
+    for rank, worst, wb, yl in sorted(q.get(timeout=5) for _ in range(world)):
+        print(f"rank {rank}: worst grad {worst:.2e}, running stats {wb:.2e}, |dy| {yl:.2e}")
+        assert worst <= 1e-3 and wb <= 1e-4
