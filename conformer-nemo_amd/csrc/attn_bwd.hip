@@ -16,6 +16,8 @@
 // Masked scores get zero gradient: the reference fills them with -10000 before the softmax and
 // zeroes their probabilities after it (:106-107), so both paths into them carry no gradient.
 #include <cmath>
+#include <initializer_list>
+#include <type_traits>
 
 #include "../../include/cfm_train.h"
 #include "cfm_abi.h"
@@ -31,6 +33,7 @@ struct BgArgs {
   float* C; long cm, cn, cz1, cz2;        // C(m, n) fp32
   int M, N, K, Z2;                        // batch z = blockIdx.z = z1 * Z2 + z2
   float alpha; int accumulate;
+  int Ktot;                               // split-K over z2: slice z2 covers K rows [z2*K, min((z2+1)*K, Ktot)) (0 = off)
 };
 
 // C = alpha * A.B (+ C).  64x64 output tile per 4-wave block (2x2 waves of 32x32 MFMA tiles), K in
@@ -48,6 +51,7 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
   const TB* Bm = (const TB*)a.B + z1 * a.bz1 + z2 * a.bz2;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const bool a_kc = a.ak == 1, b_kc = a.bk == 1;
+  const int KZ = a.Ktot ? min(a.K, a.Ktot - z2 * a.K) : a.K;
   float ra[8], rb[8];
   auto coord = [&](bool kc, int e, int& r, int& k) {
     const int idx = e * 256 + tid;
@@ -59,10 +63,10 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
       int r, k;
       coord(a_kc, e, r, k);
       const int gm = m0 + r, gk = k0 + k;
-      ra[e] = (gm < a.M && gk < a.K) ? ld_f<TA>(A + gm * a.am + gk * a.ak) : 0.0f;
+      ra[e] = (gm < a.M && gk < KZ) ? ld_f<TA>(A + gm * a.am + gk * a.ak) : 0.0f;
       coord(b_kc, e, r, k);
       const int gn = n0 + r, gk2 = k0 + k;
-      rb[e] = (gn < a.N && gk2 < a.K) ? ld_f<TB>(Bm + gk2 * a.bk + gn * a.bn) : 0.0f;
+      rb[e] = (gn < a.N && gk2 < KZ) ? ld_f<TB>(Bm + gk2 * a.bk + gn * a.bn) : 0.0f;
     }
   };
   f32x16 acc = {};
@@ -70,7 +74,7 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
   const char* ap = As + (wm * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
   const char* bp = Bs + (wn * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
   load(0);
-  for (int k0 = 0; k0 < a.K; k0 += 32) {
+  for (int k0 = 0; k0 < KZ; k0 += 32) {
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -81,7 +85,7 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
       st_f<T>((T*)(Bs + r * RB) + k, rb[e]);
     }
     __syncthreads();
-    if (k0 + 32 < a.K) load(k0 + 32);
+    if (k0 + 32 < KZ) load(k0 + 32);
 #pragma unroll
     for (int s = 0; s < (int)sizeof(T); ++s)
       mfma_slab<T>(acc, *(const uint4*)(ap + 32 * s), *(const uint4*)(bp + 32 * s));
@@ -99,11 +103,130 @@ __global__ __launch_bounds__(256) void bgemm_kernel(BgArgs a) {
   }
 }
 
+// v2: same contract, K-steps of 64 through a double-buffered LDS image (one barrier per step) and
+// 4-element vector global loads along whichever operand stride is 1.  Requires every stride and
+// base offset to be a multiple of 4 elements (checked on the host; v1 otherwise).
+template <typename TS> struct Quad;
+template <> struct Quad<float> {
+  static CFM_DEV void ld(const float* p, float* v) { const float4 q = *(const float4*)p; v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w; }
+};
+template <> struct Quad<bf16_t> {
+  static CFM_DEV void ld(const bf16_t* p, float* v) {
+    const uint2 q = *(const uint2*)p;
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+};
+
+template <typename TA, typename TB, typename T>
+__global__ __launch_bounds__(256) void bgemm2_kernel(BgArgs a) {
+  constexpr int KS = 64;
+  constexpr int RB = KS * (int)sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char As[2][64 * RB];
+  __shared__ __attribute__((aligned(16))) char Bs[2][64 * RB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int z = blockIdx.z, z1 = z / a.Z2, z2 = z - z1 * a.Z2;
+  const TA* A = (const TA*)a.A + z1 * a.az1 + z2 * a.az2;
+  const TB* Bm = (const TB*)a.B + z1 * a.bz1 + z2 * a.bz2;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const bool a_kc = a.ak == 1, b_kc = a.bk == 1;
+  const int KZ = a.Ktot ? min(a.K, a.Ktot - z2 * a.K) : a.K;
+  float ra[16], rb[16];
+  // quad q of this thread: kc -> row r = idx >> 4, k = 4 * (idx & 15); else k = idx >> 4, row = 4 * (idx & 15)
+  auto loadop = [&](auto* P, long sr, long sk, bool kc, int r0, int R, int k0, float* v) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = q * 256 + tid;
+      const int hi = idx >> 4, lo = 4 * (idx & 15);
+      const int r = r0 + (kc ? hi : lo), k = k0 + (kc ? lo : hi);
+      float* o = v + 4 * q;
+      if (kc ? (r < R && k + 3 < KZ) : (k < KZ && r + 3 < R)) {
+        Quad<typename std::remove_cv<typename std::remove_pointer<decltype(P)>::type>::type>::ld(P + r * sr + k * sk, o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = kc ? r : r + e, kk = kc ? k + e : k;
+          o[e] = (rr < R && kk < KZ) ? ld_f(P + rr * sr + kk * sk) : 0.0f;
+        }
+      }
+    }
+  };
+  auto store = [&](char* S, bool kc, const float* v) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = q * 256 + tid;
+      const int hi = idx >> 4, lo = 4 * (idx & 15);
+      if (kc) {
+        T* d = (T*)(S + hi * RB) + lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st_f<T>(d + e, v[4 * q + e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) st_f<T>((T*)(S + (lo + e) * RB) + hi, v[4 * q + e]);
+      }
+    }
+  };
+  f32x16 acc = {};
+  const int wm = w & 1, wn = w >> 1;
+  const int aoff = (wm * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
+  const int boff = (wn * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
+  loadop(A, a.am, a.ak, a_kc, m0, a.M, 0, ra);
+  loadop(Bm, a.bn, a.bk, b_kc, n0, a.N, 0, rb);
+  store(As[0], a_kc, ra);
+  store(Bs[0], b_kc, rb);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < KZ; k0 += KS) {
+    const bool more = k0 + KS < KZ;
+    if (more) {
+      loadop(A, a.am, a.ak, a_kc, m0, a.M, k0 + KS, ra);
+      loadop(Bm, a.bn, a.bk, b_kc, n0, a.N, k0 + KS, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < KS * (int)sizeof(T) / 32; ++s)
+      mfma_slab<T>(acc, *(const uint4*)(As[buf] + aoff + 32 * s), *(const uint4*)(Bs[buf] + boff + 32 * s));
+    if (more) {
+      store(As[buf ^ 1], a_kc, ra);
+      store(Bs[buf ^ 1], b_kc, rb);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  float* C = a.C + z1 * a.cz1 + z2 * a.cz2;
+  const int n = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + wm * 32 + acc_row(r, lane);
+    if (m < a.M && n < a.N) {
+      float* c = C + m * a.cm + n * a.cn;
+      const float v = a.alpha * acc[r];
+      *c = a.accumulate ? *c + v : v;
+    }
+  }
+}
+
 enum { OP_F32 = 0, OP_CT = 1 };   // operand storage: fp32, or the compute type
+
+bool quad_ok(const void* p, int es, std::initializer_list<long> strides) {
+  if (((uintptr_t)p) % (4 * es)) return false;
+  for (long s : strides)
+    if (s != 1 && s % 4) return false;
+  return true;
+}
 
 template <typename T>
 void bgemm_t(const BgArgs& a, int ta, int tb, int Z, hipStream_t st) {
   const dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, Z), block(256);
+  const int esa = ta == OP_F32 ? 4 : (int)sizeof(T), esb = tb == OP_F32 ? 4 : (int)sizeof(T);
+  const bool v2 = (a.ak == 1 || a.am == 1) && (a.bk == 1 || a.bn == 1) &&
+                  quad_ok(a.A, esa, {a.am, a.ak, a.az1, a.az2}) && quad_ok(a.B, esb, {a.bk, a.bn, a.bz1, a.bz2});
+  if (v2) {
+    if (ta == OP_F32 && tb == OP_F32) cfm_launch((bgemm2_kernel<float, float, T>), grid, block, 0, st, a);
+    else if (ta == OP_F32) cfm_launch((bgemm2_kernel<float, T, T>), grid, block, 0, st, a);
+    else if (tb == OP_F32) cfm_launch((bgemm2_kernel<T, float, T>), grid, block, 0, st, a);
+    else cfm_launch((bgemm2_kernel<T, T, T>), grid, block, 0, st, a);
+    return;
+  }
   if (ta == OP_F32 && tb == OP_F32) cfm_launch((bgemm_kernel<float, float, T>), grid, block, 0, st, a);
   else if (ta == OP_F32) cfm_launch((bgemm_kernel<float, T, T>), grid, block, 0, st, a);
   else if (tb == OP_F32) cfm_launch((bgemm_kernel<T, float, T>), grid, block, 0, st, a);
@@ -183,6 +306,18 @@ __global__ __launch_bounds__(256) void attn_dscore_kernel(const float* __restric
   for (int j = lane; j < Tp; j += 64) dp[j] = p[j] * (dp[j] - D);
 }
 
+// dst[r][c] = sum_s part[s][r][c] (fixed order), part rows of `cols` floats
+__global__ void slab_rows_kernel(const float* __restrict__ part, int S, long rows, int cols, float* __restrict__ dst,
+                                 long ldd) {
+  const long n = rows * cols;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    float a = part[e];
+    for (int s = 1; s < S; ++s) a += part[(long)s * n + e];
+    const long r = e / cols;
+    dst[r * ldd + (e - r * cols)] = a;
+  }
+}
+
 __global__ void add_rows_kernel(float* __restrict__ dst, long ldd, const float* __restrict__ src, long lds, long rows,
                                 int cols) {
   const long n = rows * cols;
@@ -194,7 +329,8 @@ __global__ void add_rows_kernel(float* __restrict__ dst, long ldd, const float* 
 }
 
 struct BwdGeom {
-  long sld, gld, s_bytes, g_bytes, t_bytes, cs_bytes;
+  long sld, gld, s_bytes, g_bytes, t_bytes, cs_bytes, p_bytes;
+  static constexpr int kPosSplit = 16;    // split-K of the position-gradient GEMM (K = B*T')
   BwdGeom(int B, int Tp, int H, int dk) {
     sld = round_up(Tp, 4);
     gld = round_up(2L * Tp - 1, 4);
@@ -203,8 +339,9 @@ struct BwdGeom {
     g_bytes = round_up(BH * Tp * gld * 4, 256);
     t_bytes = round_up((long)B * Tp * H * dk * 4, 256);
     cs_bytes = round_up((long)col_sums_ws(B * Tp, H * dk), 256);
+    p_bytes = round_up((long)kPosSplit * (2L * Tp - 1) * H * dk * 4, 256);
   }
-  size_t total() const { return (size_t)(2 * s_bytes + g_bytes + t_bytes + cs_bytes); }
+  size_t total() const { return (size_t)(2 * s_bytes + g_bytes + t_bytes + cs_bytes + p_bytes); }
 };
 
 }  // namespace
@@ -299,13 +436,19 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
     bgemm(dt, a, OP_F32, OP_F32, Z, st);
   }
-  // dp[h] = sum_(b,i) G^T . (q+v)c * ln2: one GEMM per head with K = B*T' ((b, i) rows are uniform in G and qk)
+  // dp[h] = sum_(b,i) G^T . (q+v)c * ln2: per head a GEMM with K = B*T' ((b, i) rows are uniform in
+  // G and qk), split S ways along K (z = h * S + s) into fp32 slabs, then summed in a fixed order
   if (dpos) {
-    BgArgs a = A0(G, 1, g.gld, (long)B * szg, 0);
-    setB(a, qkc + (long)H * dkp * es, ldqk, 1, dkp, 0);
-    setC(a, dpos, ld_dpos, 1, dk, 0);
-    a.M = 2 * Tp - 1; a.N = dk; a.K = (int)BT; a.Z2 = 1; a.alpha = ln2; a.accumulate = 0;
-    bgemm(dt, a, OP_F32, OP_CT, H, st);
+    const int S = BwdGeom::kPosSplit;
+    const int kc = (int)((BT + S - 1) / S);
+    const long NP = 2L * Tp - 1;
+    float* part = (float*)(ws + 2 * g.s_bytes + g.g_bytes + g.t_bytes + g.cs_bytes);   // [s][NP][H*dk]
+    BgArgs a = A0(G, 1, g.gld, (long)B * szg, (long)kc * g.gld);
+    setB(a, qkc + (long)H * dkp * es, ldqk, 1, dkp, (long)kc * ldqk);
+    setC(a, part, (long)H * dk, 1, dk, NP * H * dk);
+    a.M = (int)NP; a.N = dk; a.K = kc; a.Z2 = S; a.alpha = ln2; a.accumulate = 0; a.Ktot = (int)BT;
+    bgemm(dt, a, OP_F32, OP_CT, H * S, st);
+    cfm_launch(slab_rows_kernel, dim3(1024), dim3(256), 0, st, (const float*)part, S, NP, H * dk, dpos, ld_dpos);
   }
 }
 

@@ -40,25 +40,37 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
   }
 }
 
-// Column sums, stage 1: partial[chunk][n] = sum of rows [chunk*R, (chunk+1)*R) (threads = columns,
-// so every row read is coalesced); stage 2 adds the chunks in order.  Fixed order: bitwise reproducible.
+// Column sums, stage 1: partial[chunk][n] = sum of a 256-row chunk (block = 64 columns x 4 row lanes,
+// every row read a coalesced 256-byte segment); stage 2 folds the chunks (16 columns x 16 lanes).
+// Fixed order: bitwise reproducible.
+constexpr int kColRows = 256;
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ src, long ld, int M, int N,
-                                                             int R, float* __restrict__ partial) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  const int chunk = blockIdx.y;
-  if (n >= N) return;
-  const int r0 = chunk * R, r1 = min(M, r0 + R);
+                                                             float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c, nc = min(n, N - 1);
+  const int r0 = blockIdx.y * kColRows, r1 = min(M, r0 + kColRows);
   float s = 0.0f;
-  for (int r = r0; r < r1; ++r) s += src[(long)r * ld + n];
-  partial[(long)chunk * N + n] = s;
+  for (int r = r0 + rl; r < r1; r += 4) s += src[(long)r * ld + nc];
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) partial[(long)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int nchunks, int N,
                                                            float* __restrict__ out, int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  __shared__ float red[16][17];
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + c, nc = min(n, N - 1);
   float s = 0.0f;
-  for (int c = 0; c < nchunks; ++c) s += partial[(long)c * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][c];
+    out[n] = accumulate ? out[n] + v : v;
+  }
 }
 
 // LayerNorm backward, one wave per row (E4 float4 chunks per lane, d % 4 == 0):
@@ -298,15 +310,15 @@ void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, b
 }
 
 size_t col_sums_ws(int M, int N) {
-  const int R = 64, nchunks = (M + R - 1) / R;
+  const int nchunks = (M + kColRows - 1) / kColRows;
   return (size_t)nchunks * N * 4;
 }
 
 void col_sums(const float* src, long ld, int M, int N, float* out, int accumulate, float* ws, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  const int R = 64, nchunks = (M + R - 1) / R;
-  cfm_launch(colsum_partial_kernel, dim3((N + 255) / 256, nchunks), dim3(256), 0, st, src, ld, M, N, R, ws);
-  cfm_launch(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, (const float*)ws, nchunks, N, out, accumulate);
+  const int nchunks = (M + kColRows - 1) / kColRows;
+  cfm_launch(colsum_partial_kernel, dim3((N + 63) / 64, nchunks), dim3(256), 0, st, src, ld, M, N, ws);
+  cfm_launch(colsum_final_kernel, dim3((N + 15) / 16), dim3(256), 0, st, (const float*)ws, nchunks, N, out, accumulate);
 }
 
 void layernorm_backward(const float* x, const float* w, const float* dy, int M, int d, float* dx, int accumulate,

@@ -80,6 +80,9 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
 // As gemm() with the packed operand's row stride ldw (elements) decoupled from K (split-K slices).
 void gemm_ldw(int dtype, const void* A, long lda, int M, int K, const void* Wp, long ldw, int N, const GemmEpi& epi,
               const void* zero_page, hipStream_t st);
+// Split-K: S slices of kchunk K-elements in one launch (grid.y), fp32 partials at epi.X + s*split_x.
+void gemm_splitk(int dtype, const void* A, long lda, int M, int K, const void* Wp, long ldw, int N, int S, int kchunk,
+                 const GemmEpi& epi, long split_x, const void* zero_page, hipStream_t st);
 // -1 = automatic tile choice; otherwise 0:128x128 1:256x128 2:128x256 3:64x128. Returns the previous value.
 int set_gemm_tile_override(int tile);
 // Microbenchmark probe bits for the dense GEMM (1 no main-loop loads, 2 no epilogue, 4 one K-step); 0 in production.

@@ -278,13 +278,41 @@ __global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
     const int s2 = s + 2;
     skipn[j] = (s2 < S) && (s2 & 1) && s2 >= 3 && tg[(s2 >> 1)] != tg[(s2 >> 1) - 1];
   }
+  // label bookkeeping once per utterance (LDS): fl[k] = k is the first occurrence of its class,
+  // nx[k] = next k' > k with the same class (-1: none)
+  int* fl = (int*)(vs + 2 * a.U + 1);
+  int* nx = fl + a.U;
+  for (int k = lane; k < Ub; k += 64) {
+    const int c = tg[k];
+    int first = 1, nk = -1;
+    for (int k2 = 0; k2 < k; ++k2) first &= tg[k2] != c;
+    for (int k2 = Ub - 1; k2 > k; --k2)
+      if (tg[k2] == c) nk = k2;
+    fl[k] = first;
+    nx[k] = nk;
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
   float bt[SPL];
 #pragma unroll
   for (int j = 0; j < SPL; ++j) bt[j] = NEG_INF;
-  for (int t = Tb - 1; t >= 0; --t) {
-    float e[SPL];
+  float e[SPL], av[SPL];
 #pragma unroll
-    for (int j = 0; j < SPL; ++j) e[j] = Eb[(long)t * K1 + col[j]];
+  for (int j = 0; j < SPL; ++j) {
+    const int s = lane * SPL + j;
+    e[j] = Eb[(long)(Tb - 1) * K1 + col[j]];
+    av[j] = s < S ? Ab[(long)(Tb - 1) * S + s] : NEG_INF;
+  }
+  for (int t = Tb - 1; t >= 0; --t) {
+    // prefetch the next (earlier) frame's emissions and alphas while this frame is processed
+    float e_n[SPL], av_n[SPL];
+    const int tn = max(t - 1, 0);
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+      const int s = lane * SPL + j;
+      e_n[j] = Eb[(long)tn * K1 + col[j]];
+      av_n[j] = Ab[(long)tn * S + min(s, S - 1)];
+    }
     const float dn1 = __shfl_down(bt[0], 1, 64);
     const float dn2 = __shfl_down(SPL >= 2 ? bt[1] : NEG_INF, 1, 64);
     const float n1l = lane == 63 ? NEG_INF : dn1, n2l = lane == 63 ? NEG_INF : dn2;
@@ -306,7 +334,7 @@ __global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
     for (int j = 0; j < SPL; ++j) {
       bt[j] = nw[j];
       const int s = lane * SPL + j;
-      if (s < S) vs[s] = Ab[(long)t * S + s] + bt[j];
+      if (s < S) vs[s] = av[j] + bt[j];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -323,22 +351,21 @@ __global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
       const float lpv = lpt[a.blank];
       gt[a.blank] = a.scale * (expf(lpv) - expf(lcab_blank + nll - lpv));
     }
-    // labels: the first occurrence k of each class sums every k' with the same label
+    // labels: the first occurrence k of each class sums every k' with the same label (nx chain)
     for (int k = lane; k < Ub; k += 64) {
-      const int c = tg[k];
-      bool first = true;
-      for (int k2 = 0; k2 < k; ++k2) first &= tg[k2] != c;
-      if (!first) continue;
+      if (!fl[k]) continue;
       float lc = NEG_INF;
-      for (int k2 = k; k2 < Ub; ++k2)
-        if (tg[k2] == c) lc = lse2(lc, vs[2 * k2 + 1]);
+      for (int k2 = k; k2 >= 0; k2 = nx[k2]) lc = lse2(lc, vs[2 * k2 + 1]);
       if (lc != NEG_INF) {
+        const int c = tg[k];
         const float lpv = lpt[c];
         gt[c] = a.scale * (expf(lpv) - expf(lc + nll - lpv));
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) { e[j] = e_n[j]; av[j] = av_n[j]; }
   }
 }
 
@@ -577,7 +604,7 @@ cfm_status cfm_ctc_loss(const float* logprobs_btc, const int32_t* targets_bu, co
       if (grad_btc) {
         cfm_launch(ctc_grad_base_kernel, dim3((unsigned)std::min<long>(((long)T * C + 255) / 256, 512), B), dim3(256), 0,
                    st, a);
-        cfm_launch(kbeta, dim3(B), dim3(64), (uint32_t)(S * 4), st, a);
+        cfm_launch(kbeta, dim3(B), dim3(64), (uint32_t)((S + 2 * U) * 4), st, a);
       }
     };
     if (spl <= 2) per_spl(ctc_alpha_kernel<2>, ctc_beta_kernel<2>);

@@ -106,6 +106,7 @@ struct ALoadDense {
   static constexpr bool kConv = false;
   const char* A; long lda_b; int M; long kbytes; const char* zero;
   struct State { const char* row_ptr[G]; };
+  CFM_DEV void shift_k(long koff) { A += koff; kbytes -= koff; }
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -125,6 +126,7 @@ struct ALoadConv {
   static constexpr bool kConv = true;   // conv2 + ReLU only
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
   struct State { const char* base[G]; uint32_t valid[G]; };
+  CFM_DEV void shift_k(long) {}   // never split
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
 #pragma unroll
     for (int i = 0; i < G; ++i) {
@@ -157,8 +159,12 @@ struct ALoadConv {
   }
 };
 
+thread_local int g_splits = 1;   // grid.y of the next split-K launch (gemm_splitk)
+
 struct GemmParams {
   const char* W; long ldw_b; int kb; int Mtiles, Ntiles; int M, N;   // kb = packed K bytes per row
+  long split_x;   // split-K (gridDim.y > 1, dense A only): slice y covers K bytes [y*kb, (y+1)*kb) and
+                  // writes its fp32 partial at epi.X + y * split_x
   int probe;   // microbenchmark probes only (cfm_bench_gemm): 1 no main-loop loads, 2 no epilogue, 4 one K-step
   GemmEpi epi;
 };
@@ -168,7 +174,7 @@ struct GemmParams {
 // under a per-thread condition is branched around by hipcc and serialised behind its own
 // vmcnt(0) (cdna_hip_programming.md §5, 'Three .s-level traps' (c)).
 template <typename T, int EPI, class TL>
-CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
+CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, long xoff) {
   const GemmEpi& e = p.epi;
   const int tid = threadIdx.x;
   if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
@@ -185,7 +191,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
         const int m = min(m0 + r0 + q * RPP, p.M - 1);
-        xv[q] = *(const float4*)(e.X + (long)m * e.ldx + nc);
+        xv[q] = *(const float4*)(e.X + xoff + (long)m * e.ldx + nc);
       }
     }
 #pragma unroll
@@ -200,7 +206,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0) {
       } else {
         o.x = a.x * e.alpha; o.y = a.y * e.alpha; o.z = a.z * e.alpha; o.w = a.w * e.alpha;
       }
-      if (colok && m < p.M) *(float4*)(e.X + (long)m * e.ldx + n) = o;
+      if (colok && m < p.M) *(float4*)(e.X + xoff + (long)m * e.ldx + n) = o;
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
     // packed columns: per 64-column group g, [0,32) = value channels 32g.., [32,64) = gates
@@ -336,13 +342,15 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     rows[i] = (i * TL::NW + wave) * TL::RPI + lane / TL::SLOTS;
     aslot[i] = ((lane % TL::SLOTS) ^ TL::swz(rows[i])) * 16;
   }
+  const long koff = (long)blockIdx.y * p.kb;   // split-K slice (0 without split)
+  aload.shift_k(koff);
   typename ALoad::State ast;
   aload.prepare(ast, m0, rows);
   const char* wrow[TL::GB];
 #pragma unroll
   for (int i = 0; i < TL::GB; ++i) {
     const int rr = (i * TL::NW + wave) * TL::RPI + lane / TL::SLOTS;
-    wrow[i] = p.W + (long)(n0 + rr) * p.ldw_b + ((lane % TL::SLOTS) ^ TL::swz(rr)) * 16;
+    wrow[i] = p.W + koff + (long)(n0 + rr) * p.ldw_b + ((lane % TL::SLOTS) ^ TL::swz(rr)) * 16;
   }
   const uint32_t smem_base = lds_addr(smem);
 
@@ -456,7 +464,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
         }
     }
     __syncthreads();
-    epilogue<T, EPI, EpiView<TL>>(p, img, m0 + pass * EpiView<TL>::BM, n0);
+    epilogue<T, EPI, EpiView<TL>>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x);
   }
 }
 
@@ -465,7 +473,7 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   using ALoad = AL<TL::GA>;
   ALoad al;
   args.fill(al);
-  const dim3 grid(p.Mtiles * p.Ntiles), block(TL::NT);
+  const dim3 grid(p.Mtiles * p.Ntiles, p.split_x > 0 ? g_splits : 1), block(TL::NT);
   if constexpr (ALoad::kConv) {
     cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al);
     return;
@@ -553,6 +561,7 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
   p.ldw_b = (long)Kpad * es;
   p.kb = (int)((long)Kpad * es);
   p.probe = 0;
+  p.split_x = 0;
   p.Mtiles = p.Ntiles = 0;
   p.M = M;
   p.N = N;
@@ -599,6 +608,24 @@ void gemm_ldw(int dtype, const void* A, long lda, int M, int K, const void* Wp, 
   int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
+}
+
+// Split-K GEMM: slice s (of S) contracts K elements [s*kchunk, min((s+1)*kchunk, K)) and writes its
+// fp32 partial to epi.X + s * split_x (EPI_SCALE_F32 only).  kchunk % (128 bytes / es) == 0; the
+// packed operand rows (ldw) must hold S * kchunk elements (zero beyond K).  One launch, grid.y = S.
+void gemm_splitk(int dtype, const void* A, long lda, int M, int K, const void* Wp, long ldw, int N, int S, int kchunk,
+                 const GemmEpi& epi, long split_x, const void* zero_page, hipStream_t st) {
+  if (M <= 0 || K <= 0) return;
+  const int es = dtype_size(dtype);
+  GemmParams p = make_params(es, M, Wp, (int)ldw, N, epi);
+  p.kb = kchunk * es;
+  p.split_x = split_x;
+  g_splits = S;
+  DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
+  int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
+  if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
+  else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
+  g_splits = 1;
 }
 
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,

@@ -71,11 +71,14 @@ unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n 
 // ---------------------------------------------------------------------------------------------
 // dst[i][j] = scale * fn(src)[transpose ? (j, i) : (i, j)] in the compute type, zero outside src.
 // fn 0 = identity, 1 = dropout(swish(.)) (the FFN hidden recomputed from its pre-activation; the
-// mask index is the source element (row * cols + col)).  32x32 LDS tiles.
+// mask index is the source element (row * cols + col)).  32x32 LDS tiles.  Destination row
+// `ones_row` (transposed packs) is set to 1 over the source rows: appended to the x^T operand of a
+// weight-gradient GEMM it makes the GEMM also produce the bias gradient (sum of dy over rows).
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src, long src_ld, int rows, int cols,
                                                     int transpose, float scale, int fn, Drop drop,
-                                                    Tout* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad) {
+                                                    Tout* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad,
+                                                    int ones_row) {
   __shared__ float tile[32][33];
   const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -93,7 +96,9 @@ __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src,
   __syncthreads();
   for (int k = ty; k < 32; k += 8) {
     const int di = i0 + k, dj = j0 + tx;
-    if (di < rows_pad && dj < cols_pad) st_f<Tout>(dst + (long)di * dst_ld + dj, transpose ? tile[tx][k] : tile[k][tx]);
+    float v = transpose ? tile[tx][k] : tile[k][tx];
+    if (di == ones_row) v = dj < rows ? 1.0f : 0.0f;   // bias column of a weight-gradient GEMM
+    if (di < rows_pad && dj < cols_pad) st_f<Tout>(dst + (long)di * dst_ld + dj, v);
   }
 }
 
@@ -185,31 +190,85 @@ __global__ __launch_bounds__(256) void glu_fwd_kernel(const float* __restrict__ 
 // ---------------------------------------------------------------------------------------------
 // reductions (fixed order: bitwise reproducible)
 // ---------------------------------------------------------------------------------------------
-// partial[chunk][n] = sum of rows [chunk*R, ...) of f(src) with f 0: x, 1: x*y, 2: (x - mean[n])^2
+// Column reduction out[n] (+)= alpha * sum_r f(src[r][n]) with f 0: x, 1: x*y, 2: (x - mean[n])^2.
+// Stage 1: block = 64 columns x 4 row lanes over a 256-row chunk (every row read is a coalesced
+// 256-byte segment); stage 2 folds the chunks the same way.  Fixed order: bitwise reproducible.
+constexpr int kRedRows = 256;
+template <int F>
 __global__ __launch_bounds__(256) void colred_partial_kernel(const float* __restrict__ src, const float* __restrict__ y,
                                                              const float* __restrict__ mean, long ld, int M, int N,
-                                                             int R, int f, float* __restrict__ partial) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  const int r0 = blockIdx.y * R, r1 = min(M, r0 + R);
-  const float mu = f == 2 ? mean[n] : 0.0f;
+                                                             float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int r0 = blockIdx.y * kRedRows, r1 = min(M, r0 + kRedRows);
+  const int nc = min(n, N - 1);
+  const float mu = F == 2 ? mean[nc] : 0.0f;
   float s = 0.0f;
-  for (int r = r0; r < r1; ++r) {
-    const float v = src[(long)r * ld + n];
-    s += f == 0 ? v : (f == 1 ? v * y[(long)r * ld + n] : (v - mu) * (v - mu));
+  for (int r = r0 + rl; r < r1; r += 4) {
+    const float v = src[(long)r * ld + nc];
+    s += F == 0 ? v : (F == 1 ? v * y[(long)r * ld + nc] : (v - mu) * (v - mu));
   }
-  partial[(long)blockIdx.y * N + n] = s;
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) partial[(long)blockIdx.y * N + n] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
+// stage 2: block = 16 columns x 16 chunk lanes (more blocks in flight for narrow N)
 __global__ __launch_bounds__(256) void colred_final_kernel(const float* __restrict__ partial, int nchunks, int N,
                                                            float alpha, float* __restrict__ out, int accumulate) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  __shared__ float red[16][17];
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + c;
+  const int nc = min(n, N - 1);
   float s = 0.0f;
-  for (int c = 0; c < nchunks; ++c) s += partial[(long)c * N + n];
-  s *= alpha;
-  out[n] = accumulate ? out[n] + s : s;
+  for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][c];
+    v *= alpha;
+    out[n] = accumulate ? out[n] + v : v;
+  }
 }
-constexpr int kRedRows = 64;
+// out[i] = sum_s part[s * n + i] (split-K partial slabs, fixed order), float4 when n % 4 == 0
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ part, int S, long n,
+                                                       float* __restrict__ out) {
+  if ((n & 3) == 0) {
+    const long n4 = n >> 2;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      float4 a = ((const float4*)part)[i];
+      for (int s = 1; s < S; ++s) {
+        const float4 b = ((const float4*)(part + (long)s * n))[i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      ((float4*)out)[i] = a;
+    }
+  } else {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+      float a = part[i];
+      for (int s = 1; s < S; ++s) a += part[(long)s * n + i];
+      out[i] = a;
+    }
+  }
+}
+// Weight-gradient slabs with an appended bias column: part[s][n][0..K+4) ->
+//   w[n][k] = sum_s part[s][n][k] (k < K), b[n] = sum_s part[s][n][K]
+__global__ __launch_bounds__(256) void slab_sum_wb_kernel(const float* __restrict__ part, int S, int N, int K,
+                                                          float* __restrict__ w, float* __restrict__ b) {
+  const int ldk = K + 4;
+  const long n = (long)N * ldk;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / ldk), k = (int)(i - (long)r * ldk);
+    if (k > K) continue;
+    float a = part[i];
+    for (int s2 = 1; s2 < S; ++s2) a += part[(long)s2 * n + i];
+    if (k < K) { if (w) w[(long)r * K + k] = a; }
+    else if (b) b[r] = a;
+  }
+}
+
 size_t colred_ws(long M, long N) { return (size_t)((M + kRedRows - 1) / kRedRows) * N * 4; }
 void colred(const float* src, const float* y, const float* mean, long ld, int M, int N, int f, float alpha, float* out,
             int accumulate, float* ws, hipStream_t st) {
@@ -219,10 +278,105 @@ void colred(const float* src, const float* y, const float* mean, long ld, int M,
     return;
   }
   const int nch = (M + kRedRows - 1) / kRedRows;
-  cfm_launch(colred_partial_kernel, dim3((N + 255) / 256, nch), dim3(256), 0, st, src, y, mean, ld, M, N, kRedRows, f,
-             ws);
-  cfm_launch(colred_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, (const float*)ws, nch, N, alpha, out,
-             accumulate);
+  const dim3 g1((N + 63) / 64, nch), b(256);
+  if (f == 0) cfm_launch(colred_partial_kernel<0>, g1, b, 0, st, src, y, mean, ld, M, N, ws);
+  else if (f == 1) cfm_launch(colred_partial_kernel<1>, g1, b, 0, st, src, y, mean, ld, M, N, ws);
+  else cfm_launch(colred_partial_kernel<2>, g1, b, 0, st, src, y, mean, ld, M, N, ws);
+  cfm_launch(colred_final_kernel, dim3((N + 15) / 16), b, 0, st, (const float*)ws, nch, N, alpha, out, accumulate);
+}
+
+// LayerNorm backward (eps 1e-5, biased variance; torch.nn.LayerNorm) for 8 rows per wave, 32 rows per
+// block, with the weight/bias gradient column partials reduced in-block (fixed order):
+//   dx (+)= rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
+//   pw[blk][c] = sum over the block's rows of dy * xhat,  pb[blk][c] = sum of dy
+constexpr int kLnRowsPerWave = 8;
+template <int E4>
+__global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ dy, int M, int d,
+                                                           float* __restrict__ dx, int accumulate,
+                                                           float* __restrict__ pw, float* __restrict__ pb) {
+#pragma clang fp contract(off)
+  __shared__ float4 red[2][4][64 * E4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int d4 = d >> 2;
+  const float4* wr = (const float4*)w;
+  float4 wv4[E4], aw[E4], ab[E4];
+#pragma unroll
+  for (int e = 0; e < E4; ++e) {
+    wv4[e] = wr[min(lane + 64 * e, d4 - 1)];
+    aw[e] = make_float4(0, 0, 0, 0);
+    ab[e] = make_float4(0, 0, 0, 0);
+  }
+  const float inv_d = 1.0f / (float)d;
+  for (int i = 0; i < kLnRowsPerWave; ++i) {
+    const int row = (blockIdx.x * 4 + wv) * kLnRowsPerWave + i;
+    if (row >= M) break;
+    const float4* xr = (const float4*)(x + (long)row * d);
+    const float4* dr = (const float4*)(dy + (long)row * d);
+    float4 xv[E4], dv[E4];
+    float sx = 0.0f;
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      const int g = min(lane + 64 * e, d4 - 1);
+      const bool ok = lane + 64 * e < d4;
+      xv[e] = ok ? xr[g] : make_float4(0, 0, 0, 0);
+      dv[e] = ok ? dr[g] : make_float4(0, 0, 0, 0);
+      sx += xv[e].x + xv[e].y + xv[e].z + xv[e].w;
+    }
+    const float mean = wave_sum(sx) * inv_d;
+    float q = 0.0f;
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      if (lane + 64 * e < d4) {
+        const float a0 = xv[e].x - mean, a1 = xv[e].y - mean, a2 = xv[e].z - mean, a3 = xv[e].w - mean;
+        q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+      }
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) * inv_d + 1e-5f);
+    float sg = 0.0f, sgx = 0.0f;
+    float4 xh[E4], gv[E4];
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      xh[e] = make_float4((xv[e].x - mean) * rstd, (xv[e].y - mean) * rstd, (xv[e].z - mean) * rstd,
+                          (xv[e].w - mean) * rstd);
+      gv[e] = make_float4(dv[e].x * wv4[e].x, dv[e].y * wv4[e].y, dv[e].z * wv4[e].z, dv[e].w * wv4[e].w);
+      if (lane + 64 * e < d4) {
+        sg += gv[e].x + gv[e].y + gv[e].z + gv[e].w;
+        sgx += gv[e].x * xh[e].x + gv[e].y * xh[e].y + gv[e].z * xh[e].z + gv[e].w * xh[e].w;
+      }
+    }
+    const float mg = wave_sum(sg) * inv_d, mgx = wave_sum(sgx) * inv_d;
+    float4* dxr = (float4*)(dx + (long)row * d);
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      const int g = lane + 64 * e;
+      if (g < d4) {
+        float4 o = make_float4(rstd * (gv[e].x - mg - xh[e].x * mgx), rstd * (gv[e].y - mg - xh[e].y * mgx),
+                               rstd * (gv[e].z - mg - xh[e].z * mgx), rstd * (gv[e].w - mg - xh[e].w * mgx));
+        if (accumulate) {
+          const float4 a = dxr[g];
+          o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+        }
+        dxr[g] = o;
+        aw[e].x += dv[e].x * xh[e].x; aw[e].y += dv[e].y * xh[e].y;
+        aw[e].z += dv[e].z * xh[e].z; aw[e].w += dv[e].w * xh[e].w;
+        ab[e].x += dv[e].x; ab[e].y += dv[e].y; ab[e].z += dv[e].z; ab[e].w += dv[e].w;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E4; ++e) { red[0][wv][lane + 64 * e] = aw[e]; red[1][wv][lane + 64 * e] = ab[e]; }
+  __syncthreads();
+  for (int c4 = threadIdx.x; c4 < d4; c4 += 256) {
+    float4 a = red[0][0][c4], b = red[1][0][c4];
+    for (int k = 1; k < 4; ++k) {
+      const float4 u = red[0][k][c4], v = red[1][k][c4];
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    }
+    ((float4*)(pw + (long)blockIdx.x * d))[c4] = a;
+    ((float4*)(pb + (long)blockIdx.x * d))[c4] = b;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -355,18 +509,20 @@ __global__ __launch_bounds__(256) void im2col_t_kernel(const T* __restrict__ x1,
   __syncthreads();
   for (int k = ty; k < 32; k += 8) {
     const int r = r0 + k, m = m0 + tx;
-    if (r < rows_pad && m < ld) st_f<T>(dst + (long)r * ld + m, tile[tx][k]);
+    float v = tile[tx][k];
+    if (r == 9 * C) v = m < M2 ? 1.0f : 0.0f;   // ones row: the GEMM's column 9C is conv2's bias gradient
+    if (r < rows_pad && m < ld) st_f<T>(dst + (long)r * ld + m, v);
   }
 }
 // conv1 weight gradient, stage 1: partial[chunk][c][tap] = sum over the chunk's (b, t1) rows and all
 // f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T))
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int F, int T, int T1, int F1,
                                                           int C, const float* __restrict__ dy1, int B, int R,
-                                                          float* __restrict__ partial) {
+                                                          float* __restrict__ partial, float* __restrict__ partial_b) {
   __shared__ float xs[3][264];
   const int chunk = blockIdx.x;
   const int c = blockIdx.y * 256 + threadIdx.x;
-  float acc[9];
+  float acc[9], accb = 0.0f;
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = 0.0f;
   const int r0 = chunk * R, r1 = min(B * T1, r0 + R);
@@ -382,6 +538,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
       const float* g = dy1 + ((long)bt * F1) * C + c;
       for (int f1 = 0; f1 < F1; ++f1) {
         const float gv = g[(long)f1 * C];
+        accb += gv;
 #pragma unroll
         for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
@@ -392,6 +549,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
   if (c < C) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) partial[((long)chunk * C + c) * 9 + k] = acc[k];
+    partial_b[(long)chunk * C + c] = accb;
   }
 }
 
@@ -450,9 +608,10 @@ Geo make_geo(const cfm_encoder* h, int B, int T) {
   g.d = h->d; g.dff = h->dff; g.H = h->H; g.dk = h->dk; g.dkp = h->dkp; g.C = h->C; g.F = h->F; g.F1 = h->F1;
   g.F2 = h->F2; g.K = h->K; g.L = h->L; g.es = h->es; g.dt = h->dtype; g.kg = GEMM_BK_BYTES / h->es;
   g.Mp = round_up(std::max(g.M, 1), g.kg);
-  g.Mq = round_up(std::max(g.M, g.NP), g.kg);
+  // + 16 granules of zero columns: split-K slices (<= 16, each a multiple of kg) never read past a row
+  g.Mq = round_up(std::max(g.M, g.NP), g.kg) + 16L * g.kg;
   g.M2 = (long)B * g.T2 * g.F2;
-  g.M2p = round_up(std::max<long>(g.M2, 1), g.kg);
+  g.M2p = round_up(std::max<long>(g.M2, 1), g.kg) + 16L * g.kg;
   return g;
 }
 
@@ -497,8 +656,8 @@ Tape tape_layout(const cfm_encoder* h, const Geo& g) {
 // split-K factor of a weight-gradient GEMM (N x K outputs, reduction over `rows`)
 int wgrad_splits(int N, int K, long rows) {
   const long tiles = (long)((N + 63) / 64) * ((K + 127) / 128);
-  long s = (1024 + tiles - 1) / tiles;
-  s = std::min<long>(s, std::max<long>(1, rows / 512));
+  long s = (768 + tiles - 1) / tiles;
+  s = std::min<long>(s, std::max<long>(1, rows / 256));
   return (int)std::max<long>(1, std::min<long>(s, 16));
 }
 
@@ -554,14 +713,14 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.pa = a.take(M * kp(Kmax) * es);                                   // dgrad A operand [M][N]
   const long NT = std::max({dff, 3 * d, 2 * d, (long)g.C});
   w.pat = a.take(std::max(NT * g.Mq, (long)g.C * g.M2p) * es);       // dy^T [N][Mp]
-  const long KT = np(std::max({dff, d, (long)g.F2 * g.C}));
+  const long KT = np(std::max({dff, d, (long)g.F2 * g.C}) + 4);
   w.pbt = a.take(KT * g.Mq * es);                                      // x^T [Kpad][Mp]
   w.wt = a.take(std::max({np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(3 * d), np(d) * kp(2 * d),
                           np((long)g.F2 * g.C) * kp(d), np(9L * g.C) * kp(g.C)}) * es);
   long part = 0;
   auto upd = [&](long N, long K, long rows) { part = std::max(part, (long)wgrad_splits((int)N, (int)K, rows) * N * K); };
-  upd(dff, d, M); upd(d, dff, M); upd(3 * d, d, M); upd(d, d, M); upd(2 * d, d, M); upd(d, d, g.NP);
-  upd(d, (long)g.F2 * g.C, M); upd(g.C, 9L * g.C, g.M2);
+  upd(dff, d + 4, M); upd(d, dff + 4, M); upd(3 * d, d + 4, M); upd(d, d + 4, M); upd(2 * d, d + 4, M);
+  upd(d, d, g.NP); upd(d, (long)g.F2 * g.C + 4, M); upd(g.C, 9L * g.C + 4, g.M2);
   w.part = a.take(part * 4);
   w.dqkv = a.take(M * 3 * d * 4);
   w.dctx = a.take(M * d * 4);
@@ -569,17 +728,17 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.dpre = a.take(M * 2 * d * 4);
   w.dG = a.take(M * d * 4);
   w.dD = a.take(M * d * 4);
-  const long red_rows = std::max({(long)M, g.M2, (long)g.B * g.T1, 64L});
+  const long red_rows = std::max({(long)M, g.M2, (long)g.B * g.T1 * g.F1, 64L});
   w.red = a.take(std::max({(long)colred_ws(red_rows, std::max(dff, 3 * d)), (long)colred_ws(16, 9L * g.C * g.C),
                            (long)cfm_op_dwconv_backward_ws_size(g.B, g.Tp, (int)d, g.K),
                            (long)colred_ws(g.B * g.T1, 9L * g.C)}) + 1024);
   w.dX2 = a.take(M * (long)g.F2 * g.C * 4);
   w.dcol = a.take(g.M2 * 9L * g.C * es);
-  w.i2c = a.take(np(9L * g.C) * g.M2p * es);
+  w.i2c = a.take(np(9L * g.C + 4) * g.M2p * es);
   w.dy1 = a.take((long)g.B * g.T1 * g.F1 * g.C * 4);
   const long c1ch = ((long)g.B * g.T1 + 7) / 8;
-  w.c1part = a.take(c1ch * 9L * g.C * 4 + 4096);
-  w.gtmp = a.take(std::max({d * (long)g.F2 * g.C, 9L * g.C * g.C, 3 * d * d}) * 4);
+  w.c1part = a.take(c1ch * 10L * g.C * 4 + 4096);
+  w.gtmp = a.take(std::max({d * (long)g.F2 * g.C, 9L * g.C * g.C, 3 * d * d + 3 * d}) * 4);
   w.attws = a.take((long)rel_pos_attention_backward_ws(g.B, g.Tp, g.H, g.dk) + 256);
   w.total = round_up(a.off, 256);
   return w;
@@ -618,18 +777,18 @@ struct Step {
   Drop drop(int site) const { return make_drop(o->dropout, o->seed, site); }
 
   void pack(const void* src, bool src_ct, long ld, int rows, int cols, bool tr, float scale, void* dst, long dld,
-            int rp, int cp, int fn = 0, Drop dr = Drop{0, 0, 1.0f}) const {
+            int rp, int cp, int fn = 0, Drop dr = Drop{0, 0, 1.0f}, int ones_row = -1) const {
     if (rp <= 0 || cp <= 0) return;
     const dim3 grid((cp + 31) / 32, (rp + 31) / 32), block(256);
     if (g.dt == DT_F32) {
       cfm_launch(tpack_kernel<float, float>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale, fn,
-                 dr, (float*)dst, dld, rp, cp);
+                 dr, (float*)dst, dld, rp, cp, ones_row);
     } else if (src_ct) {
       cfm_launch(tpack_kernel<bf16_t, bf16_t>, grid, block, 0, st, (const bf16_t*)src, ld, rows, cols, (int)tr, scale,
-                 fn, dr, (bf16_t*)dst, dld, rp, cp);
+                 fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row);
     } else {
       cfm_launch(tpack_kernel<float, bf16_t>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
-                 fn, dr, (bf16_t*)dst, dld, rp, cp);
+                 fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row);
     }
   }
   // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
@@ -677,37 +836,29 @@ struct Step {
     e.ldx = ldx;
     gemm(g.dt, A, lda, M, K, Wp, kpad(K), N, e, h->zero_page, st);
   }
-  // out (N, K) fp32 (ld ldo) = At[N][Mp] . Bt[K][Mp]^T over `rows` (split-K + fixed-order reduction)
-  void wgrad(const void* At, const void* Bt, long ldm, int N, int K, long rows, float* out, long ldo) const {
-    const int S = wgrad_splits(N, K, rows);
-    float* part = W_<float>(wl.part);
-    if (S == 1) {
-      GemmEpi e = epi(EPI_SCALE_F32, nullptr);
+  // out (N, K) fp32 = At[N][ldm] . Bt[K][ldm]^T over `rows` (one split-K launch + a fixed-order slab
+  // sum; the operand rows carry >= 16 zero granules past `rows`).  With `bias`, Bt has K + 4 rows whose
+  // row K is all ones (tpack ones_row), so column K of the product is the bias gradient sum_m dy[m][n].
+  void wgrad(const void* At, const void* Bt, long ldm, int N, int K, long rows, float* out, float* bias) const {
+    const int Kb = bias ? K + 4 : K;
+    const int S = wgrad_splits(N, Kb, rows);
+    const int chunk = (int)round_up((rows + S - 1) / S, g.kg);
+    GemmEpi e = epi(EPI_SCALE_F32, nullptr);
+    e.ldx = Kb;
+    if (S == 1 && !bias) {
       e.X = out;
-      e.ldx = ldo;
       gemm_ldw(g.dt, At, ldm, N, (int)rows, Bt, ldm, K, e, h->zero_page, st);
       return;
     }
-    const long chunk = round_up((rows + S - 1) / S, g.kg);
-    int used = 0;
-    for (int s = 0; s < S; ++s) {
-      const long k0 = (long)s * chunk;
-      const long kk = std::min(chunk, rows - k0);
-      if (kk <= 0) break;
-      GemmEpi e = epi(EPI_SCALE_F32, nullptr);
-      e.X = part + (long)s * N * K;
-      e.ldx = K;
-      gemm_ldw(g.dt, (const char*)At + k0 * g.es, ldm, N, (int)kk, (const char*)Bt + k0 * g.es, ldm, K, e,
-               h->zero_page, st);
-      ++used;
-    }
-    float* red = W_<float>(wl.red);
-    if (ldo == K) {
-      colred(part, nullptr, nullptr, (long)N * K, used, N * K, 0, 1.0f, out, 0, red, st);
-    } else {
-      for (int n = 0; n < N; ++n)   // (not used on the current paths: every gradient is dense)
-        colred(part + (long)n * K, nullptr, nullptr, (long)N * K, used, K, 0, 1.0f, out + (long)n * ldo, 0, red, st);
-    }
+    float* part = W_<float>(wl.part);
+    e.X = part;
+    if (S == 1) gemm_ldw(g.dt, At, ldm, N, (int)rows, Bt, ldm, Kb, e, h->zero_page, st);
+    else gemm_splitk(g.dt, At, ldm, N, (int)rows, Bt, ldm, Kb, S, chunk, e, (long)N * Kb, h->zero_page, st);
+    const long n = (long)N * Kb;
+    if (bias)
+      cfm_launch(slab_sum_wb_kernel, dim3(ew_grid(n)), dim3(256), 0, st, (const float*)part, S, N, K, out, bias);
+    else
+      cfm_launch(slab_sum_kernel, dim3(ew_grid(n / 4 + 1)), dim3(256), 0, st, (const float*)part, S, n, out);
   }
   void sync(float* buf, long n) const {
     if (o->world > 1 && o->allreduce) {
@@ -954,32 +1105,36 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   void* wt = S.W_(S.wl.wt);
   const long Mq = g.Mq;
   auto Gp = [&](int i) -> float* { return G ? G[i] : nullptr; };
-  // column sums of an fp32 (rows, n) gradient into a parameter gradient (if requested)
-  auto bias_grad = [&](const float* src, long ld, int rows, int n, int gi, float alpha = 1.0f) {
-    if (Gp(gi)) colred(src, nullptr, nullptr, ld, rows, n, 0, alpha, Gp(gi), 0, red, st);
-  };
   // Linear y = x W^T + b backward for a dense fp32 output gradient dy (M, N):
   //   dx (M, K) fp32 (ldx; accumulate or overwrite), dW (N, K) -> G[gw], db -> G[gb]
   //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
   auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
                         float* dx, long ldx, bool acc, int gw, int gb) {
-    if (gb >= 0) bias_grad(dy, N, M, N, gb);
     S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
     if (dx) {
       S.packWt(w, N, K, wt);
       S.gemm_f32out(pa, S.kpad(N), M, N, wt, K, nullptr, 1.0f, dx, ldx, acc);
     }
-    if (gw >= 0 && Gp(gw)) {
+    const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
+    if (want_w || want_b) {   // [dW | db] = dy^T . [x | 1]
       S.pack(dy, false, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
-      S.pack(xin, true, ldxin, M, K, true, 1.0f, pbt, Mq, S.npad(K), (int)Mq, xfn, xdr);
-      S.wgrad(pat, pbt, Mq, N, K, M, Gp(gw), K);
+      S.pack(xin, true, ldxin, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, xfn, xdr, want_b ? K : -1);
+      S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(gw) : nullptr, want_b ? Gp(gb) : nullptr);
     }
   };
   auto ln_bwd = [&](const float* x, int wi, int bi, const float* dy, float* dx, bool acc) {
-    // dx (+)= LN backward; prod (dy * xhat) reuses dbr
-    layernorm_backward(x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, dbr, st);
-    if (Gp(wi)) colred(dbr, nullptr, nullptr, d, M, d, 0, 1.0f, Gp(wi), 0, red, st);
-    bias_grad(dy, d, M, d, bi);
+    // dx (+)= LN backward; per-block column partials of dy*xhat and dy (in dbr), then folded
+    const int nblk = (M + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave);
+    float* pw = dbr;
+    float* pb = dbr + (long)nblk * d;
+    const int E4 = (d / 4 + 63) / 64;
+    const dim3 grid(nblk), blk(256);
+    if (E4 <= 1) cfm_launch(ln_bwd_fused_kernel<1>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
+    else if (E4 <= 2) cfm_launch(ln_bwd_fused_kernel<2>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
+    else if (E4 <= 4) cfm_launch(ln_bwd_fused_kernel<4>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
+    else cfm_launch(ln_bwd_fused_kernel<8>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
+    if (Gp(wi)) cfm_launch(colred_final_kernel, dim3((d + 15) / 16), blk, 0, st, (const float*)pw, nblk, d, 1.0f, Gp(wi), 0);
+    if (Gp(bi)) cfm_launch(colred_final_kernel, dim3((d + 15) / 16), blk, 0, st, (const float*)pb, nblk, d, 1.0f, Gp(bi), 0);
   };
 
   // dy (B, d, T') -> gA (B*T', d)
@@ -1069,12 +1224,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
         S.pack(dP, false, d, g.NP, d, true, 1.0f, pat, Mq, d, (int)Mq);
         S.pack(pe_slice, true, d, g.NP, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
-        S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), d);
+        S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), nullptr);
       }
       // q/k/v: biases, input gradient through [Wq; Wk; Wv], stacked weight gradient
-      bias_grad(dqkv, 3L * d, M, d, q.q_b);
-      bias_grad(dqkv + d, 3L * d, M, d, q.k_b);
-      bias_grad(dqkv + 2 * d, 3L * d, M, d, q.v_b);
       S.pack(dqkv, false, 3L * d, M, 3 * d, false, 1.0f, pa, S.kpad(3L * d), M, S.kpad(3L * d));
       {
         const long ldw = S.kpad(3L * d);
@@ -1084,14 +1236,19 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
                  p == 2 ? (int)(ldw - 2L * d) : d);
         float* dhn = dctx;   // dctx consumed
         S.gemm_f32out(pa, S.kpad(3L * d), M, 3 * d, wt, d, nullptr, 1.0f, dhn, d, false);
-        if (Gp(q.q_w) || Gp(q.k_w) || Gp(q.v_w)) {
+        const int bi3[3] = {q.q_b, q.k_b, q.v_b};
+        if (Gp(q.q_w) || Gp(q.k_w) || Gp(q.v_w) || Gp(q.q_b) || Gp(q.k_b) || Gp(q.v_b)) {
           S.pack(dqkv, false, 3L * d, M, 3 * d, true, 1.0f, pat, Mq, 3 * d, (int)Mq);
-          S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
-          float* tmp = S.W_<float>(S.wl.gtmp);   // (3d, d) stacked gradient
-          S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, d);
-          for (int p = 0; p < 3; ++p)
+          S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, d);
+          float* tmp = S.W_<float>(S.wl.gtmp);   // (3d, d) stacked weight gradient, then the (3d) biases
+          S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, tmp + 3L * d * d);
+          for (int p = 0; p < 3; ++p) {
             if (Gp(wi[p]))
               HIP_OK(hipMemcpyAsync(Gp(wi[p]), tmp + (long)p * d * d, (size_t)d * d * 4, hipMemcpyDeviceToDevice, st));
+            if (Gp(bi3[p]))
+              HIP_OK(hipMemcpyAsync(Gp(bi3[p]), tmp + 3L * d * d + (long)p * d, (size_t)d * 4, hipMemcpyDeviceToDevice,
+                                    st));
+          }
         }
         ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true);   // gB = d x1
       }
@@ -1105,16 +1262,15 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gA, xs, n_md, S.drop(0), dbr);
   const int KS = g.F2 * g.C;
   float* dX2 = S.W_<float>(S.wl.dX2);
-  bias_grad(dbr, d, M, d, S.i_sb);
   S.pack(dbr, false, d, M, d, false, 1.0f, pa, S.kpad(d), M, S.kpad(d));
   S.perm(S.prm(S.i_sw), 1, wt, false, S.kpad(d), S.npad(KS), S.kpad(d));
   S.gemm_f32out(pa, S.kpad(d), M, d, wt, KS, nullptr, 1.0f, dX2, KS, false);
-  if (Gp(S.i_sw)) {
+  if (Gp(S.i_sw) || Gp(S.i_sb)) {
     S.pack(dbr, false, d, M, d, true, 1.0f, pat, Mq, d, (int)Mq);
-    S.pack(S.T_(S.tp.X2), true, KS, M, KS, true, 1.0f, pbt, Mq, S.npad(KS), (int)Mq);
+    S.pack(S.T_(S.tp.X2), true, KS, M, KS, true, 1.0f, pbt, Mq, S.npad(KS + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, KS);
     float* tmp = S.W_<float>(S.wl.gtmp);   // (d, KS) permuted gradient
-    S.wgrad(pat, pbt, Mq, d, KS, M, tmp, KS);
-    S.perm(tmp, 4, Gp(S.i_sw), true, KS, d, KS);
+    S.wgrad(pat, pbt, Mq, d, KS, M, tmp, Gp(S.i_sb));
+    if (Gp(S.i_sw)) S.perm(tmp, 4, Gp(S.i_sw), true, KS, d, KS);
   }
   // conv2 + ReLU: dY2 = dX2 * [X2 > 0], rows (b, t2, f2) x C
   const long n2 = g.M2 * g.C;
@@ -1122,20 +1278,19 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     cfm_launch(relu_mask_kernel<float>, dim3(ew_grid(n2)), dim3(256), 0, st, dX2, S.T_<const float>(S.tp.X2), n2);
   else
     cfm_launch(relu_mask_kernel<bf16_t>, dim3(ew_grid(n2)), dim3(256), 0, st, dX2, S.T_<const bf16_t>(S.tp.X2), n2);
-  bias_grad(dX2, g.C, (int)g.M2, g.C, S.i_c2b);
   const bool need_c1 = Gp(S.i_c1w) || Gp(S.i_c1b);
-  if (Gp(S.i_c2w)) {   // dW2 = dY2^T . im2col(X1)
+  if (Gp(S.i_c2w) || Gp(S.i_c2b)) {   // [dW2 | db2] = dY2^T . [im2col(X1) | 1]
     S.pack(dX2, false, g.C, (int)g.M2, g.C, true, 1.0f, pat, g.M2p, g.C, (int)g.M2p);
-    const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C) + 31) / 32));
+    const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C + 4) + 31) / 32));
     if (dt == DT_F32)
       cfm_launch(im2col_t_kernel<float>, grid, dim3(256), 0, st, S.T_<const float>(S.tp.X1), g.T1, g.F1, g.T2, g.F2,
-                 g.C, (int)g.M2, S.W_<float>(S.wl.i2c), g.M2p, S.npad(9L * g.C));
+                 g.C, (int)g.M2, S.W_<float>(S.wl.i2c), g.M2p, S.npad(9L * g.C + 4));
     else
       cfm_launch(im2col_t_kernel<bf16_t>, grid, dim3(256), 0, st, S.T_<const bf16_t>(S.tp.X1), g.T1, g.F1, g.T2, g.F2,
-                 g.C, (int)g.M2, S.W_<bf16_t>(S.wl.i2c), g.M2p, S.npad(9L * g.C));
+                 g.C, (int)g.M2, S.W_<bf16_t>(S.wl.i2c), g.M2p, S.npad(9L * g.C + 4));
     float* tmp = S.W_<float>(S.wl.gtmp);   // (C, 9C) permuted gradient
-    S.wgrad(pat, S.W_(S.wl.i2c), g.M2p, g.C, 9 * g.C, g.M2, tmp, 9L * g.C);
-    S.perm(tmp, 5, Gp(S.i_c2w), true, 9L * g.C, g.C, 9 * g.C);
+    S.wgrad(pat, S.W_(S.wl.i2c), g.M2p, g.C, 9 * g.C, g.M2, tmp, Gp(S.i_c2b));
+    if (Gp(S.i_c2w)) S.perm(tmp, 5, Gp(S.i_c2w), true, 9L * g.C, g.C, 9 * g.C);
   }
   if (need_c1) {   // dCol = dY2 . W2mat, col2im + conv1 ReLU mask, then conv1's weight/bias gradient
     S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
@@ -1152,13 +1307,14 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     else
       cfm_launch(col2im_relu_kernel<bf16_t>, dim3(ew_grid(n1)), dim3(256), 0, st, S.W_<const bf16_t>(S.wl.dcol),
                  S.T_<const bf16_t>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
-    bias_grad(dy1, g.C, g.B * g.T1 * g.F1, g.C, S.i_c1b);
-    if (Gp(S.i_c1w)) {
+    {
       const int rows = g.B * g.T1, R = 8, nch = (rows + R - 1) / R;
       float* part = S.W_<float>(S.wl.c1part);
-      cfm_launch(conv1_wgrad_kernel, dim3(nch, (g.C + 255) / 256), dim3(256), 0, st, S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1,
-                 g.C, (const float*)dy1, g.B, R, part);
-      colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
+      float* part_b = part + (long)nch * 9 * g.C;
+      cfm_launch(conv1_wgrad_kernel, dim3(nch, (g.C + 255) / 256), dim3(256), 0, st, S.T_<const float>(S.tp.xin), g.F,
+                 g.T, g.T1, g.F1, g.C, (const float*)dy1, g.B, R, part, part_b);
+      if (Gp(S.i_c1w)) colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
+      if (Gp(S.i_c1b)) colred(part_b, nullptr, nullptr, g.C, nch, g.C, 0, 1.0f, Gp(S.i_c1b), 0, red, st);
     }
   }
 }
