@@ -1,4 +1,5 @@
-"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h and cfm_train.h).
+"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h and
+cfm_joint.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -32,6 +33,11 @@ TRAIN_SYMBOLS = (
     "cfm_op_dwconv_backward", "cfm_op_batchnorm_train_ws_size", "cfm_op_batchnorm_train_forward",
     "cfm_op_batchnorm_train_backward", "cfm_op_rel_attention_backward_ws_size", "cfm_op_rel_attention_backward",
     "cfm_train_tape_size", "cfm_train_workspace_size", "cfm_train_forward", "cfm_train_backward",
+)
+# every symbol include/cfm_joint.h declares
+JOINT_SYMBOLS = (
+    "cfm_rnnt_joint_create", "cfm_rnnt_joint_destroy", "cfm_rnnt_joint_set_weights", "cfm_rnnt_joint_workspace_size",
+    "cfm_rnnt_joint_forward",
 )
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
@@ -108,6 +114,11 @@ def load() -> ctypes.CDLL:
         "cfm_op_rel_attention_backward_ws_size": (sz, [ci, ci, ci, ci, ci]),
         "cfm_op_rel_attention_backward": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp, vp,
                                                vp, vp, vp, vp, sz, vp]),
+        "cfm_rnnt_joint_create": (ci, [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(vp)]),
+        "cfm_rnnt_joint_destroy": (None, [vp]),
+        "cfm_rnnt_joint_set_weights": (ci, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "cfm_rnnt_joint_workspace_size": (sz, [vp, ci, ci, ci]),
+        "cfm_rnnt_joint_forward": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, sz, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -67,6 +67,7 @@ struct GemmEpi {
   int qk_cols;         // EPI_QKV: columns < qk_cols (= 2*H*dkp) are q and k, the rest are V
   const float* uv;     // EPI_QKV: pos_bias_u then pos_bias_v, each [H][dkp] zero-padded
   float qscale;        // EPI_QKV: (q + u), (q + v) are written pre-multiplied by log2(e) / sqrt(dk)
+  int out_scalar;      // EPI_SCALE_F32: element stores (fp32 rows whose stride is not a multiple of 4)
 };
 
 struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)

@@ -206,7 +206,17 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       } else {
         o.x = a.x * e.alpha; o.y = a.y * e.alpha; o.z = a.z * e.alpha; o.w = a.w * e.alpha;
       }
-      if (colok && m < p.M) *(float4*)(e.X + xoff + (long)m * e.ldx + n) = o;
+      if (e.out_scalar) {   // unaligned rows (ldx % 4 != 0): element stores, tail-masked
+        float* xr = e.X + xoff + (long)m * e.ldx + n;
+        if (m < p.M) {
+          if (n < p.N) xr[0] = o.x;
+          if (n + 1 < p.N) xr[1] = o.y;
+          if (n + 2 < p.N) xr[2] = o.z;
+          if (n + 3 < p.N) xr[3] = o.w;
+        }
+      } else if (colok && m < p.M) {
+        *(float4*)(e.X + xoff + (long)m * e.ldx + n) = o;
+      }
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
     // packed columns: per 64-column group g, [0,32) = value channels 32g.., [32,64) = gates

@@ -1,0 +1,266 @@
+// RNN-T joint network forward (RNNTJoint.joint, rnnt.py:951-1008), SURVEY §8 row a-ext4.
+//
+//   f' = enc(f) (B*T, H),  g' = pred(g) (B*U, H)            two small GEMMs, fp32 out
+//   Hj[(b,t,u)] = act(f'[b,t] + g'[b,u])                   broadcast-add + activation, compute type
+//   out[(b,t,u)] = Hj . W_out^T + b_out                     the big GEMM (B*T*U x C x H), fp32 out
+//   optional log_softmax over C, one wave per row, in place
+// The hidden tensor is materialised in the compute type (HBM-bound pass, ~1/3 of the GEMM's own
+// output bytes) so the big contraction runs on the tuned LDS-DMA MFMA GEMM; its fp32 output rows
+// are C = V + 1 wide (odd), written with the epilogue's element stores.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "../../include/cfm_joint.h"
+#include "cfm_abi.h"
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+using namespace cfm;
+
+struct cfm_rnnt_joint {
+  int H1, H2, H, C, act, device, dtype, es, kg;
+  char* wbuf = nullptr;
+  long w_enc, b_enc, w_pred, b_pred, w_out, b_out, total;
+  void* zero = nullptr;
+  bool weights_set = false;
+  long kp(long k) const { return round_up(k, kg); }
+  long np(long n) const { return round_up(n, GEMM_BN); }
+};
+
+namespace {
+
+// (B, D, L) fp32 -> rows (b, l) of D values in the compute type, ld = Dp (zero-padded)
+template <typename T>
+__global__ __launch_bounds__(256) void bdl_to_rows_kernel(const float* __restrict__ src, int D, int L,
+                                                          T* __restrict__ dst, int Dp) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, l0 = blockIdx.x * 32, d0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int d = d0 + k, l = l0 + tx;
+    tile[k][tx] = (d < D && l < L) ? src[((long)b * D + d) * L + l] : 0.0f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int l = l0 + k, d = d0 + tx;
+    if (l < L && d < Dp) st_f<T>(dst + ((long)b * L + l) * Dp + d, tile[tx][k]);
+  }
+}
+
+// Hj[(b,t,u)][h] = act(f[b*T+t][h] + g[b*U+u][h]); 8 h per thread (16-byte bf16 / 2x16-byte fp32 stores)
+template <typename TO>
+__global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restrict__ f, const float* __restrict__ g,
+                                                           int B, int T, int U, int H, int Hp, int act,
+                                                           TO* __restrict__ out) {
+  const int HG = Hp / 8;
+  const long n = (long)B * T * U * HG;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int hg = (int)(i % HG);
+    const long row = i / HG;
+    const int u = (int)(row % U);
+    const long bt = row / U;
+    const int b = (int)(bt / T);
+    const float* fr = f + bt * H;
+    const float* gr = g + ((long)b * U + u) * H;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int h = hg * 8 + j;
+      float x = h < H ? fr[h] + gr[h] : 0.0f;
+      if (act == CFM_JOINT_RELU) x = fmaxf(x, 0.0f);
+      else if (act == CFM_JOINT_SIGMOID) x = 1.0f / (1.0f + expf(-x));
+      else x = tanhf(x);
+      v[j] = h < H ? x : 0.0f;
+    }
+    TO* o = out + row * Hp + hg * 8;
+    if constexpr (sizeof(TO) == 2) {
+      *(uint4*)o = Vec16<bf16_t>::from_f32(v);
+    } else {
+      *(uint4*)o = Vec16<float>::from_f32(v);
+      *(uint4*)(o + 4) = Vec16<float>::from_f32(v + 4);
+    }
+  }
+}
+
+// in-place log_softmax over rows of C fp32 values, one wave per row
+__global__ __launch_bounds__(256) void row_log_softmax_kernel(float* __restrict__ x, long rows, int C) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float* r = x + row * C;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, r[c]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  float s = 0.0f;
+  for (int c = lane; c < C; c += 64) s += expf(r[c] - m);
+  s = wave_sum(s);
+  const float lse = m + logf(s);
+  for (int c = lane; c < C; c += 64) r[c] -= lse;
+}
+
+unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 16384)); }
+
+struct JWs { long af, ag, fp, gp, hid, total; };
+JWs jws(const cfm_rnnt_joint* h, int B, int T, int U) {
+  JWs w;
+  long off = 0;
+  auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(std::max(bytes, 1L), 256); return o; };
+  const long Hp = round_up(h->H, std::max(8, h->kg));
+  w.af = take((long)B * T * h->kp(h->H1) * h->es);
+  w.ag = take((long)B * U * h->kp(h->H2) * h->es);
+  w.fp = take((long)B * T * h->H * 4);
+  w.gp = take((long)B * U * h->H * 4);
+  w.hid = take((long)B * T * U * Hp * h->es);
+  w.total = round_up(off, 256);
+  return w;
+}
+
+GemmEpi epi_f32(const float* bias, float* X, long ldx, int scalar) {
+  GemmEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = EPI_SCALE_F32;
+  e.bias = bias;
+  e.alpha = 1.0f;
+  e.X = X;
+  e.ldx = ldx;
+  e.out_scalar = scalar;
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+cfm_status cfm_rnnt_joint_create(int encoder_hidden, int pred_hidden, int joint_hidden, int num_classes,
+                                 int activation, int device, int compute_mode, cfm_rnnt_joint** out) {
+  return guarded([&] {
+    if (!out) fail(CFM_ERR_INVALID_ARG, "null output");
+    *out = nullptr;
+    if (encoder_hidden <= 0 || pred_hidden <= 0 || joint_hidden <= 0 || num_classes <= 0)
+      fail(CFM_ERR_INVALID_ARG, "sizes must be positive");
+    if (activation < 0 || activation > 2) fail(CFM_ERR_INVALID_ARG, "activation must be relu, sigmoid or tanh");
+    if (compute_mode != CFM_COMPUTE_FP32 && compute_mode != CFM_COMPUTE_BF16) fail(CFM_ERR_INVALID_ARG, "compute mode");
+    if (encoder_hidden % 4 || pred_hidden % 4) fail(CFM_ERR_UNSUPPORTED, "encoder/pred hidden must be multiples of 4");
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) fail(CFM_ERR_INVALID_ARG, "bad device");
+    HIP_OK(hipSetDevice(device));
+    auto* h = new cfm_rnnt_joint();
+    h->H1 = encoder_hidden; h->H2 = pred_hidden; h->H = joint_hidden; h->C = num_classes; h->act = activation;
+    h->device = device;
+    h->dtype = compute_mode == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16;
+    h->es = dtype_size(h->dtype);
+    h->kg = GEMM_BK_BYTES / h->es;
+    long off = 0;
+    auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(bytes, 256); return o; };
+    const long Hk = h->kp(h->H);
+    h->w_enc = take(h->np(h->H) * h->kp(h->H1) * h->es);
+    h->b_enc = take(h->np(h->H) * 4);
+    h->w_pred = take(h->np(h->H) * h->kp(h->H2) * h->es);
+    h->b_pred = take(h->np(h->H) * 4);
+    h->w_out = take(h->np(h->C) * Hk * h->es);
+    h->b_out = take(h->np(h->C) * 4);
+    h->total = off;
+    if (hipMalloc(&h->wbuf, (size_t)off) != hipSuccess || hipMalloc(&h->zero, 4096) != hipSuccess) {
+      if (h->wbuf) (void)hipFree(h->wbuf);
+      delete h;
+      fail(CFM_ERR_NOMEM, "joint weight allocation failed");
+    }
+    HIP_OK(hipMemset(h->zero, 0, 4096));
+    HIP_OK(hipMemset(h->wbuf, 0, (size_t)off));
+    *out = h;
+  });
+}
+
+void cfm_rnnt_joint_destroy(cfm_rnnt_joint* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->wbuf) (void)hipFree(h->wbuf);
+  if (h->zero) (void)hipFree(h->zero);
+  delete h;
+}
+
+cfm_status cfm_rnnt_joint_set_weights(cfm_rnnt_joint* h, const float* w_enc, const float* b_enc, const float* w_pred,
+                                      const float* b_pred, const float* w_out, const float* b_out, void* stream) {
+  return guarded([&] {
+    if (!h || !w_enc || !w_pred || !w_out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    auto packw = [&](const float* w, int N, int K, long off) {
+      pack_matrix(h->dtype, w, K, N, K, false, h->wbuf + off, h->kp(K), (int)h->np(N), (int)h->kp(K), st);
+    };
+    auto packb = [&](const float* b, int N, long off) {
+      HIP_OK(hipMemsetAsync(h->wbuf + off, 0, (size_t)h->np(N) * 4, st));
+      if (b) HIP_OK(hipMemcpyAsync(h->wbuf + off, b, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    };
+    packw(w_enc, h->H, h->H1, h->w_enc);
+    packb(b_enc, h->H, h->b_enc);
+    packw(w_pred, h->H, h->H2, h->w_pred);
+    packb(b_pred, h->H, h->b_pred);
+    packw(w_out, h->C, h->H, h->w_out);
+    packb(b_out, h->C, h->b_out);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(st));   // the sources may be temporaries
+    h->weights_set = true;
+  });
+}
+
+size_t cfm_rnnt_joint_workspace_size(const cfm_rnnt_joint* h, int B, int T, int U) {
+  if (!h || B <= 0 || T <= 0 || U <= 0) return 0;
+  return (size_t)jws(h, B, T, U).total;
+}
+
+cfm_status cfm_rnnt_joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T, int U,
+                                  int log_softmax, float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    if (!h || !enc_bdt || !dec_bdu || !out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+    if (B <= 0 || T <= 0 || U <= 0) fail(CFM_ERR_INVALID_ARG, "B, T and U must be positive");
+    const long rows = (long)B * T * U;
+    if (rows > 0x7fffffffL) fail(CFM_ERR_UNSUPPORTED, "B*T*U exceeds 2^31 rows");
+    const JWs w = jws(h, B, T, U);
+    if (!workspace || workspace_bytes < (size_t)w.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    const int dt = h->dtype;
+    const int H1p = (int)h->kp(h->H1), H2p = (int)h->kp(h->H2);
+    const int Hp = (int)round_up(h->H, std::max(8, h->kg));
+    // (B, D, L) -> rows
+    if (dt == DT_F32) {
+      cfm_launch(bdl_to_rows_kernel<float>, dim3((T + 31) / 32, (H1p + 31) / 32, B), dim3(256), 0, st, enc_bdt, h->H1,
+                 T, (float*)(ws + w.af), H1p);
+      cfm_launch(bdl_to_rows_kernel<float>, dim3((U + 31) / 32, (H2p + 31) / 32, B), dim3(256), 0, st, dec_bdu, h->H2,
+                 U, (float*)(ws + w.ag), H2p);
+    } else {
+      cfm_launch(bdl_to_rows_kernel<bf16_t>, dim3((T + 31) / 32, (H1p + 31) / 32, B), dim3(256), 0, st, enc_bdt,
+                 h->H1, T, (bf16_t*)(ws + w.af), H1p);
+      cfm_launch(bdl_to_rows_kernel<bf16_t>, dim3((U + 31) / 32, (H2p + 31) / 32, B), dim3(256), 0, st, dec_bdu,
+                 h->H2, U, (bf16_t*)(ws + w.ag), H2p);
+    }
+    float* fp = (float*)(ws + w.fp);
+    float* gp = (float*)(ws + w.gp);
+    const int sc = h->H % 4 ? 1 : 0;
+    gemm(dt, ws + w.af, H1p, B * T, h->H1, h->wbuf + h->w_enc, H1p, h->H,
+         epi_f32((const float*)(h->wbuf + h->b_enc), fp, h->H, sc), h->zero, st);
+    gemm(dt, ws + w.ag, H2p, B * U, h->H2, h->wbuf + h->w_pred, H2p, h->H,
+         epi_f32((const float*)(h->wbuf + h->b_pred), gp, h->H, sc), h->zero, st);
+    const long nh = rows * (Hp / 8);
+    if (dt == DT_F32)
+      cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
+                 T, U, h->H, Hp, h->act, (float*)(ws + w.hid));
+    else
+      cfm_launch(joint_hidden_kernel<bf16_t>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp,
+                 B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid));
+    gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), h->C,
+         epi_f32((const float*)(h->wbuf + h->b_out), out, h->C, h->C % 4 ? 1 : 0), h->zero, st);
+    if (log_softmax)
+      cfm_launch(row_log_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, out, rows, h->C);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

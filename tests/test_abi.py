@@ -32,7 +32,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(ctc) == set(_lib.CTC_SYMBOLS)
     train = _declared_symbols("cfm_train.h")
     assert set(train) == set(_lib.TRAIN_SYMBOLS)
-    for name in ctc + train:
+    joint = _declared_symbols("cfm_joint.h")
+    assert set(joint) == set(_lib.JOINT_SYMBOLS)
+    for name in ctc + train + joint:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 

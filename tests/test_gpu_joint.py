@@ -1,0 +1,64 @@
+"""GPU parity of the native RNN-T joint (include/cfm_joint.h) through the drop-in
+`nemo.collections.asr.modules.RNNTJoint` against the reference's outputs (tests/golden/joint_*.npz).
+Gates: fp32 compute rel-L2 <= 1e-5, bf16 operands rel-L2 <= 2e-2 (logits and log-probs)."""
+import ast
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_l2
+
+pytestmark = pytest.mark.gpu
+FILES = sorted(glob.glob(os.path.join(GOLDEN, "joint_*.npz")))
+GATE = {"fp32": 1e-5, "bf16": 2e-2}
+
+
+def _joint(z, compute):
+    from nemo.collections.asr.modules import RNNTJoint
+    jn = dict(ast.literal_eval(str(z["jointnet"])))
+    j = RNNTJoint(jointnet=jn, num_classes=int(z["num_classes"]))
+    j.load_state_dict({k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p__")})
+    j.set_compute_mode(compute)
+    return j.cuda().eval()
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f) for f in FILES])
+def test_joint_matches_reference(path, compute):
+    z = np.load(path)
+    j = _joint(z, compute)
+    enc = torch.from_numpy(z["enc"]).cuda()
+    dec = torch.from_numpy(z["dec"]).cuda()
+    with torch.no_grad():
+        j.log_softmax = None            # on a GPU: logits (rnnt.py:998-1002)
+        lo = j(encoder_outputs=enc, decoder_outputs=dec)
+        j.log_softmax = True
+        lp = j(encoder_outputs=enc, decoder_outputs=dec)
+        j.log_softmax = False
+        lo2 = j.joint(enc.transpose(1, 2), dec.transpose(1, 2))
+    torch.cuda.synchronize()
+    assert tuple(lo.shape) == z["logits"].shape
+    assert rel_l2(lo.cpu().numpy(), z["logits"]) <= GATE[compute]
+    assert rel_l2(lp.cpu().numpy(), z["logprobs"]) <= GATE[compute]
+    assert rel_l2(lo2.cpu().numpy(), z["logits"]) <= GATE[compute]
+
+
+def test_joint_large_shape_properties():
+    """cfg-4-like shape (odd class count, B*T*U rows not a tile multiple): finite, log-probs normalised,
+    and every (b, t, u) row independent of its neighbours (one utterance re-run alone is identical)."""
+    from nemo.collections.asr.modules import RNNTJoint
+    torch.manual_seed(0)
+    j = RNNTJoint(jointnet=dict(encoder_hidden=512, pred_hidden=640, joint_hidden=640, activation="relu"),
+                  num_classes=1024, log_softmax=True).cuda().eval()
+    enc = torch.randn(3, 512, 37, device="cuda")
+    dec = torch.randn(3, 640, 13, device="cuda")
+    with torch.no_grad():
+        lp = j(encoder_outputs=enc, decoder_outputs=dec)
+        one = j(encoder_outputs=enc[1:2].contiguous(), decoder_outputs=dec[1:2].contiguous())
+    assert lp.shape == (3, 37, 13, 1025) and torch.isfinite(lp).all()
+    s = torch.logsumexp(lp.double(), -1)
+    assert torch.allclose(s, torch.zeros_like(s), atol=1e-4)
+    assert torch.equal(lp[1:2], one)
