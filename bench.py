@@ -123,9 +123,11 @@ def main():
     ap.add_argument("--layers", type=int, default=17)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--mode", default="forward", choices=["forward", "train"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
-                         "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW)")
+                         "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
+                         "joint: config 4 (Large-17 encoder B=16 T=1600 + RNN-T joint U=100 V=1024); "
+                         "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks)")
     ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
     args = ap.parse_args()
 
@@ -147,6 +149,10 @@ def main():
 
     if args.mode == "train":
         return run_train(args, world, rank, dev, dist, barrier)
+    if args.mode == "joint":
+        return run_joint(args, world, rank, dev, dist, barrier)
+    if args.mode == "stream":
+        return run_stream(args, world, rank, dev, dist, barrier)
     from nemo.collections.asr.modules import ConformerEncoder
     torch.manual_seed(0)
     d, H, L, B, T = 512, 8, args.layers, args.batch, args.seq
@@ -314,6 +320,128 @@ def run_train(args, world, rank, dev, dist, barrier):
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
+
+
+def timed_loop(step, warmup, steps, barrier):
+    for _ in range(warmup):
+        r = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = step()
+    barrier()
+    return time.perf_counter() - t0, r
+
+
+def emit(rank, dist, out):
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+JOINT_METRIC = "encoder+joint audio-frames/sec, Conformer-Transducer-Large B=16 T=1600 U=100 V=1024 (BASELINE config 4)"
+
+
+def run_joint(args, world, rank, dev, dist, barrier):
+    """BASELINE config 4: Large-17 encoder forward (B=16, T=1600) + RNNTJoint forward over the
+    (B, T'=400, U+1=101) lattice with V=1024 (+blank), logits as on a GPU (rnnt.py:998-1002).
+    The prediction-network output is synthetic (B, 640, U+1): the decoder LSTM is not on this path."""
+    from nemo.collections.asr.modules import ConformerEncoder, RNNTJoint
+    torch.manual_seed(0)
+    d, H, L, B, T, U, V = 512, 8, args.layers, 16, 1600, 100, 1024
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
+    enc.set_compute_mode(args.compute)
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=d, pred_hidden=640, joint_hidden=640, activation="relu"),
+                      num_classes=V).to(dev).eval()
+    joint.set_compute_mode(args.compute)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, 80, T, device=dev, generator=g)
+    lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
+    pred = torch.randn(B, 640, U + 1, device=dev, generator=g)
+
+    def step():
+        y, yl = enc(audio_signal=x, length=lengths)
+        return joint(encoder_outputs=y, decoder_outputs=pred)
+
+    with torch.inference_mode():
+        elapsed, out = timed_loop(step, args.warmup, args.steps, barrier)
+        assert torch.isfinite(out[:1]).all().item()
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops
+    Tp = (((T - 1) // 2 + 1) - 1) // 2 + 1
+    f_enc = encoder_flops(B, T, d, L)
+    f_joint = 2 * B * Tp * d * 640 + 2 * B * (U + 1) * 640 * 640 + 2 * B * Tp * (U + 1) * 640 * (V + 1)
+    tot = f_enc + f_joint
+    emit(rank, dist, {
+        "metric": JOINT_METRIC, "value": round(job_throughput(t_max, world, B, T, args.steps), 1),
+        "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.compute, "data": "synthetic",
+        "config": {"workload": f"Conformer-Transducer-Large encoder ({L} layers) + RNNTJoint (640 hidden, relu), "
+                               f"B={B}/GPU, T={T}, U+1={U + 1}, V+1={V + 1}, logits fp32 "
+                               f"({B * Tp * (U + 1) * (V + 1) * 4 / 1e9:.2f} GB per step)",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (replicas, no collective)"},
+        "model_flops": {"GFLOP_per_step_per_gpu": round(tot / 1e9, 1), "encoder_GFLOP": round(f_enc / 1e9, 1),
+                        "joint_GFLOP": round(f_joint / 1e9, 1),
+                        "TFLOP/s_per_gpu": round(tot / (ms_step * 1e-3) / 1e12, 1),
+                        "frac_of_peak": round(tot / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
+
+
+STREAM_METRIC = ("streaming audio-frames/sec, Conformer-XLarge buffered (400-frame buffer, 160-frame chunk), "
+                 "B=64 streams (BASELINE config 5)")
+
+
+def run_stream(args, world, rank, dev, dist, barrier):
+    """BASELINE config 5: every step advances B=64 independent streams by one 1.6 s chunk (160 frames):
+    device-resident shift + per-feature normalisation of the 4 s buffers (cfm_frame_buffer_step,
+    BatchedFeatureFrameBufferer semantics, streaming_utils.py:686-818), then the stateless XL encoder
+    (d1024, 8 heads, 24 layers) over the whole 400-frame buffer, as FrameBatchASR does.  `value`
+    counts NEW audio frames (B x 160 per step): the stream's real-time throughput."""
+    from types import SimpleNamespace
+    from nemo.collections.asr.modules import ConformerEncoder
+    from nemo.collections.asr.parts.utils.streaming_utils import BatchedFeatureFrameBufferer
+    torch.manual_seed(0)
+    d, H, L, B, Tbuf, n = 1024, 8, 24, 64, 400, 160
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
+    enc.set_compute_mode(args.compute)
+    model = SimpleNamespace(_cfg=SimpleNamespace(sample_rate=16000, preprocessor=SimpleNamespace(
+        window_stride=0.01, features=80)), device=dev)
+    bb = BatchedFeatureFrameBufferer(model, frame_len=1.6, batch_size=B, total_buffer=4.0)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    chunks = torch.randn(8, B, 80, n, device=dev, generator=g) * 4.0 - 6.0   # synthetic log-mel chunks
+    buf = torch.empty(B, 80, Tbuf, device=dev)
+    lengths = torch.full((B,), Tbuf, dtype=torch.int64, device=dev)
+    it = [0]
+
+    def step():
+        bb.step(chunks[it[0] % 8], out=buf)
+        it[0] += 1
+        return enc(audio_signal=buf, length=lengths)
+
+    with torch.inference_mode():
+        elapsed, (y, yl) = timed_loop(step, args.warmup, args.steps, barrier)
+        assert torch.isfinite(y).all().item()
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops
+    fl = encoder_flops(B, Tbuf, d, L)
+    emit(rank, dist, {
+        "metric": STREAM_METRIC, "value": round(world * B * n * args.steps / t_max, 1), "unit": "audio-frames/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
+        "config": {"workload": f"Conformer-XLarge (d1024, 8 heads, {L} layers) buffered streaming: B={B} streams, "
+                               f"{Tbuf}-frame buffer, {n}-frame chunk, device-resident buffer normalisation",
+                   "global_batch": B * world, "seq_len": Tbuf, "parallelism": f"dp{world} (replicas, no collective)"},
+        "buffer_frames_per_s": round(world * B * Tbuf * args.steps / t_max, 1),
+        "model_flops": {"GFLOP_per_step_per_gpu": round(fl / 1e9, 1),
+                        "TFLOP/s_per_gpu": round(fl / (ms_step * 1e-3) / 1e12, 1),
+                        "frac_of_peak": round(fl / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
-"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h and
-cfm_joint.h).
+"""ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
+cfm_joint.h and cfm_stream.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -39,6 +39,8 @@ JOINT_SYMBOLS = (
     "cfm_rnnt_joint_create", "cfm_rnnt_joint_destroy", "cfm_rnnt_joint_set_weights", "cfm_rnnt_joint_workspace_size",
     "cfm_rnnt_joint_forward",
 )
+# every symbol include/cfm_stream.h declares
+STREAM_SYMBOLS = ("cfm_frame_buffer_step",)
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",
@@ -119,6 +121,7 @@ def load() -> ctypes.CDLL:
         "cfm_rnnt_joint_set_weights": (ci, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "cfm_rnnt_joint_workspace_size": (sz, [vp, ci, ci, ci]),
         "cfm_rnnt_joint_forward": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, sz, vp]),
+        "cfm_frame_buffer_step": (ci, [vp, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, vp, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -34,7 +34,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(train) == set(_lib.TRAIN_SYMBOLS)
     joint = _declared_symbols("cfm_joint.h")
     assert set(joint) == set(_lib.JOINT_SYMBOLS)
-    for name in ctc + train + joint:
+    stream = _declared_symbols("cfm_stream.h")
+    assert set(stream) == set(_lib.STREAM_SYMBOLS)
+    for name in ctc + train + joint + stream:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
