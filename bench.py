@@ -123,11 +123,12 @@ def main():
     ap.add_argument("--layers", type=int, default=17)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "mel"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
                          "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
                          "joint: config 4 (Large-17 encoder B=16 T=1600 + RNN-T joint U=100 V=1024); "
-                         "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks)")
+                         "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks); "
+                         "mel: the log-mel preprocessor in front of config 2 (SURVEY f1)")
     ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
     args = ap.parse_args()
 
@@ -153,6 +154,8 @@ def main():
         return run_joint(args, world, rank, dev, dist, barrier)
     if args.mode == "stream":
         return run_stream(args, world, rank, dev, dist, barrier)
+    if args.mode == "mel":
+        return run_mel(args, world, rank, dev, dist, barrier)
     from nemo.collections.asr.modules import ConformerEncoder
     torch.manual_seed(0)
     d, H, L, B, T = 512, 8, args.layers, args.batch, args.seq
@@ -441,6 +444,41 @@ def run_stream(args, world, rank, dev, dist, barrier):
         "model_flops": {"GFLOP_per_step_per_gpu": round(fl / 1e9, 1),
                         "TFLOP/s_per_gpu": round(fl / (ms_step * 1e-3) / 1e12, 1),
                         "frac_of_peak": round(fl / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
+
+
+MEL_METRIC = "preprocessor audio-frames/sec, AudioToMelSpectrogramPreprocessor (conformer_ctc_bpe.yaml) B=32 T=1000"
+
+
+def run_mel(args, world, rank, dev, dist, barrier):
+    """the conformer_ctc_bpe.yaml preprocessor (25 ms hann window, 10 ms hop, n_fft 512,
+    80 mels, per_feature normalisation, pad_to 0) over B=32 utterances of 159,840 samples (16 kHz,
+    1000 output frames each): raw samples in HBM -> normalised (B, 80, 1000) features, eval mode."""
+    from nemo.collections.asr.modules import AudioToMelSpectrogramPreprocessor
+    B, N = args.batch, 160 * (args.seq - 1)
+    p = AudioToMelSpectrogramPreprocessor(sample_rate=16000, normalize="per_feature", window_size=0.025,
+                                          window_stride=0.01, window="hann", features=80, n_fft=512, log=True,
+                                          frame_splicing=1, dither=0.00001, pad_to=0, pad_value=0.0).to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, N, device=dev, generator=g) * 0.1
+    L = torch.full((B,), N, dtype=torch.int64, device=dev)
+    with torch.inference_mode():
+        elapsed, (y, yl) = timed_loop(lambda: p(input_signal=x, length=L), args.warmup, args.steps, barrier)
+        assert torch.isfinite(y).all().item()
+    T = y.shape[-1]
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    algo = B * N * 4 + 2 * B * 80 * T * 4 * 2      # samples once; features written, re-read and re-written by the norm pass
+    ach = algo / (ms_step * 1e-3) / 1e9
+    emit(rank, dist, {
+        "metric": MEL_METRIC, "value": round(world * B * T * args.steps / t_max, 1), "unit": "audio-frames/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"AudioToMelSpectrogramPreprocessor 80-mel, n_fft 512, B={B}, {N} samples/utterance",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (replicas, no collective)"},
+        "roofline": {"kernel": "mel_frames_kernel + mel_norm_rows_kernel (whole step)", "bound": "hbm",
+                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": None, "per_launch": f"{algo / 1e6:.1f} MB algorithmic per step"},
     })
 
 

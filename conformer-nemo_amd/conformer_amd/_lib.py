@@ -1,5 +1,5 @@
 """ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
-cfm_joint.h and cfm_stream.h).
+cfm_joint.h, cfm_stream.h and cfm_mel.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -41,6 +41,9 @@ JOINT_SYMBOLS = (
 )
 # every symbol include/cfm_stream.h declares
 STREAM_SYMBOLS = ("cfm_frame_buffer_step",)
+# every symbol include/cfm_mel.h declares
+MEL_SYMBOLS = ("cfm_mel_create", "cfm_mel_destroy", "cfm_mel_set_tables", "cfm_mel_num_frames", "cfm_mel_output_frames",
+               "cfm_mel_forward", "cfm_normalize_batch", "cfm_mel_filterbank_slaney")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",
@@ -53,6 +56,15 @@ class CfmEncoderCfg(ctypes.Structure):
         "feat_in", "n_layers", "d_model", "feat_out", "subsampling_factor", "subsampling_conv_channels",
         "ff_expansion_factor", "n_heads", "att_context_left", "att_context_right", "xscaling", "pos_emb_max_len",
         "conv_kernel_size", "conv_norm_type")]
+
+
+class CfmMelCfg(ctypes.Structure):
+    _fields_ = [("n_window_size", ctypes.c_int), ("n_window_stride", ctypes.c_int), ("n_fft", ctypes.c_int),
+                ("nfilt", ctypes.c_int), ("exact_pad", ctypes.c_int), ("use_preemph", ctypes.c_int),
+                ("preemph", ctypes.c_float), ("mag_power", ctypes.c_float), ("log", ctypes.c_int),
+                ("log_zero_guard_type", ctypes.c_int), ("log_zero_guard_value", ctypes.c_float),
+                ("normalize", ctypes.c_int), ("pad_value", ctypes.c_float), ("pad_to", ctypes.c_int),
+                ("max_length", ctypes.c_int)]
 
 
 class CfmTensorView(ctypes.Structure):
@@ -122,6 +134,15 @@ def load() -> ctypes.CDLL:
         "cfm_rnnt_joint_workspace_size": (sz, [vp, ci, ci, ci]),
         "cfm_rnnt_joint_forward": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, sz, vp]),
         "cfm_frame_buffer_step": (ci, [vp, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, vp, vp]),
+        "cfm_mel_create": (ci, [ctypes.POINTER(CfmMelCfg), ci, ctypes.POINTER(vp)]),
+        "cfm_mel_destroy": (None, [vp]),
+        "cfm_mel_set_tables": (ci, [vp, vp, vp, vp]),
+        "cfm_mel_num_frames": (ctypes.c_long, [vp, ctypes.c_long]),
+        "cfm_mel_output_frames": (ctypes.c_long, [vp, ctypes.c_long]),
+        "cfm_mel_forward": (ci, [vp, vp, vp, ci, ctypes.c_long, ctypes.c_float, ctypes.c_uint64, vp, ci, vp, vp, vp]),
+        "cfm_normalize_batch": (ci, [vp, vp, ci, ci, ci, ci, vp, vp]),
+        "cfm_mel_filterbank_slaney": (ci, [ci, ci, ci, ctypes.c_double, ctypes.c_double, ci, ci,
+                                           ctypes.POINTER(ctypes.c_float)]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -40,3 +40,12 @@ class NeuralType:
 
     def __repr__(self):
         return f"NeuralType(axes={self.axes}, elements_type={self.elements_type!r}, optional={self.optional})"
+
+
+class AudioSignal(ElementType):
+    def __init__(self, freq=None):
+        self.freq = freq
+
+
+class MelSpectrogramType(SpectrogramType):
+    pass

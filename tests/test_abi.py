@@ -36,7 +36,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(joint) == set(_lib.JOINT_SYMBOLS)
     stream = _declared_symbols("cfm_stream.h")
     assert set(stream) == set(_lib.STREAM_SYMBOLS)
-    for name in ctc + train + joint + stream:
+    mel = _declared_symbols("cfm_mel.h")
+    assert set(mel) == set(_lib.MEL_SYMBOLS)
+    for name in ctc + train + joint + stream + mel:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
