@@ -1,5 +1,6 @@
 """ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
-cfm_joint.h, cfm_stream.h and cfm_mel.h).
+cfm_joint.h, cfm_stream.h, cfm_mel.h and
+cfm_rnnt_loss.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -44,6 +45,8 @@ STREAM_SYMBOLS = ("cfm_frame_buffer_step",)
 # every symbol include/cfm_mel.h declares
 MEL_SYMBOLS = ("cfm_mel_create", "cfm_mel_destroy", "cfm_mel_set_tables", "cfm_mel_num_frames", "cfm_mel_output_frames",
                "cfm_mel_forward", "cfm_normalize_batch", "cfm_mel_filterbank_slaney")
+# every symbol include/cfm_rnnt_loss.h declares
+RNNT_LOSS_SYMBOLS = ("cfm_rnnt_loss_workspace_size", "cfm_rnnt_loss")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",
@@ -143,6 +146,9 @@ def load() -> ctypes.CDLL:
         "cfm_normalize_batch": (ci, [vp, vp, ci, ci, ci, ci, vp, vp]),
         "cfm_mel_filterbank_slaney": (ci, [ci, ci, ci, ctypes.c_double, ctypes.c_double, ci, ci,
                                            ctypes.POINTER(ctypes.c_float)]),
+        "cfm_rnnt_loss_workspace_size": (sz, [ci, ci, ci]),
+        "cfm_rnnt_loss": (ci, [vp, vp, ci, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, ctypes.c_float, vp, vp, vp, sz,
+                               vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -1,0 +1,41 @@
+/*
+ * cfm_rnnt_loss.h — C-ABI of the MI355X-native RNN-T loss (libcfm.so), SURVEY §8 row f2: the step
+ * after the joint in BASELINE config-4 training.
+ *
+ * Replaces the arithmetic behind
+ *   nemo.collections.asr.losses.rnnt.RNNTLoss.forward()           (losses/rnnt.py:252-306)
+ *   RNNTLossNumba / _RNNTNumba.forward()                          (numba/rnnt_loss/rnnt_pytorch.py:36-84, 191-219)
+ *   GPURNNT.compute_cost_and_score(): log-softmax denominators,   (numba/rnnt_loss/utils/cuda_utils/gpu_rnnt.py:122-238)
+ *     compute_alphas_kernel / compute_betas_kernel /              (gpu_rnnt_kernel.py:66-399)
+ *     compute_grad_kernel (FastEmit, clamp), compute_costs_data   (rnnt_helper.py:106-115)
+ * acts are the joint's raw logits (B, T, U, V) fp32 (the log-softmax is folded in, as the GPU
+ * reference does); costs[b] = -log P(y_b | x_b) * (1 + fastemit_lambda); grads (optional) =
+ * d costs[b] / d acts[b], zero outside each utterance's (act_len, label_len + 1) lattice.
+ *
+ * Conventions as in cfm_encoder.h: device pointers, status codes + cfm_last_error(),
+ * stream-ordered (void* = hipStream_t), caller-owned workspace, no host synchronisation.
+ */
+#ifndef CFM_RNNT_LOSS_H_
+#define CFM_RNNT_LOSS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cfm_encoder.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+size_t cfm_rnnt_loss_workspace_size(int B, int T, int U);
+/* labels (B, labels_ld) int32 (entries past label_lens[b] ignored); act_lens / label_lens (B) int32
+ * with act_lens[b] <= T and label_lens[b] + 1 <= U (clamped on device otherwise); clamp <= 0 = off. */
+cfm_status cfm_rnnt_loss(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+                         const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
+                         float clamp, float* costs, float* grads, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFM_RNNT_LOSS_H_ */

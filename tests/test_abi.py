@@ -38,7 +38,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(stream) == set(_lib.STREAM_SYMBOLS)
     mel = _declared_symbols("cfm_mel.h")
     assert set(mel) == set(_lib.MEL_SYMBOLS)
-    for name in ctc + train + joint + stream + mel:
+    rl = _declared_symbols("cfm_rnnt_loss.h")
+    assert set(rl) == set(_lib.RNNT_LOSS_SYMBOLS)
+    for name in ctc + train + joint + stream + mel + rl:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
