@@ -1,6 +1,6 @@
 """ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
-cfm_joint.h, cfm_stream.h, cfm_mel.h and
-cfm_rnnt_loss.h).
+cfm_joint.h, cfm_stream.h, cfm_mel.h,
+cfm_rnnt_loss.h and cfm_augment.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -47,6 +47,8 @@ MEL_SYMBOLS = ("cfm_mel_create", "cfm_mel_destroy", "cfm_mel_set_tables", "cfm_m
                "cfm_mel_forward", "cfm_normalize_batch", "cfm_mel_filterbank_slaney")
 # every symbol include/cfm_rnnt_loss.h declares
 RNNT_LOSS_SYMBOLS = ("cfm_rnnt_loss_workspace_size", "cfm_rnnt_loss")
+# every symbol include/cfm_augment.h declares
+AUGMENT_SYMBOLS = ("cfm_spec_mask_rects", "cfm_spec_shot")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",
@@ -149,6 +151,8 @@ def load() -> ctypes.CDLL:
         "cfm_rnnt_loss_workspace_size": (sz, [ci, ci, ci]),
         "cfm_rnnt_loss": (ci, [vp, vp, ci, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, ctypes.c_float, vp, vp, vp, sz,
                                vp]),
+        "cfm_spec_mask_rects": (ci, [vp, ci, ci, ci, vp, ci, ctypes.c_float, vp]),
+        "cfm_spec_shot": (ci, [vp, vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),
         "cfm_ctc_head_destroy": (None, [vp]),
         "cfm_ctc_head_set_weights": (ci, [vp, vp, vp, vp]),

@@ -2,4 +2,5 @@
 from nemo.collections.asr.modules.conformer_encoder import ConformerEncoder  # noqa: F401
 from nemo.collections.asr.modules.conv_asr import ConvASRDecoder  # noqa: F401
 from nemo.collections.asr.modules.rnnt import RNNTJoint  # noqa: F401
-from nemo.collections.asr.modules.audio_preprocessing import AudioToMelSpectrogramPreprocessor  # noqa: F401
+from nemo.collections.asr.modules.audio_preprocessing import (  # noqa: F401
+    AudioToMelSpectrogramPreprocessor, SpectrogramAugmentation)

@@ -1,20 +1,26 @@
-"""Drop-in `AudioToMelSpectrogramPreprocessor` (reference
+"""Drop-in `AudioToMelSpectrogramPreprocessor` and `SpectrogramAugmentation` (reference
 nemo/collections/asr/modules/audio_preprocessing.py:63-281), SURVEY §8 row f1: the yaml
 `preprocessor._target_` of conformer_ctc_bpe.yaml:78-92 resolves here with the same kwargs, the
 same `featurizer.window` / `featurizer.fb` buffers, and keyword-only forward(input_signal, length)
 -> (processed_signal (B, features, T), processed_length (B,)).  The featurizer runs in
 libcfm.so (include/cfm_mel.h).
+
+`SpectrogramAugmentation` (audio_preprocessing.py:416-521) composes the drop-in
+SpecCutout / SpecAugment / SpecShot (on-device masking, include/cfm_augment.h) and picks one per
+call with the global `random.choice`, as the reference does.
 """
 from __future__ import annotations
 
+import random
 from collections import OrderedDict
 
 import torch
 
 from nemo.collections.asr.parts.preprocessing.features import FilterbankFeatures
+from nemo.collections.asr.parts.submodules.spectr_augment import SpecAugment, SpecCutout, SpecShot
 from nemo.core.classes.common import typecheck
 from nemo.core.classes.module import NeuralModule
-from nemo.core.neural_types import AudioSignal, LengthsType, MelSpectrogramType, NeuralType
+from nemo.core.neural_types import AudioSignal, LengthsType, MelSpectrogramType, NeuralType, SpectrogramType
 
 
 class AudioPreprocessor(NeuralModule):
@@ -77,3 +83,42 @@ class AudioToMelSpectrogramPreprocessor(AudioPreprocessor):
     @property
     def filter_banks(self):
         return self.featurizer.filter_banks
+
+
+class SpectrogramAugmentation(NeuralModule):
+    """audio_preprocessing.py:416-521: one of SpecCutout / SpecAugment / SpecShot per call."""
+
+    @property
+    def input_types(self):
+        return {"input_spec": NeuralType(("B", "D", "T"), SpectrogramType()),
+                "length": NeuralType(tuple("B"), LengthsType())}
+
+    @property
+    def output_types(self):
+        return {"augmented_spec": NeuralType(("B", "D", "T"), SpectrogramType())}
+
+    def __init__(self, freq_masks=0, time_masks=0, freq_width=10, time_width=10, rect_masks=0, rect_time=5,
+                 rect_freq=20, specshot_ratio=0, rng=None, augmask_value=0.0, use_numba_spec_augment: bool = True):
+        super().__init__()
+        self.augment_type = []
+        if rect_masks > 0:
+            self.spec_cutout = SpecCutout(rect_masks=rect_masks, rect_time=rect_time, rect_freq=rect_freq, rng=rng)
+            self.augment_type.append("spec_cutout")
+        if freq_masks + time_masks > 0:
+            self.spec_augment = SpecAugment(freq_masks=freq_masks, time_masks=time_masks, freq_width=freq_width,
+                                            time_width=time_width, rng=rng, mask_value=augmask_value)
+            self.augment_type.append("spec_augment")
+        if specshot_ratio > 0.0:
+            self.spec_shot = SpecShot(mask_ratio=specshot_ratio, mask_value=augmask_value)
+            self.augment_type.append("spec_shot")
+
+    @typecheck()
+    def forward(self, input_spec, length):
+        if len(self.augment_type) == 0:
+            return input_spec
+        augment = random.choice(self.augment_type)
+        if augment == "spec_augment":
+            return self.spec_augment(input_spec=input_spec, length=length)
+        elif augment == "spec_shot":
+            return self.spec_shot(input_spec=input_spec)
+        return self.spec_cutout(input_spec=input_spec)

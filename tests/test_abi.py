@@ -40,7 +40,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(mel) == set(_lib.MEL_SYMBOLS)
     rl = _declared_symbols("cfm_rnnt_loss.h")
     assert set(rl) == set(_lib.RNNT_LOSS_SYMBOLS)
-    for name in ctc + train + joint + stream + mel + rl:
+    aug = _declared_symbols("cfm_augment.h")
+    assert set(aug) == set(_lib.AUGMENT_SYMBOLS)
+    for name in ctc + train + joint + stream + mel + rl + aug:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
