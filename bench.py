@@ -123,12 +123,13 @@ def main():
     ap.add_argument("--layers", type=int, default=17)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "mel"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "mel", "decode"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
                          "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
                          "joint: config 4 (Large-17 encoder B=16 T=1600 + RNN-T joint U=100 V=1024); "
                          "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks); "
-                         "mel: the log-mel preprocessor in front of config 2 (SURVEY f1)")
+                         "mel: the log-mel preprocessor in front of config 2 (SURVEY f1); "
+                         "decode: config-4 transducer inference (encoder + greedy batch RNN-T decoding, SURVEY f2)")
     ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
     args = ap.parse_args()
 
@@ -156,6 +157,8 @@ def main():
         return run_stream(args, world, rank, dev, dist, barrier)
     if args.mode == "mel":
         return run_mel(args, world, rank, dev, dist, barrier)
+    if args.mode == "decode":
+        return run_decode(args, world, rank, dev, dist, barrier)
     from nemo.collections.asr.modules import ConformerEncoder
     torch.manual_seed(0)
     d, H, L, B, T = 512, 8, args.layers, args.batch, args.seq
@@ -347,10 +350,10 @@ JOINT_METRIC = "encoder+joint audio-frames/sec, Conformer-Transducer-Large B=16 
 
 
 def run_joint(args, world, rank, dev, dist, barrier):
-    """BASELINE config 4: Large-17 encoder forward (B=16, T=1600) + RNNTJoint forward over the
-    (B, T'=400, U+1=101) lattice with V=1024 (+blank), logits as on a GPU (rnnt.py:998-1002).
-    The prediction-network output is synthetic (B, 640, U+1): the decoder LSTM is not on this path."""
-    from nemo.collections.asr.modules import ConformerEncoder, RNNTJoint
+    """BASELINE config 4: Large-17 encoder forward (B=16, T=1600) + RNNTDecoder prediction network
+    over U=100 random targets (+SOS) + RNNTJoint forward over the (B, T'=400, U+1=101) lattice with
+    V=1024 (+blank), logits as on a GPU (rnnt.py:998-1002)."""
+    from nemo.collections.asr.modules import ConformerEncoder, RNNTDecoder, RNNTJoint
     torch.manual_seed(0)
     d, H, L, B, T, U, V = 512, 8, args.layers, 16, 1600, 100, 1024
     enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
@@ -361,10 +364,13 @@ def run_joint(args, world, rank, dev, dist, barrier):
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(B, 80, T, device=dev, generator=g)
     lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
-    pred = torch.randn(B, 640, U + 1, device=dev, generator=g)
+    dec = RNNTDecoder(prednet=dict(pred_hidden=640, pred_rnn_layers=1), vocab_size=V).to(dev).eval()
+    targets = torch.randint(0, V, (B, U), device=dev, generator=g)
+    tlen = torch.full((B,), U, dtype=torch.int64, device=dev)
 
     def step():
         y, yl = enc(audio_signal=x, length=lengths)
+        pred, _, _ = dec(targets=targets, target_length=tlen)
         return joint(encoder_outputs=y, decoder_outputs=pred)
 
     with torch.inference_mode():
@@ -377,20 +383,77 @@ def run_joint(args, world, rank, dev, dist, barrier):
     Tp = (((T - 1) // 2 + 1) - 1) // 2 + 1
     f_enc = encoder_flops(B, T, d, L)
     f_joint = 2 * B * Tp * d * 640 + 2 * B * (U + 1) * 640 * 640 + 2 * B * Tp * (U + 1) * 640 * (V + 1)
-    tot = f_enc + f_joint
+    f_pred = 2 * B * (U + 1) * (2 * 640) * (4 * 640)
+    tot = f_enc + f_joint + f_pred
     emit(rank, dist, {
         "metric": JOINT_METRIC, "value": round(job_throughput(t_max, world, B, T, args.steps), 1),
         "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.compute, "data": "synthetic",
-        "config": {"workload": f"Conformer-Transducer-Large encoder ({L} layers) + RNNTJoint (640 hidden, relu), "
+        "config": {"workload": f"Conformer-Transducer-Large encoder ({L} layers) + RNNTDecoder (LSTM 640, 1 layer, "
+                               f"U={U} targets + SOS) + RNNTJoint (640 hidden, relu), "
                                f"B={B}/GPU, T={T}, U+1={U + 1}, V+1={V + 1}, logits fp32 "
                                f"({B * Tp * (U + 1) * (V + 1) * 4 / 1e9:.2f} GB per step)",
                    "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (replicas, no collective)"},
         "model_flops": {"GFLOP_per_step_per_gpu": round(tot / 1e9, 1), "encoder_GFLOP": round(f_enc / 1e9, 1),
-                        "joint_GFLOP": round(f_joint / 1e9, 1),
+                        "joint_GFLOP": round(f_joint / 1e9, 1), "prediction_net_GFLOP": round(f_pred / 1e9, 2),
                         "TFLOP/s_per_gpu": round(tot / (ms_step * 1e-3) / 1e12, 1),
                         "frac_of_peak": round(tot / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
+
+
+DECODE_METRIC = "transducer greedy inference audio-frames/sec, Conformer-Transducer-Large B=16 T=1600 V=1024 (config 4 + SURVEY f2)"
+
+
+def run_decode(args, world, rank, dev, dist, barrier):
+    """Config-4 transducer inference: Large-17 encoder forward (B=16, T=1600) followed by greedy batch
+    RNN-T decoding (GreedyBatchedRNNTInfer, max_symbols 30, conformer_transducer_bpe.yaml:172-177) with
+    the LSTM prediction network (640, 1 layer) and the joint (640, relu, V=1024).  Random weights; the
+    joint's blank logit is biased (+BLANK_BIAS) so the emission rate is speech-like (reported)."""
+    from nemo.collections.asr.modules import ConformerEncoder, RNNTDecoder, RNNTJoint
+    from nemo.collections.asr.parts.submodules.rnnt_greedy_decoding import GreedyBatchedRNNTInfer
+    torch.manual_seed(0)
+    d, H, L, B, T, V = 512, 8, args.layers, 16, 1600, 1024
+    blank_bias = float(os.environ.get("BLANK_BIAS", "1.5"))
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
+    enc.set_compute_mode(args.compute)
+    dec = RNNTDecoder(prednet=dict(pred_hidden=640, pred_rnn_layers=1), vocab_size=V).to(dev).eval()
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=d, pred_hidden=640, joint_hidden=640, activation="relu"),
+                      num_classes=V).to(dev).eval()
+    with torch.no_grad():
+        joint.joint_net[-1].bias[V] += blank_bias
+    greedy = GreedyBatchedRNNTInfer(dec, joint, blank_index=V, max_symbols_per_step=30)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, 80, T, device=dev, generator=g)
+    lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
+    dec_ms = []
+
+    def step():
+        y, yl = enc(audio_signal=x, length=lengths)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        hyps = greedy(encoder_output=y, encoded_lengths=yl)[0]
+        dec_ms.append(1000.0 * (time.perf_counter() - t0))
+        return hyps
+
+    with torch.inference_mode():
+        elapsed, hyps = timed_loop(step, args.warmup, args.steps, barrier)
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    Tp = (((T - 1) // 2 + 1) - 1) // 2 + 1
+    ntok = sum(len(h.y_sequence) for h in hyps)
+    emit(rank, dist, {
+        "metric": DECODE_METRIC, "value": round(job_throughput(t_max, world, B, T, args.steps), 1),
+        "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": f"{args.compute} encoder, fp32 decoder", "data": "synthetic",
+        "config": {"workload": f"Conformer-Transducer-Large encoder ({L} layers, B={B}, T={T} -> T'={Tp}) + greedy "
+                               f"batch RNN-T decoding (LSTM 640, joint 640 relu, V+1={V + 1}, max_symbols 30, "
+                               f"blank logit bias +{blank_bias})",
+                   "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world} (replicas, no collective)"},
+        "decode": {"ms_per_step": round(sorted(dec_ms[-args.steps:])[len(dec_ms[-args.steps:]) // 2], 3),
+                   "tokens_per_step": ntok, "tokens_per_frame": round(ntok / (B * Tp), 3),
+                   "note": "median host wall time of the greedy decode (it synchronises: it polls a device done-flag)"},
     })
 
 

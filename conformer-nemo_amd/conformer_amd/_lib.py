@@ -1,6 +1,6 @@
 """ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
 cfm_joint.h, cfm_stream.h, cfm_mel.h,
-cfm_rnnt_loss.h and cfm_augment.h).
+cfm_rnnt_loss.h, cfm_augment.h and cfm_rnnt_decode.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -49,6 +49,10 @@ MEL_SYMBOLS = ("cfm_mel_create", "cfm_mel_destroy", "cfm_mel_set_tables", "cfm_m
 RNNT_LOSS_SYMBOLS = ("cfm_rnnt_loss_workspace_size", "cfm_rnnt_loss")
 # every symbol include/cfm_augment.h declares
 AUGMENT_SYMBOLS = ("cfm_spec_mask_rects", "cfm_spec_shot")
+# every symbol include/cfm_rnnt_decode.h declares (bound in conformer_amd/rnnt_decode.py)
+RNNT_DECODE_SYMBOLS = ("cfm_rnnt_decoder_create", "cfm_rnnt_decoder_destroy", "cfm_rnnt_decoder_set_weights",
+                       "cfm_rnnt_decoder_predict_workspace_size", "cfm_rnnt_decoder_predict",
+                       "cfm_rnnt_greedy_workspace_size", "cfm_rnnt_greedy_decode")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",

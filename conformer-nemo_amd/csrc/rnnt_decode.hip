@@ -1,0 +1,691 @@
+// RNN-T prediction network (LSTM) and greedy batch decoding (SURVEY §8 a-ext4 / f2); contract in
+// include/cfm_rnnt_decode.h.
+//
+// Everything here is a skinny fp32 contraction: a handful of utterances (rows) against weight
+// matrices of a few MB, so the kernels are weight-bandwidth bound (L2 / MALL resident after the first
+// iteration).  Shape of every kernel: a block stages RB utterance rows of its input in LDS once; each
+// wave owns 4 output columns, its lanes stride the contraction axis with coalesced weight loads and
+// keep 4 x RB partial sums, which one LDS transpose turns into per-(column, row) totals; the epilogue
+// is fused (LSTM cell update, joint activation, or the per-block max / argmax / sum-exp of the logits).
+//   lstm_step_kernel   one layer step: the 4 gate rows (i, f, g, o) of a hidden unit live in one wave,
+//                      so the cell update needs no second pass
+//   joint_hidden_kernel  act(f[b, t_b] + W_pred h + b_pred) for each utterance's current frame
+//   joint_logits_kernel  W_out hid + b_out -> block partials (max, first argmax, sum exp(z - max))
+//   greedy_commit_kernel one block: argmax/log-sum-exp fold, emit-or-advance decision per utterance,
+//                        state commit for emitting utterances, the any-active flag
+//   enc_proj_kernel      f = enc W_enc^T + b_enc for all (b, t) up front (64x64 LDS-tiled fp32 GEMM
+//                        reading the (B, D1, T) encoder output along time)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/cfm_rnnt_decode.h"
+#include "cfm_abi.h"
+
+using namespace cfm;
+
+struct cfm_rnnt_decoder {
+  int V = 0, H = 0, L = 0, device = 0;
+  float* wbuf = nullptr;        // emb (V+1, H) | per layer [W_ih | W_hh] (4H, 2H) | per layer bias (4H)
+  long emb_off = 0, w_off = 0, b_off = 0;
+  int* host_flag = nullptr;     // pinned, 2 slots (greedy done-flag polling)
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  const float* emb() const { return wbuf + emb_off; }
+  const float* W(int l) const { return wbuf + w_off + (long)l * 4 * H * 2 * H; }
+  const float* bias(int l) const { return wbuf + b_off + (long)l * 4 * H; }
+};
+
+namespace {
+
+constexpr int RB = 8;                 // utterance rows per block
+constexpr int RED = 4 * 64 * 33;      // per-block transpose-reduce scratch (floats)
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float act_fn(int act, float x) {
+  return act == CFM_JOINT_RELU ? fmaxf(x, 0.0f) : act == CFM_JOINT_SIGMOID ? sigm(x) : tanhf(x);
+}
+
+// Stage rows [b0, b0 + nb) of concat(x, h) (I + Hh floats per row, both multiples of 4) into As as
+// float4s.  x comes from xsrc, or from the embedding row xlab[b] (xlab < 0: the zero
+// start-of-sequence vector).  All of a thread's loads are issued before the LDS stores (latency).
+__device__ __forceinline__ void stage_rows(float* As, int K, int I, int Hh, int b0, int nb, const float* xsrc,
+                                           const int32_t* xlab, const float* emb, int nemb, const float* h) {
+  const int K4 = K >> 2, I4 = I >> 2;
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    const long b = b0 + r;
+    const float4* xs = nullptr;
+    if (r < nb) {
+      if (xsrc) xs = (const float4*)(xsrc + b * I);
+      else if (xlab[b] >= 0) xs = (const float4*)(emb + (long)min(xlab[b], nemb - 1) * I);
+    }
+    const float4* hs = (r < nb && Hh > 0) ? (const float4*)(h + b * Hh) : nullptr;
+    for (int k4 = threadIdx.x; k4 < K4; k4 += blockDim.x) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k4 < I4) { if (xs) v = xs[k4]; }
+      else if (hs) v = hs[k4 - I4];
+      ((float4*)As)[r * K4 + k4] = v;
+    }
+  }
+}
+
+// acc[c][r] = sum_k As[r][k] * Wrow_c[k] over this lane's float4 slots; then the per-wave transpose:
+// lane l < 4*RB returns the total for (c = l / RB, r = l % RB).  K % 4 == 0.
+__device__ __forceinline__ float wave_dot4(const float* As, int K, const float* const (&wr)[4], bool valid,
+                                           float* red_wave) {
+  const int lane = threadIdx.x & 63;
+  const int K4 = K >> 2;
+  float acc[4][RB];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < RB; ++r) acc[c][r] = 0.0f;
+  if (valid) {
+    // UK float4 steps of weight loads are issued before any is consumed: the loop is latency-bound,
+    // so this keeps 4 * UK 16-byte loads in flight per lane.
+    constexpr int UK = 8;                 // one round for K <= 2048
+    for (int k4 = lane; k4 < K4; k4 += 64 * UK) {
+      float4 w[UK][4];
+#pragma unroll
+      for (int u = 0; u < UK; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int kk = k4 + 64 * u;
+          w[u][c] = (wr[c] && kk < K4) ? ((const float4*)wr[c])[kk] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+      for (int u = 0; u < UK; ++u) {
+        const int kk = min(k4 + 64 * u, K4 - 1);   // out-of-range steps multiply zero weights
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const float4 a = ((const float4*)(As + r * K))[kk];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float t = acc[c][r];
+            t = fmaf(w[u][c].x, a.x, t);
+            t = fmaf(w[u][c].y, a.y, t);
+            t = fmaf(w[u][c].z, a.z, t);
+            acc[c][r] = fmaf(w[u][c].w, a.w, t);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int r = 0; r < RB; ++r) red_wave[lane * 33 + c * RB + r] = acc[c][r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  float s = 0.0f;
+  if (lane < 4 * RB)
+    for (int l = 0; l < 64; ++l) s += red_wave[l * 33 + lane];
+  return s;
+}
+
+// One LSTM layer step for rows [b0, b0 + RB): wave w owns hidden unit j = 4 * blockIdx.x + w.
+__global__ __launch_bounds__(256) void lstm_step_kernel(const float* __restrict__ W, const float* __restrict__ bias,
+                                                        const float* __restrict__ emb, int nemb,
+                                                        const int32_t* __restrict__ xlab, const float* __restrict__ xsrc,
+                                                        const float* __restrict__ h, const float* __restrict__ c,
+                                                        float* __restrict__ h2, float* __restrict__ c2,
+                                                        float* __restrict__ gout, long gstride, int B, int I, int H,
+                                                        const int* __restrict__ run_flag) {
+  if (run_flag && *run_flag == 0) return;   // uniform: every utterance finished
+  extern __shared__ float lds[];
+  const int K = I + H;
+  const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  float* As = lds;
+  float* red = lds + RB * K;
+  float* gsum = red + RED;               // [4 waves][4 * RB] gate totals
+  stage_rows(As, K, I, H, b0, nb, xsrc, xlab, emb, nemb, h);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + wave;
+  const bool valid = j < H;
+  const float* wr[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) wr[g] = valid ? W + (long)(g * H + j) * K : nullptr;
+  float* rw = red + wave * 64 * 33;
+  const float s = wave_dot4(As, K, wr, valid, rw);
+  // gather the 4 gates of row r into lane r
+  float* gs = gsum + wave * 4 * RB;
+  if (lane < 4 * RB) gs[lane] = s;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (!valid || lane >= nb) return;
+  const long b = b0 + lane;
+  const float gi = sigm(gs[0 * RB + lane] + bias[0 * H + j]);
+  const float gf = sigm(gs[1 * RB + lane] + bias[1 * H + j]);
+  const float gg = tanhf(gs[2 * RB + lane] + bias[2 * H + j]);
+  const float go = sigm(gs[3 * RB + lane] + bias[3 * H + j]);
+  const float cn = gf * c[b * H + j] + gi * gg;
+  const float hn = go * tanhf(cn);
+  c2[b * H + j] = cn;
+  h2[b * H + j] = hn;
+  if (gout) gout[b * gstride + j] = hn;
+}
+
+// hid[b][n] = act(F[b, t_b][n] + sum_k h[b][k] Wp[n][k] + bp[n]),  n < J
+__global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restrict__ Wp, const float* __restrict__ bp,
+                                                           const float* __restrict__ h, const float* __restrict__ F,
+                                                           const int32_t* __restrict__ tptr, int T, int B, int H,
+                                                           int J, int act, float* __restrict__ hid,
+                                                           const int* __restrict__ run_flag) {
+  if (run_flag && *run_flag == 0) return;
+  extern __shared__ float lds[];
+  const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  float* As = lds;
+  float* red = lds + RB * H;
+  stage_rows(As, H, H, 0, b0, nb, h, nullptr, nullptr, 1, nullptr);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n0 = blockIdx.x * 16 + wave * 4;
+  const float* wr[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) wr[c] = (n0 + c < J) ? Wp + (long)(n0 + c) * H : nullptr;
+  const float s = wave_dot4(As, H, wr, n0 < J, red + wave * 64 * 33);
+  if (lane >= 4 * RB) return;
+  const int c = lane / RB, r = lane % RB, n = n0 + c;
+  if (r >= nb || n >= J) return;
+  const long b = b0 + r;
+  const int t = min(max(tptr[b], 0), T - 1);
+  hid[b * J + n] = act_fn(act, s + bp[n] + F[(b * T + t) * J + n]);
+}
+
+struct Part {
+  float m;
+  int idx;
+  float se;
+};
+
+// z[b][n] = sum_k hid[b][k] Wo[n][k] + bo[n] for the block's 16 columns -> part[blockIdx.x * B + b]
+__global__ __launch_bounds__(256) void joint_logits_kernel(const float* __restrict__ Wo, const float* __restrict__ bo,
+                                                           const float* __restrict__ hid, int B, int J, int N,
+                                                           Part* __restrict__ part, const int* __restrict__ run_flag) {
+  if (run_flag && *run_flag == 0) return;
+  extern __shared__ float lds[];
+  const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  float* As = lds;
+  float* red = lds + RB * J;
+  float* zs = red + RED;                 // [16][RB]
+  stage_rows(As, J, J, 0, b0, nb, hid, nullptr, nullptr, 1, nullptr);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n0 = blockIdx.x * 16 + wave * 4;
+  const float* wr[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) wr[c] = (n0 + c < N) ? Wo + (long)(n0 + c) * J : nullptr;
+  const float s = wave_dot4(As, J, wr, n0 < N, red + wave * 64 * 33);
+  if (lane < 4 * RB) {
+    const int c = lane / RB, r = lane % RB;
+    const int n = n0 + c;
+    zs[(wave * 4 + c) * RB + r] = (n < N) ? s + bo[n] : -INFINITY;
+  }
+  __syncthreads();
+  if (threadIdx.x >= nb) return;
+  const int r = threadIdx.x;
+  const int nend = min(16, N - blockIdx.x * 16);
+  float m = -INFINITY;
+  int idx = -1;
+  for (int c = 0; c < nend; ++c) {
+    const float z = zs[c * RB + r];
+    if (idx < 0 || z > m) { m = z; idx = blockIdx.x * 16 + c; }
+  }
+  float se = 0.0f;
+  for (int c = 0; c < nend; ++c) se += expf(zs[c * RB + r] - m);
+  part[(long)blockIdx.x * B + b0 + r] = Part{m, idx, se};
+}
+
+struct Ctrl {
+  int32_t* t;        // current frame
+  int32_t* s;        // labels emitted at this frame
+  int32_t* xlab;     // next LSTM input label (-1: zero SOS vector)
+  int32_t* active;
+  int32_t* copy;     // 1: commit the new state this iteration
+  int* flag;         // any utterance still active
+};
+
+__global__ __launch_bounds__(256) void greedy_init_kernel(const int64_t* __restrict__ len, int B, int T, Ctrl ct,
+                                                          int32_t* __restrict__ ntok, double* __restrict__ scores,
+                                                          float* __restrict__ hc, long nhc) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) {
+    ct.t[i] = 0;
+    ct.s[i] = 0;
+    ct.xlab[i] = -1;
+    const long L = len[i];
+    ct.active[i] = (min(L, (long)T) > 0) ? 1 : 0;
+    ct.copy[i] = 0;
+    ntok[i] = 0;
+    scores[i] = 0.0;
+  }
+  if (i == 0) *ct.flag = 1;
+  for (long k = i; k < nhc; k += (long)gridDim.x * blockDim.x) hc[k] = 0.0f;
+}
+
+// One wave per utterance (grid B): fold the logits partials (lanes stride the column blocks), decide
+// emit-or-advance, record the label, commit the new LSTM state if a label was emitted.
+__global__ __launch_bounds__(64) void greedy_commit_kernel(const Part* __restrict__ part, int nblk, int B, int T,
+                                                           const int64_t* __restrict__ len, int blank,
+                                                           int max_symbols, int log_normalize, int sos_until_label,
+                                                           Ctrl ct, int32_t* __restrict__ tokens,
+                                                           int32_t* __restrict__ tsteps, long cap,
+                                                           int32_t* __restrict__ ntok, double* __restrict__ scores,
+                                                           float* __restrict__ h, float* __restrict__ c,
+                                                           const float* __restrict__ h2, const float* __restrict__ c2,
+                                                           int L, int H) {
+  if (*ct.flag == 0) return;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (!ct.active[b]) return;                    // block-uniform
+  float m = -INFINITY;
+  int k = -1;
+  for (int q = lane; q < nblk; q += 64) {
+    const Part p = part[(long)q * B + b];
+    if (k < 0 || p.m > m) { m = p.m; k = p.idx; }
+  }
+  // wave argmax (ties -> lowest column: the partials' own first-max rule, folded in index order)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int k2 = __shfl_xor(k, o, 64);
+    if (k2 >= 0 && (k < 0 || m2 > m || (m2 == m && k2 < k))) { m = m2; k = k2; }
+  }
+  double v = m;
+  if (log_normalize) {
+    double s = 0.0;
+    for (int q = lane; q < nblk; q += 64) {
+      const Part p = part[(long)q * B + b];
+      s += (double)p.se * exp((double)p.m - (double)m);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    v = -log(s);                                // z[k] - logsumexp(z) with z[k] = max
+  }
+  const int tb = ct.t[b];
+  const bool emit = k != blank;
+  if (lane == 0) {
+    if (emit) {
+      const int n = ntok[b];
+      tokens[b * cap + n] = k;
+      tsteps[b * cap + n] = tb;
+      ntok[b] = n + 1;
+      scores[b] += v;
+      ct.xlab[b] = k;
+      if (ct.s[b] + 1 >= max_symbols) { ct.t[b] = tb + 1; ct.s[b] = 0; } else { ct.s[b] += 1; }
+    } else {
+      // batched decoding embeds the blank (padding) row after the first step; the per-utterance
+      // decoder keeps feeding the zero SOS vector until a label is emitted (rnnt_greedy_decoding.py:315-318)
+      if (ct.xlab[b] < 0 && !sos_until_label) ct.xlab[b] = blank;
+      ct.t[b] = tb + 1;
+      ct.s[b] = 0;
+    }
+    const long lb = min(len[b], (long)T);
+    if (ct.t[b] >= lb) ct.active[b] = 0;
+  }
+  if (emit) {
+    for (int l = 0; l < L; ++l) {
+      const long o = ((long)l * B + b) * H;
+      for (int j = lane; j < H; j += 64) { h[o + j] = h2[o + j]; c[o + j] = c2[o + j]; }
+    }
+  }
+}
+
+// flag = any utterance still active (one block; run once per chunk of iterations)
+__global__ __launch_bounds__(256) void greedy_flag_kernel(const int32_t* __restrict__ active, int B, int* flag) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  int a = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) a |= active[b];
+  if (a) any = 1;                               // benign race: every writer stores 1
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = any;
+}
+
+// F[(b*T + t)*J + n] = sum_d enc[b][d][t] * W[n][d] + bias[n]
+__global__ __launch_bounds__(256) void enc_proj_kernel(const float* __restrict__ enc, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, int B, int T, int D, int J,
+                                                       float* __restrict__ F) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Ws[16][64 + 4];
+  const long M = (long)B * T;
+  const long m0 = (long)blockIdx.x * 64;
+  const int n0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < D; k0 += 16) {
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+      const int kk = i >> 6, mm = i & 63;
+      const long m = m0 + mm;
+      const int k = k0 + kk;
+      float v = 0.0f;
+      if (m < M && k < D) {
+        const long b = m / T, t = m - b * T;
+        v = enc[(b * D + k) * T + t];
+      }
+      As[kk][mm] = v;
+      const int nn = i >> 4, kw = i & 15;
+      const int n = n0 + nn, k2 = k0 + kw;
+      Ws[kw][nn] = (n < J && k2 < D) ? W[(long)n * D + k2] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = Ws[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], w[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n < J) F[m * J + n] = acc[i][j] + bias[n];
+    }
+  }
+}
+
+__global__ void predict_labels_kernel(const int64_t* __restrict__ y, int B, int U, int S, int add_sos, int nemb,
+                                      int32_t* __restrict__ xlab) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)S * B) return;
+  const int u = (int)(i / B), b = (int)(i % B);
+  const int uu = u - add_sos;
+  int lab = -1;
+  if (y && uu >= 0) lab = (int)min(max(y[(long)b * U + uu], (int64_t)0), (int64_t)(nemb - 1));
+  xlab[i] = lab;
+}
+
+__global__ void pack_lstm_kernel(const float* __restrict__ wih, const float* __restrict__ whh,
+                                 const float* __restrict__ bih, const float* __restrict__ bhh, int H,
+                                 float* __restrict__ Wc, float* __restrict__ bc) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = 4L * H * 2 * H;
+  if (i < n) {
+    const long r = i / (2 * H), k = i % (2 * H);
+    Wc[i] = k < H ? wih[r * H + k] : whh[r * H + (k - H)];
+  }
+  if (i < 4L * H) bc[i] = bih[i] + bhh[i];
+}
+
+size_t lstm_lds(int K) { return (size_t)(RB * K + RED + 4 * 4 * RB) * sizeof(float); }
+
+// > 64 KB of dynamic LDS needs the per-kernel opt-in; done once per process.
+void set_lds_limits() {
+  static const bool once = [] {
+    constexpr int kMax = 160 * 1024;
+    (void)hipFuncSetAttribute((const void*)lstm_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+    (void)hipFuncSetAttribute((const void*)joint_hidden_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+    (void)hipFuncSetAttribute((const void*)joint_logits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kMax);
+    return true;
+  }();
+  (void)once;
+}
+
+void check_device(const cfm_rnnt_decoder* h) {
+  int cur = -1;
+  HIP_OK(hipGetDevice(&cur));
+  if (cur != h->device) HIP_OK(hipSetDevice(h->device));
+}
+
+void lstm_layer(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, const float* xsrc, const float* hcur,
+                const float* ccur, float* hn, float* cn, float* gout, long gstride, int B, const int* flag,
+                hipStream_t st) {
+  const int H = d->H, K = 2 * H;
+  const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
+  hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(K), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
+                     xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, H, H, flag);
+}
+
+struct GreedyWs {
+  long F, h, c, h2, c2, hid, part, ctrl, total;
+};
+
+GreedyWs greedy_layout(const cfm_rnnt_decoder* d, int B, int T, int J) {
+  GreedyWs w{};
+  long o = 0;
+  auto take = [&](long bytes) { const long at = o; o += round_up(std::max(bytes, 1L), 256); return at; };
+  const long lbh = (long)d->L * B * d->H * 4;
+  w.F = take((long)B * T * J * 4);
+  w.h = take(lbh);
+  w.c = take(lbh);
+  w.h2 = take(lbh);
+  w.c2 = take(lbh);
+  w.hid = take((long)B * J * 4);
+  const long nblk = (d->V + 1 + 15) / 16;
+  w.part = take(nblk * B * (long)sizeof(Part));
+  w.ctrl = take(5L * B * 4 + 64);
+  w.total = o;
+  return w;
+}
+
+long predict_ws_bytes(const cfm_rnnt_decoder* d, int B, int U) {
+  const long lbh = round_up((long)d->L * B * d->H * 4, 256);
+  return 4 * lbh + round_up((long)(U + 2) * B * 4, 256);
+}
+
+}  // namespace
+
+extern "C" {
+
+cfm_status cfm_rnnt_decoder_create(int vocab_size, int pred_hidden, int layers, int device, cfm_rnnt_decoder** out) {
+  return guarded([&] {
+    if (!out) fail(CFM_ERR_INVALID_ARG, "null out");
+    *out = nullptr;
+    if (vocab_size < 1 || pred_hidden < 4 || pred_hidden > 1536 || pred_hidden % 4 || layers < 1 || layers > 16)
+      fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_decoder_create: need vocab_size >= 1, pred_hidden % 4 == 0 in [4, 1536], "
+                                "1 <= layers <= 16");
+    HIP_OK(hipSetDevice(device));
+    set_lds_limits();
+    auto* d = new cfm_rnnt_decoder();
+    d->V = vocab_size;
+    d->H = pred_hidden;
+    d->L = layers;
+    d->device = device;
+    const long H = pred_hidden;
+    d->emb_off = 0;
+    d->w_off = round_up((long)(vocab_size + 1) * H, 64);
+    d->b_off = d->w_off + (long)layers * 4 * H * 2 * H;
+    const long total = d->b_off + (long)layers * 4 * H;
+    hipError_t e = hipMalloc((void**)&d->wbuf, total * sizeof(float));
+    if (e == hipSuccess) e = hipHostMalloc((void**)&d->host_flag, 2 * sizeof(int), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->ev[0], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&d->ev[1], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      cfm_rnnt_decoder_destroy(d);
+      fail(CFM_ERR_NOMEM, std::string("cfm_rnnt_decoder_create: ") + hipGetErrorString(e));
+    }
+    *out = d;
+  });
+}
+
+void cfm_rnnt_decoder_destroy(cfm_rnnt_decoder* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->device);
+  if (d->wbuf) (void)hipFree(d->wbuf);
+  if (d->host_flag) (void)hipHostFree(d->host_flag);
+  for (auto& e : d->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete d;
+}
+
+cfm_status cfm_rnnt_decoder_set_weights(cfm_rnnt_decoder* d, const float* embed, const float* const* w_ih,
+                                        const float* const* w_hh, const float* const* b_ih,
+                                        const float* const* b_hh, void* stream) {
+  return guarded([&] {
+    if (!d || !embed || !w_ih || !w_hh || !b_ih || !b_hh) fail(CFM_ERR_INVALID_ARG, "null argument");
+    check_device(d);
+    hipStream_t st = (hipStream_t)stream;
+    const long H = d->H;
+    HIP_OK(hipMemcpyAsync(d->wbuf + d->emb_off, embed, (size_t)(d->V + 1) * H * sizeof(float),
+                          hipMemcpyDeviceToDevice, st));
+    for (int l = 0; l < d->L; ++l) {
+      if (!w_ih[l] || !w_hh[l] || !b_ih[l] || !b_hh[l]) fail(CFM_ERR_INVALID_ARG, "null LSTM parameter");
+      const long n = 4 * H * 2 * H;
+      hipLaunchKernelGGL(pack_lstm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w_ih[l], w_hh[l],
+                         b_ih[l], b_hh[l], (int)H, d->wbuf + d->w_off + (long)l * n, d->wbuf + d->b_off + l * 4 * H);
+    }
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_rnnt_decoder_predict_workspace_size(const cfm_rnnt_decoder* d, int B, int U) {
+  if (!d || B < 0 || U < 0) return 0;
+  return (size_t)predict_ws_bytes(d, B, std::max(U, 1));
+}
+
+cfm_status cfm_rnnt_decoder_predict(cfm_rnnt_decoder* d, const int64_t* y, int B, int U, int add_sos, const float* h0,
+                                    const float* c0, float* g, float* h_out, float* c_out, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    if (!d || !g || !h_out || !c_out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (B < 0 || U < 0 || (y && U < 1)) fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_decoder_predict: bad B / U");
+    if (B == 0) return;
+    check_device(d);
+    const int Ue = y ? U : 1;
+    const int S = Ue + (add_sos ? 1 : 0);
+    if (!workspace || (long)workspace_bytes < predict_ws_bytes(d, B, Ue))
+      fail(CFM_ERR_WORKSPACE, "cfm_rnnt_decoder_predict: workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    const long lbh = (long)d->L * B * d->H;
+    const long lbh_b = round_up(lbh * 4, 256);
+    char* ws = (char*)workspace;
+    float* hs[2] = {(float*)ws, (float*)(ws + 2 * lbh_b)};
+    float* cs[2] = {(float*)(ws + lbh_b), (float*)(ws + 3 * lbh_b)};
+    int32_t* xlab = (int32_t*)(ws + 4 * lbh_b);
+    if (h0) HIP_OK(hipMemcpyAsync(hs[0], h0, lbh * 4, hipMemcpyDeviceToDevice, st));
+    else HIP_OK(hipMemsetAsync(hs[0], 0, lbh * 4, st));
+    if (c0) HIP_OK(hipMemcpyAsync(cs[0], c0, lbh * 4, hipMemcpyDeviceToDevice, st));
+    else HIP_OK(hipMemsetAsync(cs[0], 0, lbh * 4, st));
+    hipLaunchKernelGGL(predict_labels_kernel, dim3((unsigned)(((long)S * B + 255) / 256)), dim3(256), 0, st, y, B,
+                       U, S, add_sos ? 1 : 0, d->V + 1, xlab);
+    const long bh = (long)B * d->H;
+    int cur = 0;
+    for (int u = 0; u < S; ++u) {
+      const int nx = cur ^ 1;
+      for (int l = 0; l < d->L; ++l) {
+        const bool top = l == d->L - 1;
+        lstm_layer(d, l, xlab + (long)u * B, l ? hs[nx] + (l - 1) * bh : nullptr, hs[cur] + l * bh, cs[cur] + l * bh,
+                   hs[nx] + l * bh, cs[nx] + l * bh, top ? g + (long)u * d->H : nullptr, (long)S * d->H, B, nullptr,
+                   st);
+      }
+      cur = nx;
+    }
+    HIP_OK(hipMemcpyAsync(h_out, hs[cur], lbh * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemcpyAsync(c_out, cs[cur], lbh * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_rnnt_greedy_workspace_size(const cfm_rnnt_decoder* d, int B, int T, int J) {
+  if (!d || B < 0 || T < 0 || J < 1) return 0;
+  return (size_t)greedy_layout(d, B, T, J).total;
+}
+
+cfm_status cfm_rnnt_greedy_decode(cfm_rnnt_decoder* d, const float* enc_bdt, const int64_t* enc_len, int B, int T,
+                                  int D1, int J, const float* w_enc, const float* b_enc, const float* w_pred,
+                                  const float* b_pred, const float* w_out, const float* b_out, int activation,
+                                  int max_symbols, int log_normalize, int sos_until_label, int32_t* tokens,
+                                  int32_t* timesteps, int32_t* ntok, double* scores, float* h_out, float* c_out,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    if (!d || !enc_bdt || !enc_len || !w_enc || !b_enc || !w_pred || !b_pred || !w_out || !b_out || !tokens ||
+        !timesteps || !ntok || !scores || !h_out || !c_out)
+      fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (B < 0 || T < 0 || D1 < 1 || J < 4 || J > 3072 || J % 4 || D1 > (1 << 20) || max_symbols < 1)
+      fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_greedy_decode: need D1 >= 1, J % 4 == 0 in [4, 3072], max_symbols >= 1");
+    if (((uintptr_t)w_pred | (uintptr_t)w_out) & 15) fail(CFM_ERR_INVALID_ARG, "joint weights must be 16-byte aligned");
+    if (activation < CFM_JOINT_RELU || activation > CFM_JOINT_TANH) fail(CFM_ERR_INVALID_ARG, "bad activation");
+    check_device(d);
+    hipStream_t st = (hipStream_t)stream;
+    const long lbh = (long)d->L * B * d->H;
+    if (B == 0) return;
+    if (T == 0) {
+      HIP_OK(hipMemsetAsync(ntok, 0, (size_t)B * 4, st));
+      HIP_OK(hipMemsetAsync(scores, 0, (size_t)B * 8, st));
+      HIP_OK(hipMemsetAsync(h_out, 0, lbh * 4, st));
+      HIP_OK(hipMemsetAsync(c_out, 0, lbh * 4, st));
+      HIP_OK(hipStreamSynchronize(st));
+      return;
+    }
+    const GreedyWs w = greedy_layout(d, B, T, J);
+    if (!workspace || (long)workspace_bytes < w.total) fail(CFM_ERR_WORKSPACE, "cfm_rnnt_greedy_decode: workspace too small");
+    char* ws = (char*)workspace;
+    float* F = (float*)(ws + w.F);
+    float* hS = (float*)(ws + w.h);
+    float* cS = (float*)(ws + w.c);
+    float* h2 = (float*)(ws + w.h2);
+    float* c2 = (float*)(ws + w.c2);
+    float* hid = (float*)(ws + w.hid);
+    Part* part = (Part*)(ws + w.part);
+    int32_t* ci = (int32_t*)(ws + w.ctrl);
+    Ctrl ct{ci, ci + B, ci + 2 * B, ci + 3 * B, ci + 4 * B, (int*)(ci + 5 * B)};
+    const int N = d->V + 1, H = d->H;
+    const int nblk = (N + 15) / 16;
+    const long cap = (long)T * max_symbols;
+
+    // f = enc W_enc^T + b_enc for every frame (rnnt.py:981 joint's enc projection), state and control init
+    hipLaunchKernelGGL(enc_proj_kernel, dim3((unsigned)(((long)B * T + 63) / 64), (J + 63) / 64), dim3(256), 0, st,
+                       enc_bdt, w_enc, b_enc, B, T, D1, J, F);
+    // hS and cS are adjacent in the workspace: zero both in one pass
+    hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)std::max<long>(1, std::min<long>((2 * lbh + 255) / 256, 1024))),
+                       dim3(256), 0, st, enc_len, B, T, ct, ntok, scores, hS, (long)((char*)h2 - (char*)hS) / 4);
+    HIP_OK(hipGetLastError());
+    const long bh = (long)B * H;
+    auto iteration = [&]() {
+      for (int l = 0; l < d->L; ++l)
+        lstm_layer(d, l, ct.xlab, l ? h2 + (l - 1) * bh : nullptr, hS + l * bh, cS + l * bh, h2 + l * bh, c2 + l * bh,
+                   nullptr, 0, B, ct.flag, st);
+      const dim3 gh((J + 15) / 16, (B + RB - 1) / RB);
+      hipLaunchKernelGGL(joint_hidden_kernel, gh, dim3(256), (size_t)(RB * H + RED) * 4, st, w_pred, b_pred,
+                         h2 + (long)(d->L - 1) * bh, F, ct.t, T, B, H, J, activation, hid, ct.flag);
+      const dim3 gl(nblk, (B + RB - 1) / RB);
+      hipLaunchKernelGGL(joint_logits_kernel, gl, dim3(256), (size_t)(RB * J + RED + 16 * RB) * 4, st, w_out, b_out,
+                         hid, B, J, N, part, ct.flag);
+      hipLaunchKernelGGL(greedy_commit_kernel, dim3(B), dim3(64), 0, st, part, nblk, B, T, enc_len, d->V,
+                         max_symbols, log_normalize, sos_until_label, ct, tokens, timesteps, cap, ntok, scores, hS, cS, h2, c2, d->L, H);
+    };
+    // Every iteration advances each active utterance by one frame or one label, so T * (max_symbols + 1)
+    // iterations always suffice.  Chunks of CH iterations are queued ahead; the done-flag copied after
+    // chunk i is read while chunk i + 1 runs (finished utterances make the extra kernels no-ops).
+    constexpr int CH = 8;
+    const long max_iter = (long)T * (max_symbols + 1) + 1;
+    long done_iter = 0;
+    int pending = -1;
+    for (int chunk = 0; done_iter < max_iter; ++chunk) {
+      for (int i = 0; i < CH && done_iter < max_iter; ++i, ++done_iter) iteration();
+      hipLaunchKernelGGL(greedy_flag_kernel, dim3(1), dim3(256), 0, st, ct.active, B, ct.flag);
+      const int slot = chunk & 1;
+      HIP_OK(hipMemcpyAsync(d->host_flag + slot, ct.flag, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIP_OK(hipEventRecord(d->ev[slot], st));
+      if (pending >= 0) {
+        HIP_OK(hipEventSynchronize(d->ev[pending]));
+        if (d->host_flag[pending] == 0) break;
+      }
+      pending = slot;
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h_out, hS, lbh * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemcpyAsync(c_out, cS, lbh * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));
+  });
+}
+
+}  // extern "C"

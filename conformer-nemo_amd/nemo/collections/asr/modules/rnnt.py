@@ -1,5 +1,15 @@
-"""Drop-in `nemo.collections.asr.modules.RNNTJoint` (reference nemo/collections/asr/modules/rnnt.py:613-1038)
-backed by the MI355X-native joint (include/cfm_joint.h).
+"""Drop-in `nemo.collections.asr.modules.RNNTDecoder` (reference rnnt.py:50-610, backed by
+include/cfm_rnnt_decode.h) and `RNNTJoint` (reference nemo/collections/asr/modules/rnnt.py:613-1038,
+backed by the MI355X-native joint, include/cfm_joint.h).
+
+RNNTDecoder: same constructor (prednet dict, vocab_size, normalization_mode, random_state_sampling,
+blank_as_pad), the same `prediction.embed` / `prediction.dec_rnn.lstm` parameters (state_dicts load
+unchanged; init as rnn.py:151-237: forget-gate bias, chrono init, weights_init_scale), keyword-only
+forward(targets, target_length, states) -> (g (B, H, U+1), target_length, states), `predict`, and the
+state bookkeeping helpers the decoders use.  The embedding + LSTM recurrence runs in libcfm.so (fp32).
+Differences by design: inference only (a forward that requires grad raises NotImplementedError);
+normalization_mode must be None and blank_as_pad True (the reference's defaults and the transducer
+configs' values); rnn_hidden_size > pred_hidden (LSTM projection) is not built.
 
 Same constructor (jointnet dict with encoder_hidden / pred_hidden / joint_hidden / activation /
 dropout, num_classes, vocabulary, log_softmax, preserve_memory, fuse_loss_wer, fused_batch_size),
@@ -21,9 +31,171 @@ import torch
 
 from nemo.core.classes.common import typecheck
 from nemo.core.classes.module import NeuralModule
-from nemo.core.neural_types import AcousticEncodedRepresentation, LogprobsType, NeuralType
+from nemo.core.neural_types import (AcousticEncodedRepresentation, ElementType, EmbeddedTextType, LabelsType,
+                                    LengthsType, LogprobsType, NeuralType)
 
-__all__ = ["RNNTJoint"]
+__all__ = ["RNNTDecoder", "RNNTJoint"]
+
+
+class _LSTMDropout(torch.nn.Module):
+    """Parameter container of rnn.LSTMDropout (nemo/collections/common/parts/rnn.py:151-237): an
+    nn.LSTM under `.lstm` (the arithmetic runs natively) with the reference's initialisation."""
+
+    def __init__(self, input_size, hidden_size, num_layers, dropout, forget_gate_bias, t_max=None,
+                 weights_init_scale=1.0, hidden_hidden_bias_scale=0.0):
+        super().__init__()
+        self.lstm = torch.nn.LSTM(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers,
+                                  dropout=dropout)
+        with torch.no_grad():
+            if t_max is not None:                                   # chrono init (rnn.py:194-205)
+                for name, p in self.lstm.named_parameters():
+                    if "bias" in name:
+                        n = p.nelement() // 4
+                        p.fill_(0)
+                        p[n:2 * n] = torch.log(torch.nn.init.uniform_(p[0:n], 1, t_max - 1))
+                        p[0:n] = -p[n:2 * n]
+            elif forget_gate_bias is not None:                      # rnn.py:206-213
+                for name, p in self.lstm.named_parameters():
+                    if "bias_ih" in name:
+                        p[hidden_size:2 * hidden_size].fill_(forget_gate_bias)
+                    if "bias_hh" in name:
+                        p[hidden_size:2 * hidden_size] *= float(hidden_hidden_bias_scale)
+            for name, p in self.named_parameters():
+                if "weight" in name or "bias" in name:
+                    p *= float(weights_init_scale)
+        self.dropout = torch.nn.Dropout(dropout) if dropout else None
+
+
+class RNNTDecoder(NeuralModule):
+    """Stateful LSTM prediction network (rnnt.py:50-610)."""
+
+    @property
+    def input_types(self):
+        return {"targets": NeuralType(("B", "T"), LabelsType()),
+                "target_length": NeuralType(tuple("B"), LengthsType()),
+                "states": [NeuralType(("D", "B", "D"), ElementType(), optional=True)]}
+
+    @property
+    def output_types(self):
+        return {"outputs": NeuralType(("B", "D", "T"), EmbeddedTextType()),
+                "prednet_lengths": NeuralType(tuple("B"), LengthsType()),
+                "states": [NeuralType(("D", "B", "D"), ElementType(), optional=True)]}
+
+    def __init__(self, prednet: Dict[str, Any], vocab_size: int, normalization_mode: Optional[str] = None,
+                 random_state_sampling: bool = False, blank_as_pad: bool = True):
+        super().__init__()
+        self.pred_hidden = prednet["pred_hidden"]
+        self.pred_rnn_layers = prednet["pred_rnn_layers"]
+        self.blank_idx = vocab_size
+        self.vocab_size = vocab_size
+        self.blank_as_pad = blank_as_pad
+        if not blank_as_pad:
+            raise NotImplementedError("blank_as_pad=False (masked greedy decoding) is not on the native path")
+        if normalization_mode is not None:
+            raise NotImplementedError("normalization_mode 'batch' / 'layer' LSTMs are not on the native path")
+        rnn_hidden_size = prednet.get("rnn_hidden_size", -1)
+        if rnn_hidden_size > 0 and rnn_hidden_size != self.pred_hidden:
+            raise NotImplementedError("rnn_hidden_size != pred_hidden (projected LSTM) is not on the native path")
+        self.random_state_sampling = random_state_sampling
+        dropout = prednet.get("dropout", 0.0)
+        self.prediction = torch.nn.ModuleDict({
+            "embed": torch.nn.Embedding(vocab_size + 1, self.pred_hidden, padding_idx=self.blank_idx),
+            "dec_rnn": _LSTMDropout(self.pred_hidden, self.pred_hidden, self.pred_rnn_layers, dropout,
+                                    prednet.get("forget_gate_bias", 1.0), prednet.get("t_max", None),
+                                    prednet.get("weights_init_scale", 1.0),
+                                    prednet.get("hidden_hidden_bias_scale", 0.0)),
+        })
+        self._native = {}
+        self._native_versions = {}
+        self._rnnt_export = False
+
+    def _apply(self, fn, *args, **kwargs):
+        self._native_versions = {}
+        return super()._apply(fn, *args, **kwargs)
+
+    def _lstm_tensors(self):
+        lstm = self.prediction["dec_rnn"].lstm
+        L = self.pred_rnn_layers
+        return ([getattr(lstm, f"weight_ih_l{l}") for l in range(L)], [getattr(lstm, f"weight_hh_l{l}") for l in range(L)],
+                [getattr(lstm, f"bias_ih_l{l}") for l in range(L)], [getattr(lstm, f"bias_hh_l{l}") for l in range(L)])
+
+    def native_for(self, dev: torch.device):
+        from conformer_amd.rnnt_decode import NativePredictionNet
+        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        nat = self._native.get(key)
+        if nat is None:
+            nat = NativePredictionNet(self.vocab_size, self.pred_hidden, self.pred_rnn_layers, key)
+            self._native[key] = nat
+        emb = self.prediction["embed"].weight
+        lists = self._lstm_tensors()
+        ts = [emb] + [t for ts in lists for t in ts]
+        version = tuple((t.data_ptr(), t._version) for t in ts)
+        if self._native_versions.get(key) != version:
+            nat.set_weights(emb, *lists)
+            self._native_versions[key] = version
+        return nat
+
+    @typecheck()
+    def forward(self, targets, target_length, states=None):
+        y = targets.type(torch.int64)                               # rnn.label_collate
+        g, states = self.predict(y, state=states, add_sos=not self._rnnt_export)
+        return g.transpose(1, 2), target_length, states
+
+    def predict(self, y: Optional[torch.Tensor] = None, state: Optional[List[torch.Tensor]] = None,
+                add_sos: bool = True, batch_size: Optional[int] = None):
+        """rnnt.py:190-283: (g (B, U(+1), H), [h, c] each (L, B, H))."""
+        _p = next(self.parameters())
+        if _p.device.type != "cuda":
+            raise RuntimeError("RNNTDecoder (MI355X-native) needs its parameters on a ROCm GPU")
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("the native prediction network is inference-only; use torch.no_grad() or .eval()")
+        if y is not None:
+            y = y.to(_p.device)
+            if y.numel() and (int(y.min()) < 0 or int(y.max()) > self.blank_idx):
+                raise IndexError("index out of range in self")       # nn.Embedding's error
+            B = y.shape[0]
+        else:
+            B = (1 if state is None else state[0].size(1)) if batch_size is None else batch_size
+        if state is None and self.random_state_sampling and self.training:
+            state = self.initialize_state(torch.empty(B, 1, device=_p.device))
+        h0, c0 = (None, None) if state is None else (state[0], state[1])
+        g, (h, c) = self.native_for(_p.device).predict(y, h0, c0, add_sos, B)
+        return g, [h, c]
+
+    def initialize_state(self, y: torch.Tensor) -> List[torch.Tensor]:
+        batch = y.size(0)
+        shape = (self.pred_rnn_layers, batch, self.pred_hidden)
+        if self.random_state_sampling and self.training:
+            return [torch.randn(shape, dtype=y.dtype, device=y.device), torch.randn(shape, dtype=y.dtype, device=y.device)]
+        return [torch.zeros(shape, dtype=y.dtype, device=y.device), torch.zeros(shape, dtype=y.dtype, device=y.device)]
+
+    def batch_select_state(self, batch_states: List[torch.Tensor], idx: int) -> List[List[torch.Tensor]]:
+        """rnnt.py:514-531."""
+        if batch_states is None:
+            return None
+        return [[batch_states[s][layer][idx] for layer in range(self.pred_rnn_layers)] for s in range(len(batch_states))]
+
+    def batch_copy_states(self, old_states: List[torch.Tensor], new_states: List[torch.Tensor], ids: List[int],
+                          value: Optional[float] = None) -> List[torch.Tensor]:
+        """rnnt.py:579-610."""
+        for s in range(len(old_states)):
+            if value is None:
+                old_states[s][:, ids, :] = new_states[s][:, ids, :]
+            else:
+                old_states[s][:, ids, :] *= 0.0
+                old_states[s][:, ids, :] += value
+        return old_states
+
+    def batch_concat_states(self, batch_states: List[List[torch.Tensor]]) -> List[torch.Tensor]:
+        """rnnt.py:533-555: B x ([L x (H)], [L x (H)]) -> [(L, B, H), (L, B, H)]."""
+        return [torch.stack([torch.stack(b[s]) for b in batch_states], 0).transpose(1, 0)
+                for s in range(len(batch_states[0]))]
+
+    def batch_initialize_states(self, batch_states: List[torch.Tensor], decoder_states: List[List[torch.Tensor]]):
+        """rnnt.py:485-512."""
+        return [torch.stack([torch.stack([d[s][layer] for d in decoder_states]) for layer in range(self.pred_rnn_layers)])
+                for s in range(len(decoder_states[0]))]
+
 
 
 class RNNTJoint(NeuralModule):

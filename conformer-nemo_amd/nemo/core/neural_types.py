@@ -49,3 +49,11 @@ class AudioSignal(ElementType):
 
 class MelSpectrogramType(SpectrogramType):
     pass
+
+
+class EmbeddedTextType(ElementType):
+    pass
+
+
+class HypothesisType(ElementType):
+    pass

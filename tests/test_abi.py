@@ -42,7 +42,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(rl) == set(_lib.RNNT_LOSS_SYMBOLS)
     aug = _declared_symbols("cfm_augment.h")
     assert set(aug) == set(_lib.AUGMENT_SYMBOLS)
-    for name in ctc + train + joint + stream + mel + rl + aug:
+    dec = _declared_symbols("cfm_rnnt_decode.h")
+    assert set(dec) == set(_lib.RNNT_DECODE_SYMBOLS)
+    for name in ctc + train + joint + stream + mel + rl + aug + dec:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
