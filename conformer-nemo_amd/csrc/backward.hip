@@ -51,6 +51,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   const int n = blockIdx.x * 64 + c, nc = min(n, N - 1);
   const int r0 = blockIdx.y * kColRows, r1 = min(M, r0 + kColRows);
   float s = 0.0f;
+#pragma unroll 8
   for (int r = r0 + rl; r < r1; r += 4) s += src[(long)r * ld + nc];
   red[rl][c] = s;
   __syncthreads();
@@ -62,6 +63,7 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restri
   const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int n = blockIdx.x * 16 + c, nc = min(n, N - 1);
   float s = 0.0f;
+#pragma unroll 8
   for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
   red[rl][c] = s;
   __syncthreads();

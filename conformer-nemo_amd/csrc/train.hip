@@ -71,34 +71,75 @@ unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n 
 // ---------------------------------------------------------------------------------------------
 // dst[i][j] = scale * fn(src)[transpose ? (j, i) : (i, j)] in the compute type, zero outside src.
 // fn 0 = identity, 1 = dropout(swish(.)) (the FFN hidden recomputed from its pre-activation; the
-// mask index is the source element (row * cols + col)).  32x32 LDS tiles.  Destination row
-// `ones_row` (transposed packs) is set to 1 over the source rows: appended to the x^T operand of a
-// weight-gradient GEMM it makes the GEMM also produce the bias gradient (sum of dy over rows).
+// mask index is the source element (row * cols + col)).  Destination row `ones_row` (transposed
+// packs) is set to 1 over the source rows: appended to the x^T operand of a weight-gradient GEMM it
+// makes the GEMM also produce the bias gradient (sum of dy over rows).
+// 64x64 LDS tiles; 16-byte (fp32) / 8-byte (bf16) source loads along source rows and 16-byte stores
+// along destination rows when the strides and base pointers allow (src_vec / dst_vec).
 template <typename Tin, typename Tout>
 __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src, long src_ld, int rows, int cols,
-                                                    int transpose, float scale, int fn, Drop drop,
-                                                    Tout* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad,
-                                                    int ones_row) {
-  __shared__ float tile[32][33];
-  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int k = ty; k < 32; k += 8) {
-    const int si = transpose ? j0 + k : i0 + k;
-    const int sj = transpose ? i0 + tx : j0 + tx;
-    float v = 0.0f;
-    if (si < rows && sj < cols) {
-      v = ld_f<Tin>(src + (long)si * src_ld + sj);
-      if (fn == 1) v = swishf(v) * drop_mul(drop, (uint64_t)si * cols + sj);
-      v *= scale;
+                                                      int transpose, float scale, int fn, Drop drop,
+                                                      Tout* __restrict__ dst, long dst_ld, int rows_pad,
+                                                      int cols_pad, int ones_row, int src_vec, int dst_vec) {
+  __shared__ float tile[64][65];                      // [dst row][dst col] of this block
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int sr0 = transpose ? j0 : i0, sc0 = transpose ? i0 : j0;
+  const int c4 = threadIdx.x & 15, r = threadIdx.x >> 4;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int rr = r + 16 * pass, cc = 4 * c4;
+    const int si = sr0 + rr, sj = sc0 + cc;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (si < rows) {
+      const Tin* sp = src + (long)si * src_ld + sj;
+      if (src_vec && sj + 3 < cols) {
+        if constexpr (sizeof(Tin) == 4) {
+          const float4 t = *(const float4*)sp;
+          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+          const uint2 t = *(const uint2*)sp;
+          v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+          v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (sj + e < cols) v[e] = ld_f<Tin>(sp + e);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (fn == 1 && sj + e < cols) v[e] = swishf(v[e]) * drop_mul(drop, (uint64_t)si * cols + sj + e);
+        v[e] *= scale;
+      }
     }
-    tile[k][tx] = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (transpose) tile[cc + e][rr] = v[e];
+      else tile[rr][cc + e] = v[e];
+    }
   }
   __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int di = i0 + k, dj = j0 + tx;
-    float v = transpose ? tile[tx][k] : tile[k][tx];
-    if (di == ones_row) v = dj < rows ? 1.0f : 0.0f;   // bias column of a weight-gradient GEMM
-    if (di < rows_pad && dj < cols_pad) st_f<Tout>(dst + (long)di * dst_ld + dj, v);
+  constexpr int VE = 16 / (int)sizeof(Tout);
+  constexpr int CPR = 64 / VE, RPP = 256 / CPR;
+  const int q = threadIdx.x % CPR, k0 = threadIdx.x / CPR;
+  for (int k = k0; k < 64; k += RPP) {
+    const int di = i0 + k;
+    if (di >= rows_pad) break;
+    const int dj = j0 + q * VE;
+    float o[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      o[e] = tile[k][q * VE + e];
+      if (di == ones_row) o[e] = (dj + e < rows) ? 1.0f : 0.0f;   // bias column of a weight-gradient GEMM
+    }
+    Tout* dp = dst + (long)di * dst_ld + dj;
+    if (dst_vec && dj + VE <= cols_pad) {
+      *(uint4*)dp = Vec16<Tout>::from_f32(o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VE; ++e)
+        if (dj + e < cols_pad) st_f<Tout>(dp + e, o[e]);
+    }
   }
 }
 
@@ -205,6 +246,7 @@ __global__ __launch_bounds__(256) void colred_partial_kernel(const float* __rest
   const int nc = min(n, N - 1);
   const float mu = F == 2 ? mean[nc] : 0.0f;
   float s = 0.0f;
+#pragma unroll 8
   for (int r = r0 + rl; r < r1; r += 4) {
     const float v = src[(long)r * ld + nc];
     s += F == 0 ? v : (F == 1 ? v * y[(long)r * ld + nc] : (v - mu) * (v - mu));
@@ -221,6 +263,7 @@ __global__ __launch_bounds__(256) void colred_final_kernel(const float* __restri
   const int n = blockIdx.x * 16 + c;
   const int nc = min(n, N - 1);
   float s = 0.0f;
+#pragma unroll 8
   for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
   red[rl][c] = s;
   __syncthreads();
@@ -779,16 +822,20 @@ struct Step {
   void pack(const void* src, bool src_ct, long ld, int rows, int cols, bool tr, float scale, void* dst, long dld,
             int rp, int cp, int fn = 0, Drop dr = Drop{0, 0, 1.0f}, int ones_row = -1) const {
     if (rp <= 0 || cp <= 0) return;
-    const dim3 grid((cp + 31) / 32, (rp + 31) / 32), block(256);
+    const dim3 grid((cp + 63) / 64, (rp + 63) / 64), block(256);
+    const int ses = (g.dt != DT_F32 && src_ct) ? 2 : 4;           // source element bytes
+    const int des = g.dt == DT_F32 ? 4 : 2;
+    const int sv = (ld % 4 == 0 && ((uintptr_t)src % (4 * ses)) == 0) ? 1 : 0;
+    const int dv = (dld % (16 / des) == 0 && ((uintptr_t)dst % 16) == 0) ? 1 : 0;
     if (g.dt == DT_F32) {
-      cfm_launch(tpack_kernel<float, float>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale, fn,
-                 dr, (float*)dst, dld, rp, cp, ones_row);
+      cfm_launch(tpack_kernel<float, float>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
+                 fn, dr, (float*)dst, dld, rp, cp, ones_row, sv, dv);
     } else if (src_ct) {
-      cfm_launch(tpack_kernel<bf16_t, bf16_t>, grid, block, 0, st, (const bf16_t*)src, ld, rows, cols, (int)tr, scale,
-                 fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row);
+      cfm_launch(tpack_kernel<bf16_t, bf16_t>, grid, block, 0, st, (const bf16_t*)src, ld, rows, cols, (int)tr,
+                 scale, fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row, sv, dv);
     } else {
       cfm_launch(tpack_kernel<float, bf16_t>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
-                 fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row);
+                 fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row, sv, dv);
     }
   }
   // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
