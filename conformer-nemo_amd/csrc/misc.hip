@@ -22,49 +22,67 @@ __global__ void calc_length_kernel(const int32_t* in, int32_t* out, int B, int T
 // reading the reference's (B, F, T) audio_signal directly (the (B,T,F) transpose of
 // conformer_encoder.py:248 is folded into the indexing).  Output channels-last (B, T1, F1, C).
 // One block per (b, t1); thread (x = 8-channel group, y = f1 slot); weights held in registers.
+constexpr int CONV1_ROWS = 4;   // (b, t1) rows per block: the weight registers are loaded once for all
+
 template <typename T>
 __global__ __launch_bounds__(256) void conv1_kernel(const float* __restrict__ x, int F, int Tlen, int T1, int F1,
                                                     const float* __restrict__ w9, const float* __restrict__ bias,
-                                                    int C, T* __restrict__ out) {
+                                                    int C, int BT, T* __restrict__ out) {
   __shared__ float xs[3][264];
-  const int bt = blockIdx.x;
-  const int b = bt / T1, t1 = bt - b * T1;
-  for (int i = threadIdx.y * 64 + threadIdx.x; i < 3 * F; i += 256) {
-    const int kt = i / F, f = i - kt * F;
-    const int t = 2 * t1 - 1 + kt;
-    xs[kt][f + 1] = (t >= 0 && t < Tlen) ? x[((long)b * F + f) * Tlen + t] : 0.0f;
-  }
-  if (threadIdx.y == 0 && threadIdx.x < 3) { xs[threadIdx.x][0] = 0.0f; xs[threadIdx.x][F + 1] = 0.0f; }
-  __syncthreads();
   const int c0 = (blockIdx.y * 64 + threadIdx.x) * 8;
-  if (c0 >= C) return;
+  const bool cok = c0 < C;
+  // a thread's 8 channels x 9 taps are 72 consecutive floats of the (C, 1, 3, 3) weight: 18 float4
+  // loads, kept in registers for the CONV1_ROWS (b, t1) rows of this block
   float w[8][9], bb[8];
+  if (cok) {
+    float wf[72];
+    const float4* wp = (const float4*)(w9 + (long)c0 * 9);
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    bb[c] = bias[c0 + c];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) w[c][k] = w9[(c0 + c) * 9 + k];
-  }
-  for (int f1 = threadIdx.y; f1 < F1; f1 += 4) {
-    float in[9];
-#pragma unroll
-    for (int kt = 0; kt < 3; ++kt)
-#pragma unroll
-      for (int kf = 0; kf < 3; ++kf) in[kt * 3 + kf] = xs[kt][2 * f1 + kf];   // (2f1 - 1 + kf) + 1 pad offset
-    float o[8];
+    for (int i = 0; i < 18; ++i) {
+      const float4 v = wp[i];
+      wf[4 * i] = v.x; wf[4 * i + 1] = v.y; wf[4 * i + 2] = v.z; wf[4 * i + 3] = v.w;
+    }
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      float a = 0.0f;
+      bb[c] = bias[c0 + c];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) a = fmaf(w[c][k], in[k], a);
-      o[c] = fmaxf(a + bb[c], 0.0f);
+      for (int k = 0; k < 9; ++k) w[c][k] = wf[c * 9 + k];
     }
-    T* dst = out + (((long)b * T1 + t1) * F1 + f1) * C + c0;
-    if constexpr (sizeof(T) == 2) {
-      *(uint4*)dst = Vec16<bf16_t>::from_f32(o);
-    } else {
-      *(uint4*)dst = Vec16<float>::from_f32(o);
-      *(uint4*)(dst + 4) = Vec16<float>::from_f32(o + 4);
+  }
+  for (int rr = 0; rr < CONV1_ROWS; ++rr) {
+    const int bt = blockIdx.x * CONV1_ROWS + rr;
+    if (bt >= BT) break;                       // block-uniform
+    const int b = bt / T1, t1 = bt - b * T1;
+    if (rr > 0) __syncthreads();               // previous row's reads of xs are done
+    for (int i = threadIdx.y * 64 + threadIdx.x; i < 3 * F; i += 256) {
+      const int kt = i / F, f = i - kt * F;
+      const int t = 2 * t1 - 1 + kt;
+      xs[kt][f + 1] = (t >= 0 && t < Tlen) ? x[((long)b * F + f) * Tlen + t] : 0.0f;
+    }
+    if (threadIdx.y == 0 && threadIdx.x < 3) { xs[threadIdx.x][0] = 0.0f; xs[threadIdx.x][F + 1] = 0.0f; }
+    __syncthreads();
+    if (!cok) continue;
+    for (int f1 = threadIdx.y; f1 < F1; f1 += 4) {
+      float in[9];
+#pragma unroll
+      for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+        for (int kf = 0; kf < 3; ++kf) in[kt * 3 + kf] = xs[kt][2 * f1 + kf];   // (2f1 - 1 + kf) + 1 pad offset
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) a = fmaf(w[c][k], in[k], a);
+        o[c] = fmaxf(a + bb[c], 0.0f);
+      }
+      T* dst = out + (((long)b * T1 + t1) * F1 + f1) * C + c0;
+      if constexpr (sizeof(T) == 2) {
+        *(uint4*)dst = Vec16<bf16_t>::from_f32(o);
+      } else {
+        *(uint4*)dst = Vec16<float>::from_f32(o);
+        *(uint4*)(dst + 4) = Vec16<float>::from_f32(o + 4);
+      }
     }
   }
 }
@@ -219,11 +237,12 @@ void conv1_subsample(int dtype, const float* x, int B, int F, int T, const float
                      void* out, hipStream_t st) {
   const int T1 = (T - 1) / 2 + 1, F1 = (F - 1) / 2 + 1;
   if (B <= 0 || T1 <= 0) return;
-  const dim3 grid(B * T1, (C / 8 + 63) / 64), block(64, 4);
+  const int BT = B * T1;
+  const dim3 grid((BT + CONV1_ROWS - 1) / CONV1_ROWS, (C / 8 + 63) / 64), block(64, 4);
   if (dtype == DT_F32)
-    cfm_launch(conv1_kernel<float>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (float*)out);
+    cfm_launch(conv1_kernel<float>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, BT, (float*)out);
   else
-    cfm_launch(conv1_kernel<bf16_t>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, (bf16_t*)out);
+    cfm_launch(conv1_kernel<bf16_t>, grid, block, 0, st, x, F, T, T1, F1, w9, bias, C, BT, (bf16_t*)out);
 }
 
 template <typename T>
