@@ -87,7 +87,7 @@ __device__ __forceinline__ float wave_dot4(const float* As, int K, const float* 
   if (valid) {
     // UK float4 steps of weight loads are issued before any is consumed: the loop is latency-bound,
     // so this keeps 4 * UK 16-byte loads in flight per lane.
-    constexpr int UK = 8;                 // one round for K <= 2048
+    constexpr int UK = 4;
     for (int k4 = lane; k4 < K4; k4 += 64 * UK) {
       float4 w[UK][4];
 #pragma unroll
@@ -136,18 +136,23 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(const float* __restrict_
                                                         float* __restrict__ h2, float* __restrict__ c2,
                                                         float* __restrict__ gout, long gstride, int B, int I, int H,
                                                         const int* __restrict__ run_flag) {
-  if (run_flag && *run_flag == 0) return;   // uniform: every utterance finished
   extern __shared__ float lds[];
   const int K = I + H;
   const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + wave;
+  const bool valid = j < H;
+  // loads the epilogue needs, issued before the staging so their latency overlaps it
+  const int run = run_flag ? *run_flag : 1;
+  const int jc = min(j, H - 1), bl = b0 + min(lane, nb - 1);
+  const float cprev = c[(long)bl * H + jc];
+  const float bs0 = bias[jc], bs1 = bias[H + jc], bs2 = bias[2 * H + jc], bs3 = bias[3 * H + jc];
   float* As = lds;
   float* red = lds + RB * K;
   float* gsum = red + RED;               // [4 waves][4 * RB] gate totals
   stage_rows(As, K, I, H, b0, nb, xsrc, xlab, emb, nemb, h);
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + wave;
-  const bool valid = j < H;
+  if (run == 0) return;                  // uniform: every utterance finished, nothing written yet
   const float* wr[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) wr[g] = valid ? W + (long)(g * H + j) * K : nullptr;
@@ -161,11 +166,11 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(const float* __restrict_
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (!valid || lane >= nb) return;
   const long b = b0 + lane;
-  const float gi = sigm(gs[0 * RB + lane] + bias[0 * H + j]);
-  const float gf = sigm(gs[1 * RB + lane] + bias[1 * H + j]);
-  const float gg = tanhf(gs[2 * RB + lane] + bias[2 * H + j]);
-  const float go = sigm(gs[3 * RB + lane] + bias[3 * H + j]);
-  const float cn = gf * c[b * H + j] + gi * gg;
+  const float gi = sigm(gs[0 * RB + lane] + bs0);
+  const float gf = sigm(gs[1 * RB + lane] + bs1);
+  const float gg = tanhf(gs[2 * RB + lane] + bs2);
+  const float go = sigm(gs[3 * RB + lane] + bs3);
+  const float cn = gf * cprev + gi * gg;
   const float hn = go * tanhf(cn);
   c2[b * H + j] = cn;
   h2[b * H + j] = hn;
@@ -178,15 +183,22 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
                                                            const int32_t* __restrict__ tptr, int T, int B, int H,
                                                            int J, int act, float* __restrict__ hid,
                                                            const int* __restrict__ run_flag) {
-  if (run_flag && *run_flag == 0) return;
   extern __shared__ float lds[];
   const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n0 = blockIdx.x * 16 + wave * 4;
+  // the epilogue's operands (this lane's (row, column) after the transpose), fetched up front
+  const int run = run_flag ? *run_flag : 1;
+  const int ec = (lane % (4 * RB)) / RB, er = lane % RB;
+  const int en = min(n0 + ec, J - 1);
+  const long eb = b0 + min(er, nb - 1);
+  const int et = min(max(tptr[eb], 0), T - 1);
+  const float fe = F[(eb * T + et) * J + en] + bp[en];
   float* As = lds;
   float* red = lds + RB * H;
   stage_rows(As, H, H, 0, b0, nb, h, nullptr, nullptr, 1, nullptr);
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n0 = blockIdx.x * 16 + wave * 4;
+  if (run == 0) return;
   const float* wr[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) wr[c] = (n0 + c < J) ? Wp + (long)(n0 + c) * H : nullptr;
@@ -194,9 +206,7 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
   if (lane >= 4 * RB) return;
   const int c = lane / RB, r = lane % RB, n = n0 + c;
   if (r >= nb || n >= J) return;
-  const long b = b0 + r;
-  const int t = min(max(tptr[b], 0), T - 1);
-  hid[b * J + n] = act_fn(act, s + bp[n] + F[(b * T + t) * J + n]);
+  hid[(b0 + r) * (long)J + n] = act_fn(act, s + fe);
 }
 
 struct Part {
@@ -209,16 +219,18 @@ struct Part {
 __global__ __launch_bounds__(256) void joint_logits_kernel(const float* __restrict__ Wo, const float* __restrict__ bo,
                                                            const float* __restrict__ hid, int B, int J, int N,
                                                            Part* __restrict__ part, const int* __restrict__ run_flag) {
-  if (run_flag && *run_flag == 0) return;
   extern __shared__ float lds[];
   const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n0 = blockIdx.x * 16 + wave * 4;
+  const int run = run_flag ? *run_flag : 1;
+  const float be = bo[min(n0 + (lane % (4 * RB)) / RB, N - 1)];
   float* As = lds;
   float* red = lds + RB * J;
   float* zs = red + RED;                 // [16][RB]
   stage_rows(As, J, J, 0, b0, nb, hid, nullptr, nullptr, 1, nullptr);
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n0 = blockIdx.x * 16 + wave * 4;
+  if (run == 0) return;
   const float* wr[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) wr[c] = (n0 + c < N) ? Wo + (long)(n0 + c) * J : nullptr;
@@ -226,7 +238,7 @@ __global__ __launch_bounds__(256) void joint_logits_kernel(const float* __restri
   if (lane < 4 * RB) {
     const int c = lane / RB, r = lane % RB;
     const int n = n0 + c;
-    zs[(wave * 4 + c) * RB + r] = (n < N) ? s + bo[n] : -INFINITY;
+    zs[(wave * 4 + c) * RB + r] = (n < N) ? s + be : -INFINITY;
   }
   __syncthreads();
   if (threadIdx.x >= nb) return;
