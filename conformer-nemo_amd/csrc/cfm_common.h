@@ -95,3 +95,15 @@ CFM_DEV void glds16(const void* gsrc, void* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
+
+namespace cfm {
+// 16-byte store with the sc1 (write-through) cache policy, through a raw buffer descriptor built
+// from the wave-uniform tensor base: the line goes to memory as it is written, so the kernel leaves
+// no dirty L2 lines for the launch boundary to write back (MI355X_MICROARCH.md, boundary row).
+CFM_DEV void store16_wt(const void* base, long byte_off, uint4 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0x7fffffff, 0x00020000);
+  u32x4 d = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)byte_off, 0, 16);
+}
+}  // namespace cfm

@@ -68,6 +68,7 @@ struct GemmEpi {
   const float* uv;     // EPI_QKV: pos_bias_u then pos_bias_v, each [H][dkp] zero-padded
   float qscale;        // EPI_QKV: (q + u), (q + v) are written pre-multiplied by log2(e) / sqrt(dk)
   int out_scalar;      // EPI_SCALE_F32: element stores (fp32 rows whose stride is not a multiple of 4)
+  int wt;              // set by gemm(): 16-byte output stores write-through (sc1), see store16_wt
 };
 
 struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)

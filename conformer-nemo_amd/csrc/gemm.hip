@@ -20,6 +20,7 @@
 //   * Blocks are remapped so that each XCD owns a contiguous range of tiles (A panels stay in one L2).
 // Epilogue: the fp32 accumulators are staged through LDS and written back row-major with 16-byte
 // vector accesses (bias, activation, GLU, residual read-modify-write all vectorised).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -215,7 +216,10 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           if (n + 3 < p.N) xr[3] = o.w;
         }
       } else if (colok && m < p.M) {
-        *(float4*)(e.X + xoff + (long)m * e.ldx + n) = o;
+        const long off = xoff + (long)m * e.ldx + n;
+        if (e.wt) store16_wt(e.X, off * 4, make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                                      __float_as_uint(o.w)));
+        else *(float4*)(e.X + off) = o;
       }
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
@@ -248,7 +252,8 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       if (m >= p.M || c >= p.N) continue;
       T* dst = (T*)e.C + (long)m * e.ldc + c;
       if (c + VE <= p.N) {
-        *(uint4*)dst = Vec16<T>::from_f32(o);
+        if (e.wt) store16_wt(e.C, ((long)m * e.ldc + c) * (long)sizeof(T), Vec16<T>::from_f32(o));
+        else *(uint4*)dst = Vec16<T>::from_f32(o);
       } else {
         for (int i = 0; i < VE && c + i < p.N; ++i) st_f<T>(dst + i, o[i]);
       }
@@ -293,8 +298,15 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           float ou[VE], ov[VE];
 #pragma unroll
           for (int i = 0; i < VE; ++i) { ou[i] = (o[i] + ub[i]) * e.qscale; ov[i] = (o[i] + vb[i]) * e.qscale; }
-          *(uint4*)(row + n) = Vec16<T>::from_f32(ou);
-          *(uint4*)(row + hq + n) = Vec16<T>::from_f32(ov);
+          if (e.wt) {
+            store16_wt(e.C, ((long)m * e.ldc + n) * (long)sizeof(T), Vec16<T>::from_f32(ou));
+            store16_wt(e.C, ((long)m * e.ldc + hq + n) * (long)sizeof(T), Vec16<T>::from_f32(ov));
+          } else {
+            *(uint4*)(row + n) = Vec16<T>::from_f32(ou);
+            *(uint4*)(row + hq + n) = Vec16<T>::from_f32(ov);
+          }
+        } else if (e.wt) {
+          store16_wt(e.C, ((long)m * e.ldc + hq + n) * (long)sizeof(T), Vec16<T>::from_f32(o));
         } else {
           *(uint4*)(row + hq + n) = Vec16<T>::from_f32(o);
         }
@@ -302,7 +314,8 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       }
       T* dst = (T*)e.C + (long)m * e.ldc + n;
       if (vec) {
-        *(uint4*)dst = Vec16<T>::from_f32(o);
+        if (e.wt) store16_wt(e.C, ((long)m * e.ldc + n) * (long)sizeof(T), Vec16<T>::from_f32(o));
+        else *(uint4*)dst = Vec16<T>::from_f32(o);
       } else {
         for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
       }
@@ -516,6 +529,8 @@ int packed_width(const GemmEpi& epi, int N) {
 }
 
 int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
+// write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
+int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 
 // Tile ids (CFM_GEMM_TILE / set_gemm_tile_override):
 //   0 128x128 NS2 | 1 256x128 NS3 | 5 64x128 NS2          (128-byte K-steps, several blocks / CU)
@@ -576,6 +591,9 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
   p.M = M;
   p.N = N;
   p.epi = epi;
+  // buffer-descriptor offsets are 31-bit: write-through only for outputs below 2 GiB
+  const long out_bytes = std::max((long)M * epi.ldc * es, (long)M * epi.ldx * 4);
+  p.epi.wt = (g_gemm_wt && out_bytes < 0x7fffffffL) ? 1 : 0;
   return p;
 }
 
@@ -630,6 +648,7 @@ void gemm_splitk(int dtype, const void* A, long lda, int M, int K, const void* W
   GemmParams p = make_params(es, M, Wp, (int)ldw, N, epi);
   p.kb = kchunk * es;
   p.split_x = split_x;
+  if ((long)S * split_x * 4 + (long)M * epi.ldx * 4 >= 0x7fffffffL) p.epi.wt = 0;
   g_splits = S;
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
   int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
