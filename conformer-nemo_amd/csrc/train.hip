@@ -143,6 +143,30 @@ __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src,
   }
 }
 
+// dst[i] = i < N && src ? src[i] : 0 for i < npad (GEMM bias arrays, zero-padded to the N granule)
+__global__ __launch_bounds__(256) void bias_pad_kernel(const float* __restrict__ src, int N, float* __restrict__ dst,
+                                                       int npad) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < npad) dst[i] = (src && i < N) ? src[i] : 0.0f;
+}
+
+// Up to 8 independent device copies in one launch (grid.y = copy index): the per-layer gradient
+// scatters that would otherwise each cost a runtime copy kernel.
+struct CopyList {
+  const float* src[8];
+  float* dst[8];
+  long n[8];
+  int count;
+};
+__global__ __launch_bounds__(256) void copy_multi_kernel(CopyList l) {
+  const int c = blockIdx.y;
+  if (c >= l.count || l.dst[c] == nullptr) return;
+  const float* s = l.src[c];
+  float* d = l.dst[c];
+  const long n = l.n[c];
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) d[i] = s[i];
+}
+
 // Head-padded row gather: dst row n = (part, head, dd) of `parts` stacked (H*dk, K) fp32 sources,
 // head dims padded dk -> dkp (the layout the QKV epilogue and attention kernels consume); K = 1
 // packs bias vectors (fp32 out).
@@ -845,9 +869,11 @@ struct Step {
   void packWt(const float* w, int N, int K, void* dst) const {
     pack(w, false, K, N, K, true, 1.0f, dst, kpad(N), npad(K), kpad(N));
   }
+  // GEMM bias: N floats zero-padded to the N granule, one small launch (a memset + copy pair costs
+  // two runtime copy kernels)
   void bias(const float* b, int N, float* dst) const {
-    HIP_OK(hipMemsetAsync(dst, 0, (size_t)npad(N) * 4, st));
-    if (b) HIP_OK(hipMemcpyAsync(dst, b, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    const int np = npad(N);
+    cfm_launch(bias_pad_kernel, dim3((np + 255) / 256), dim3(256), 0, st, b, N, dst, np);
   }
   void heads(const float* s0, const float* s1, const float* s2, int parts, int K, void* dst, bool f32, long Kp,
              int rows_pad) const {
@@ -1232,8 +1258,13 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       float* sy = S.W_<float>(S.wl.sync);
       colred(dZ, nullptr, nullptr, d, M, d, 0, 1.0f, sy, 0, red, st);
       colred(dZ, xhat, nullptr, d, M, d, 1, 1.0f, sy + d, 0, red, st);
-      if (Gp(q.bn_b)) HIP_OK(hipMemcpyAsync(Gp(q.bn_b), sy, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
-      if (Gp(q.bn_w)) HIP_OK(hipMemcpyAsync(Gp(q.bn_w), sy + d, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+      {
+        CopyList cl{};
+        cl.src[0] = sy; cl.dst[0] = Gp(q.bn_b); cl.n[0] = d;
+        cl.src[1] = sy + d; cl.dst[1] = Gp(q.bn_w); cl.n[1] = d;
+        cl.count = 2;
+        cfm_launch(copy_multi_kernel, dim3(ew_grid(d), 2), dim3(256), 0, st, cl);
+      }
       S.sync(sy, 2L * d);
       float* dD = dS;   // dS is dead after dZ
       cfm_launch(bn_bwd_apply_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dZ, xhat, S.prm(q.bn_w),
@@ -1289,13 +1320,17 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
           S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, d);
           float* tmp = S.W_<float>(S.wl.gtmp);   // (3d, d) stacked weight gradient, then the (3d) biases
           S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, tmp + 3L * d * d);
+          CopyList cl{};
           for (int p = 0; p < 3; ++p) {
-            if (Gp(wi[p]))
-              HIP_OK(hipMemcpyAsync(Gp(wi[p]), tmp + (long)p * d * d, (size_t)d * d * 4, hipMemcpyDeviceToDevice, st));
-            if (Gp(bi3[p]))
-              HIP_OK(hipMemcpyAsync(Gp(bi3[p]), tmp + 3L * d * d + (long)p * d, (size_t)d * 4, hipMemcpyDeviceToDevice,
-                                    st));
+            cl.src[2 * p] = tmp + (long)p * d * d;
+            cl.dst[2 * p] = Gp(wi[p]);
+            cl.n[2 * p] = (long)d * d;
+            cl.src[2 * p + 1] = tmp + 3L * d * d + (long)p * d;
+            cl.dst[2 * p + 1] = Gp(bi3[p]);
+            cl.n[2 * p + 1] = d;
           }
+          cl.count = 6;
+          cfm_launch(copy_multi_kernel, dim3(ew_grid((long)d * d), 6), dim3(256), 0, st, cl);
         }
         ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true);   // gB = d x1
       }
