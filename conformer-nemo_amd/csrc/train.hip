@@ -721,9 +721,14 @@ Tape tape_layout(const cfm_encoder* h, const Geo& g) {
 }
 
 // split-K factor of a weight-gradient GEMM (N x K outputs, reduction over `rows`)
+// Tile of a weight-gradient GEMM: 256x256 (tile 11, 3x the arithmetic intensity of 64x128) for the
+// very long contractions (the conv2 weight gradient over 160 000 im2col rows), 64x128 (the shape
+// picker's choice) otherwise.  The split count targets a few tiles per CU for either.
+int wgrad_tile(int N, int K, long rows) { return (rows >= 32768 && N >= 256 && K >= 256) ? 11 : -1; }
 int wgrad_splits(int N, int K, long rows) {
-  const long tiles = (long)((N + 63) / 64) * ((K + 127) / 128);
-  long s = (768 + tiles - 1) / tiles;
+  const bool big = wgrad_tile(N, K, rows) == 11;
+  const long tiles = big ? (long)((N + 255) / 256) * ((K + 255) / 256) : (long)((N + 63) / 64) * ((K + 127) / 128);
+  long s = ((big ? 512 : 768) + tiles - 1) / tiles;
   s = std::min<long>(s, std::max<long>(1, rows / 256));
   return (int)std::max<long>(1, std::min<long>(s, 16));
 }
@@ -915,6 +920,11 @@ struct Step {
   void wgrad(const void* At, const void* Bt, long ldm, int N, int K, long rows, float* out, float* bias) const {
     const int Kb = bias ? K + 4 : K;
     const int S = wgrad_splits(N, Kb, rows);
+    struct TileScope {   // the wgrad tile for this call only
+      int prev = -2;
+      explicit TileScope(int t) { if (t >= 0) prev = set_gemm_tile_override(t); }
+      ~TileScope() { if (prev != -2) set_gemm_tile_override(prev); }
+    } tile_scope(wgrad_tile(N, Kb, rows));
     const int chunk = (int)round_up((rows + S - 1) / S, g.kg);
     GemmEpi e = epi(EPI_SCALE_F32, nullptr);
     e.ldx = Kb;
