@@ -228,7 +228,8 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from conformer_oracle import encoder_flops
         total_flop = encoder_flops(B, T, d, L)
-        cpu = cpu_baseline(enc, B, T, args.cpu_budget) if args.cpu_budget > 0 else None
+        # the CPU baseline is a rank-0, N=1 measurement (a multi-GPU job reports the GPU lines only)
+        cpu = cpu_baseline(enc, B, T, args.cpu_budget) if (args.cpu_budget > 0 and world == 1) else None
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
