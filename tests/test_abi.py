@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 import conformer_oracle as O
 from conftest import ROOT
@@ -79,3 +80,23 @@ def test_bad_config_rejected():
     assert lib.cfm_encoder_create(ctypes.byref(cfg), 0, 1, ctypes.byref(h)) == 1
     cfg = make_cfg(80, 2, 64, n_heads=4, subsampling_factor=8)
     assert lib.cfm_encoder_create(ctypes.byref(cfg), 0, 1, ctypes.byref(h)) == 2
+
+
+def test_c_consumer(tmp_path):
+    """The headers compile as plain C99 (-pedantic) and a C program links libcfm.so and gets status
+    codes and messages back on the host (tests/c/abi_smoke.c): the boundary needs no C++ or torch."""
+    import shutil
+    import subprocess
+    from conformer_amd import _lib
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("gcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    exe = str(tmp_path / "abi_smoke")
+    subprocess.run([gcc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c", "abi_smoke.c"), "-L", libdir, "-lcfm", f"-Wl,-rpath,{libdir}",
+                    "-o", exe], check=True, capture_output=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("ok:") == 5
