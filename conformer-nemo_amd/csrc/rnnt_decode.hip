@@ -87,7 +87,7 @@ __device__ __forceinline__ float wave_dot4(const float* As, int K, const float* 
   if (valid) {
     // UK float4 steps of weight loads are issued before any is consumed: the loop is latency-bound,
     // so this keeps 4 * UK 16-byte loads in flight per lane.
-    constexpr int UK = 4;
+    constexpr int UK = 2;
     for (int k4 = lane; k4 < K4; k4 += 64 * UK) {
       float4 w[UK][4];
 #pragma unroll
