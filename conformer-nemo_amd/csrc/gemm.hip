@@ -321,21 +321,54 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       }
     }
     if constexpr (EPI == EPI_QKV) {
-      // V columns -> Vt[(b*H + h)][dd][t]: lanes walk rows (time) so stores are contiguous in t
+      // V columns -> Vt[(b*H + h)][dd][t] as 16-byte runs of G consecutive frames ("octets" for bf16):
+      // a thread takes (octet, column) jobs, consecutive threads consecutive columns (conflict-free
+      // image reads).  An octet whose frames (< Tp) all lie in this tile is one vector store (frames
+      // >= Tp are Vt padding and get 0); one cut by the tile edge stores only this tile's frames.
       if (n0 + TL::BN > e.qk_cols) {
+        constexpr int G = 16 / (int)sizeof(T);
         const int c_lo = (e.qk_cols > n0 ? e.qk_cols - n0 : 0);
-        constexpr int CPP = TL::NT / TL::BM;         // columns per pass
-        const int r = tid % TL::BM;
-        const int m = m0 + r;
-        const int mc = min(m, p.M - 1);
-        const int b = mc / e.Tp, t = mc - b * e.Tp;
-        for (int cl = c_lo + tid / TL::BM; cl < TL::BN; cl += CPP) {
-          const int nn = n0 + cl;
-          const float v = img[r * TL::EPS + cl];
-          if (m >= p.M || nn >= p.N) continue;
-          const int nv = nn - e.qk_cols;
-          const int h = nv / e.dkp, dd = nv - h * e.dkp;
-          st_f<T>((T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t, v);
+        const int ncols = min(TL::BN, p.N - n0) - c_lo;
+        const int mlast = min(m0 + TL::BM, p.M) - 1;
+        if (ncols > 0 && mlast >= m0) {
+          const int Tp = e.Tp;
+          const int ba = m0 / Tp, bb = mlast / Tp;
+          auto tlo = [&](int b) { return max(m0 - b * Tp, 0); };
+          auto thi = [&](int b) { return min(mlast - b * Tp, Tp - 1); };
+          int noct = 0;
+          for (int b = ba; b <= bb; ++b) noct += thi(b) / G - tlo(b) / G + 1;
+          for (int j = tid; j < noct * ncols; j += TL::NT) {
+            const int cl = c_lo + j % ncols;
+            int oi = j / ncols, b = ba;
+            for (;; ++b) {                             // the utterance this octet belongs to
+              const int n_b = thi(b) / G - tlo(b) / G + 1;
+              if (oi < n_b) break;
+              oi -= n_b;
+            }
+            const int t0 = (tlo(b) / G + oi) * G;
+            const int nv = n0 + cl - e.qk_cols;
+            const int h = nv / e.dkp, dd = nv - h * e.dkp;
+            float v[G];
+            bool full = true;
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+              const int t = t0 + q;
+              const int r = b * Tp + t - m0;
+              const bool own = t < Tp && r >= 0 && b * Tp + t <= mlast;
+              if (t < Tp && !own) full = false;
+              v[q] = own ? img[r * TL::EPS + cl] : 0.0f;
+            }
+            T* dst = (T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t0;
+            if (full) {
+              *(uint4*)dst = Vec16<T>::from_f32(v);
+            } else {
+#pragma unroll
+              for (int q = 0; q < G; ++q) {
+                const int t = t0 + q, r = b * Tp + t - m0;
+                if (t < Tp && r >= 0 && b * Tp + t <= mlast) st_f<T>(dst + q, v[q]);
+              }
+            }
+          }
         }
       }
     }
