@@ -95,7 +95,14 @@ def cpu_baseline(enc, B, T, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": round(frames / dt, 1), "unit": "audio-frames/s", "cores": int(cores), "kind": "port",
+            "cpu_model": cpu_model,
             "sample": f"oracle/conformer_oracle.py numpy fp32, Large-17, {runs} x (B=1, T={T}) utterances, {dt:.1f} s"}
 
 
