@@ -16,6 +16,7 @@
 // Masked scores get zero gradient: the reference fills them with -10000 before the softmax and
 // zeroes their probabilities after it (:106-107), so both paths into them carry no gradient.
 #include <cmath>
+#include <cstdlib>
 #include <initializer_list>
 #include <type_traits>
 
@@ -132,38 +133,54 @@ __global__ __launch_bounds__(256) void bgemm2_kernel(BgArgs a) {
   const bool a_kc = a.ak == 1, b_kc = a.bk == 1;
   const int KZ = a.Ktot ? min(a.K, a.Ktot - z2 * a.K) : a.K;
   float ra[16], rb[16];
-  // quad q of this thread: kc -> row r = idx >> 4, k = 4 * (idx & 15); else k = idx >> 4, row = 4 * (idx & 15)
+  // Each thread moves four runs of 4 consecutive k values per operand and K-step, and writes each
+  // run to LDS as one 4-element vector.  k-contiguous operand: run q is row idx >> 4, k = 4 (idx & 15)
+  // (idx = 256 q + tid).  Otherwise the thread loads a 4x4 micro-block -- 4 k rows of 4 consecutive
+  // operand rows r = 4 (tid & 15) .. +3 at k = 4 (tid >> 4) .. +3 -- and transposes it in registers:
+  // v[4 kk + e] holds (r + e, k + kk).
   auto loadop = [&](auto* P, long sr, long sk, bool kc, int r0, int R, int k0, float* v) {
+    using TS = typename std::remove_cv<typename std::remove_pointer<decltype(P)>::type>::type;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int idx = q * 256 + tid;
-      const int hi = idx >> 4, lo = 4 * (idx & 15);
-      const int r = r0 + (kc ? hi : lo), k = k0 + (kc ? lo : hi);
       float* o = v + 4 * q;
-      if (kc ? (r < R && k + 3 < KZ) : (k < KZ && r + 3 < R)) {
-        Quad<typename std::remove_cv<typename std::remove_pointer<decltype(P)>::type>::type>::ld(P + r * sr + k * sk, o);
-      } else {
+      if (kc) {
+        const int idx = q * 256 + tid;
+        const int r = r0 + (idx >> 4), k = k0 + 4 * (idx & 15);
+        if (r < R && k + 3 < KZ) {
+          Quad<TS>::ld(P + r * sr + k, o);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rr = kc ? r : r + e, kk = kc ? k + e : k;
-          o[e] = (rr < R && kk < KZ) ? ld_f(P + rr * sr + kk * sk) : 0.0f;
+          for (int e = 0; e < 4; ++e) o[e] = (r < R && k + e < KZ) ? ld_f(P + r * sr + (k + e)) : 0.0f;
+        }
+      } else {
+        const int r = r0 + 4 * (tid & 15), k = k0 + 4 * (tid >> 4) + q;
+        if (k < KZ && r + 3 < R) {
+          Quad<TS>::ld(P + r + k * sk, o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (r + e < R && k < KZ) ? ld_f(P + (r + e) + k * sk) : 0.0f;
         }
       }
     }
   };
+  auto put4 = [&](char* p, float x0, float x1, float x2, float x3) {
+    if constexpr (sizeof(T) == 2) {
+      *(uint2*)p = make_uint2((uint32_t)f2bf(x0) | ((uint32_t)f2bf(x1) << 16), (uint32_t)f2bf(x2) | ((uint32_t)f2bf(x3) << 16));
+    } else {
+      *(float4*)p = make_float4(x0, x1, x2, x3);
+    }
+  };
   auto store = [&](char* S, bool kc, const float* v) {
+    if (kc) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = q * 256 + tid;
-      const int hi = idx >> 4, lo = 4 * (idx & 15);
-      if (kc) {
-        T* d = (T*)(S + hi * RB) + lo;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) st_f<T>(d + e, v[4 * q + e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) st_f<T>((T*)(S + (lo + e) * RB) + hi, v[4 * q + e]);
+      for (int q = 0; q < 4; ++q) {
+        const int idx = q * 256 + tid;
+        put4(S + (idx >> 4) * RB + 4 * (idx & 15) * (int)sizeof(T), v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
       }
+    } else {
+      const int r = 4 * (tid & 15), k = 4 * (tid >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) put4(S + (r + e) * RB + k * (int)sizeof(T), v[e], v[4 + e], v[8 + e], v[12 + e]);
     }
   };
   f32x16 acc = {};
@@ -306,6 +323,186 @@ __global__ __launch_bounds__(256) void attn_dscore_kernel(const float* __restric
   for (int j = lane; j < Tp; j += 64) dp[j] = p[j] * (dp[j] - D);
 }
 
+// Row reduction over one block's 32 query rows for values held in 32x32 accumulator layout
+// (v[e] belongs to row acc_row(e, lane)): the 32 lanes of a half-wave, then the waves through LDS
+// in a fixed order.  Every lane returns the block-wide value of its 16 rows.
+template <bool MAX>
+CFM_DEV void block_rows(float (&v)[16], float* red, float* fin, int w, int nw, int lane) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+      const float t = __shfl_xor(v[e], o, 64);
+      v[e] = MAX ? fmaxf(v[e], t) : v[e] + t;
+    }
+  }
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[w * 32 + acc_row(e, lane)] = v[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float a = red[threadIdx.x];
+    for (int ww = 1; ww < nw; ++ww) a = MAX ? fmaxf(a, red[ww * 32 + threadIdx.x]) : a + red[ww * 32 + threadIdx.x];
+    fin[threadIdx.x] = a;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 16; ++e) v[e] = fin[acc_row(e, lane)];
+}
+
+// Fused producer of the bf16 attention backward (T' <= 512, dk % 16 == 0): the S and BD GEMMs,
+// rel_shift + mask + softmax, the dP GEMM and dS = P (dP - rowsum(P dP)) for 32 query rows of one
+// (b, h) per block, never materialising the fp32 score images.  Wave w owns keys [64w, 64w + 64)
+// as two 32x32 MFMA tiles held in registers; its BD window (32 rows x 96 positions) goes through a
+// wave-private LDS image that is read skewed (bd[i][j] = BD[i][T'-1-i+j], as the forward kernel).
+// MFMA operands are 16-byte fragment loads straight from the (L2-resident) qk / pos rows; V
+// fragments are gathered from the V^T image.  Writes P and dS ([b][h][i][j], row pitch sld) and the
+// skewed G ([h][b][i][r], all r < gld written) in bf16, the operand type of the consumer GEMMs.
+template <int NS>
+__global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
+    const bf16_t* __restrict__ qk, long ldqk, const bf16_t* __restrict__ Vt, int vt_rows, int Tpad,
+    const bf16_t* __restrict__ pos, long ldp, const float* __restrict__ dctx, long ld_dctx,
+    const int32_t* __restrict__ lens, int B, int Tp, int H, int dkp, int cl, int cr, bf16_t* __restrict__ Pg,
+    bf16_t* __restrict__ dSg, long sld, bf16_t* __restrict__ G, long gld) {
+  constexpr int BDP = 97;                       // row pitch (floats) of a wave's BD image
+  extern __shared__ float bd_all[];             // [nw][32][BDP]
+  __shared__ float red[8 * 32], fin[32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nq = (Tp + 31) / 32;
+  int blk = blockIdx.x;
+  const int nb = gridDim.x;
+  if ((nb & 7) == 0) blk = (blk & 7) * (nb >> 3) + (blk >> 3);   // the query tiles of one (b, h) share an XCD
+  const int bh = blk / nq, i0 = (blk - bh * nq) * 32, b = bh / H, h = bh - b * H;
+  const int len = lens ? min(lens[b], Tp) : Tp;
+  const int l32 = lane & 31, kh = 8 * (lane >> 5);
+  const long rowq = (long)b * Tp + min(i0 + l32, Tp - 1);
+  uint4 aqu[NS], aqv[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    aqu[s] = *(const uint4*)(qk + rowq * ldqk + h * dkp + 16 * s + kh);
+    aqv[s] = *(const uint4*)(qk + rowq * ldqk + (long)H * dkp + h * dkp + 16 * s + kh);
+  }
+  f32x16 sc[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = min(64 * w + 32 * c + l32, Tp - 1);
+    const bf16_t* kp = qk + ((long)b * Tp + j) * ldqk + 2L * H * dkp + h * dkp + kh;
+    sc[c] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mfma_slab<bf16_t>(sc[c], aqu[s], *(const uint4*)(kp + 16 * s));
+  }
+  // BD for positions rbase .. rbase + 95 (every position a row of this wave's keys can touch)
+  float* bw = bd_all + w * 32 * BDP;
+  const int rbase = Tp - 1 - (i0 + 31) + 64 * w;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int r = min(max(rbase + 32 * t + l32, 0), 2 * Tp - 2);
+    const bf16_t* pp = pos + (long)r * ldp + h * dkp + kh;
+    f32x16 a = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mfma_slab<bf16_t>(a, aqv[s], *(const uint4*)(pp + 16 * s));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bw[acc_row(e, lane) * BDP + 32 * t + l32] = a[e];
+  }
+  // dctx fragments (fp32 -> bf16) and the dP tiles are independent of the softmax: issue them first
+  uint4 adc[NS];
+  {
+    const float* dr = dctx + rowq * ld_dctx + h * dkp + kh;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float4 x0 = *(const float4*)(dr + 16 * s), x1 = *(const float4*)(dr + 16 * s + 4);
+      const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      adc[s] = Vec16<bf16_t>::from_f32(f);
+    }
+  }
+  f32x16 dp[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = min(64 * w + 32 * c + l32, Tpad - 1);
+    const bf16_t* vp = Vt + (long)bh * vt_rows * Tpad + j;
+    dp[c] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint32_t u[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        u[e] = (uint32_t)vp[(long)(16 * s + kh + 2 * e) * Tpad] | ((uint32_t)vp[(long)(16 * s + kh + 2 * e + 1) * Tpad] << 16);
+      mfma_slab<bf16_t>(dp[c], adc[s], make_uint4(u[0], u[1], u[2], u[3]));
+    }
+  }
+  __syncthreads();
+  // logits (log2 units) with the rel_shift, pad and context-window mask
+  float m[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = acc_row(e, lane), i = i0 + row;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int j = 64 * w + 32 * c + l32;
+      const float v = sc[c][e] + bw[row * BDP + 31 - row + 32 * c + l32];
+      const bool ok = key_valid(i, j, len, cl, cr);
+      sc[c][e] = ok ? v : -INFINITY;
+      if (!ok) dp[c][e] = 0.0f;   // V^T columns past T' may hold anything: keep them out of rowsum(P dP)
+    }
+    m[e] = fmaxf(sc[0][e], sc[1][e]);
+  }
+  block_rows<true>(m, red, fin, w, nw, lane);
+  float sum[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    sum[e] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float p = sc[c][e] == -INFINITY ? 0.0f : exp2f(sc[c][e] - m[e]);
+      sc[c][e] = p;
+      sum[e] += p;
+    }
+  }
+  block_rows<false>(sum, red, fin, w, nw, lane);
+  float D[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float inv = sum[e] > 0.0f ? 1.0f / sum[e] : 0.0f;
+    D[e] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      sc[c][e] *= inv;
+      D[e] += sc[c][e] * dp[c][e];
+    }
+  }
+  block_rows<false>(D, red, fin, w, nw, lane);
+  const long img = (long)bh * Tp * sld;
+  bf16_t* Gb = G + ((long)h * B + b) * Tp * gld;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int i = i0 + acc_row(e, lane);
+    if (i >= Tp) continue;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int j = 64 * w + 32 * c + l32;
+      const float ds = sc[c][e] * (dp[c][e] - D[e]);
+      if (j < Tp) {
+        Pg[img + (long)i * sld + j] = f2bf(sc[c][e]);
+        dSg[img + (long)i * sld + j] = f2bf(ds);
+      }
+      const int r = Tp - 1 - i + j;
+      if (r < gld) Gb[(long)i * gld + r] = f2bf(j < Tp ? ds : 0.0f);
+    }
+  }
+  // G positions no key of this block reaches: [0, T'-1-i) and [T'-1-i + 64 nw, gld)
+  const int span = 64 * nw;
+  for (int idx = threadIdx.x; idx < 32 * (int)gld; idx += blockDim.x) {
+    const int il = idx / (int)gld, r = idx - il * (int)gld, i = i0 + il;
+    if (i < Tp && (r < Tp - 1 - i || r >= Tp - 1 - i + span)) Gb[(long)i * gld + r] = 0;
+  }
+}
+
+bool attn_bwd_fused_enabled() {
+  static const int on = [] { const char* e = getenv("CFM_ATTN_BWD_FUSED"); return e ? atoi(e) : 1; }();
+  return on != 0;
+}
+
 // dst[r][c] = sum_s part[s][r][c] (fixed order), part rows of `cols` floats
 __global__ void slab_rows_kernel(const float* __restrict__ part, int S, long rows, int cols, float* __restrict__ dst,
                                  long ldd) {
@@ -371,8 +568,34 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
   auto setC = [](BgArgs& a, float* p, long cm, long cn, long cz1, long cz2) { a.C = p; a.cm = cm; a.cn = cn; a.cz1 = cz1; a.cz2 = cz2; };
   const int Z = B * H;
   (void)es;
+  // bf16: one fused launch produces P, dS and G (bf16) for the consumer GEMMs below
+  const bool fused = dt == DT_BF16 && Tp <= 512 && dk % 16 == 0 && dk <= 128 && dkp == dk && ld_dctx % 4 == 0 &&
+                     ((uintptr_t)dctx % 16) == 0 && attn_bwd_fused_enabled();
+  const int opS = fused ? OP_CT : OP_F32;    // storage of the P / dS / G images
+  if (fused) {
+    const int nw = (Tp + 63) / 64, nq = (Tp + 31) / 32;
+    const size_t lds = (size_t)nw * 32 * 97 * sizeof(float);
+    const dim3 grid((unsigned)(nq * Z)), block(64 * nw);
+    const bf16_t* q16 = (const bf16_t*)qk;
+    bf16_t *P16 = (bf16_t*)S, *dS16 = (bf16_t*)dP, *G16 = (bf16_t*)BD;
+    auto go = [&](auto kern) {
+      if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      cfm_launch(kern, grid, block, lds, st, q16, ldqk, (const bf16_t*)Vt, vt_rows, Tpad, (const bf16_t*)P, ldp, dctx,
+                 ld_dctx, lens, B, Tp, H, dkp, ctx_left, ctx_right, P16, dS16, g.sld, G16, g.gld);
+    };
+    switch (dkp / 16) {
+      case 1: go(attn_bwd_scores_kernel<1>); break;
+      case 2: go(attn_bwd_scores_kernel<2>); break;
+      case 3: go(attn_bwd_scores_kernel<3>); break;
+      case 4: go(attn_bwd_scores_kernel<4>); break;
+      case 5: go(attn_bwd_scores_kernel<5>); break;
+      case 6: go(attn_bwd_scores_kernel<6>); break;
+      case 7: go(attn_bwd_scores_kernel<7>); break;
+      default: go(attn_bwd_scores_kernel<8>); break;
+    }
+  }
   // S[b,h] = (q+u)c . k^T
-  {
+  if (!fused) {
     BgArgs a = A0(qkc, ldqk, 1, (long)Tp * ldqk, dkp);
     setB(a, (const void*)nullptr, 1, ldqk, (long)Tp * ldqk, dkp);
     a.B = (const void*)(qkc + 2L * H * dkp * es);
@@ -381,7 +604,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     bgemm(dt, a, OP_CT, OP_CT, Z, st);
   }
   // BD[b,h] = (q+v)c . p^T   (2T'-1 positions)
-  {
+  if (!fused) {
     BgArgs a = A0(qkc + (long)H * dkp * es, ldqk, 1, (long)Tp * ldqk, dkp);
     setB(a, P, 1, ldp, 0, dkp);
     setC(a, BD, g.gld, 1, (long)H * szg, szg);
@@ -389,17 +612,17 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     bgemm(dt, a, OP_CT, OP_CT, Z, st);
   }
   const unsigned rows_blocks = (unsigned)((BT * H + 3) / 4);
-  cfm_launch(attn_probs_kernel, dim3(rows_blocks), dim3(256), 0, st, S, g.sld, (const float*)BD, g.gld, lens, B, H, Tp,
+  if (!fused) cfm_launch(attn_probs_kernel, dim3(rows_blocks), dim3(256), 0, st, S, g.sld, (const float*)BD, g.gld, lens, B, H, Tp,
              ctx_left, ctx_right);
   // dP[b,h] = dctx . V^T
-  {
+  if (!fused) {
     BgArgs a = A0(dctx, ld_dctx, 1, (long)Tp * ld_dctx, dk);
     setB(a, Vt, (long)Tpad, 1, (long)H * vt_rows * Tpad, (long)vt_rows * Tpad);
     setC(a, dP, g.sld, 1, (long)H * szs, szs);
     a.M = Tp; a.N = Tp; a.K = dk; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
     bgemm(dt, a, OP_F32, OP_CT, Z, st);
   }
-  cfm_launch(attn_dscore_kernel, dim3(rows_blocks), dim3(256), 0, st, (const float*)S, dP, g.sld, BD, g.gld, B, H, Tp);
+  if (!fused) cfm_launch(attn_dscore_kernel, dim3(rows_blocks), dim3(256), 0, st, (const float*)S, dP, g.sld, BD, g.gld, B, H, Tp);
   float* G = BD;
   // d(q+u) = dS . k / sqrt(dk) -> dq
   {
@@ -407,7 +630,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, qkc + 2L * H * dkp * es, ldqk, 1, (long)Tp * ldqk, dkp);
     setC(a, dq, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
     a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = rs; a.accumulate = 0;
-    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+    bgemm(dt, a, opS, OP_CT, Z, st);
   }
   if (du) col_sums(dq, ld_dqkv, (int)BT, H * dk, du, 0, cs, st);
   // d(q+v) = G . p / sqrt(dk) -> tmp;  dq += tmp
@@ -416,7 +639,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, P, ldp, 1, 0, dkp);
     setC(a, tmp, (long)H * dk, 1, (long)Tp * H * dk, dk);
     a.M = Tp; a.N = dk; a.K = 2 * Tp - 1; a.Z2 = H; a.alpha = rs; a.accumulate = 0;
-    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+    bgemm(dt, a, opS, OP_CT, Z, st);
   }
   if (dvb) col_sums(tmp, (long)H * dk, (int)BT, H * dk, dvb, 0, cs, st);
   cfm_launch(add_rows_kernel, dim3(1024), dim3(256), 0, st, dq, ld_dqkv, (const float*)tmp, (long)H * dk, BT, H * dk);
@@ -426,7 +649,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, qkc, ldqk, 1, (long)Tp * ldqk, dkp);
     setC(a, dk_, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
     a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = ln2; a.accumulate = 0;
-    bgemm(dt, a, OP_F32, OP_CT, Z, st);
+    bgemm(dt, a, opS, OP_CT, Z, st);
   }
   // dv = P^T . dctx
   {
@@ -434,7 +657,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, dctx, ld_dctx, 1, (long)Tp * ld_dctx, dk);
     setC(a, dv, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
     a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
-    bgemm(dt, a, OP_F32, OP_F32, Z, st);
+    bgemm(dt, a, opS, OP_F32, Z, st);
   }
   // dp[h] = sum_(b,i) G^T . (q+v)c * ln2: per head a GEMM with K = B*T' ((b, i) rows are uniform in
   // G and qk), split S ways along K (z = h * S + s) into fp32 slabs, then summed in a fixed order
@@ -447,7 +670,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, qkc + (long)H * dkp * es, ldqk, 1, dkp, (long)kc * ldqk);
     setC(a, part, (long)H * dk, 1, dk, NP * H * dk);
     a.M = (int)NP; a.N = dk; a.K = kc; a.Z2 = S; a.alpha = ln2; a.accumulate = 0; a.Ktot = (int)BT;
-    bgemm(dt, a, OP_F32, OP_CT, H * S, st);
+    bgemm(dt, a, opS, OP_CT, H * S, st);
     cfm_launch(slab_rows_kernel, dim3(1024), dim3(256), 0, st, (const float*)part, S, NP, H * dk, dpos, ld_dpos);
   }
 }
