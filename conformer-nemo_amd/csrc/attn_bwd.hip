@@ -3,9 +3,11 @@
 //
 // Operands are the forward's own layouts (cfm_kernels.h): qk = [(q+u)c | (q+v)c | k] per row with
 // c = log2(e)/sqrt(dk), V transposed per (b, h) in Vt, and p = linear_pos(pos_emb) per head.
-// The T' x T' score matrices are materialised per (b, h) in fp32 (B*H*T'^2*4 bytes: 64 MB at
-// BASELINE config 3) and every contraction runs on one batched MFMA GEMM (`bgemm`, LDS-staged,
-// any operand orientation):
+// bf16 compute (T' <= 512, dk % 16 == 0): one fused launch (`attn_bwd_scores_kernel`) recomputes S,
+// BD, the softmax and dP per 32 query rows in registers and writes only the bf16 images the
+// remaining contractions read (P, dS and the skewed G: 128 MB at BASELINE config 3).  fp32 parity
+// mode (and any other shape) materialises the fp32 score matrices per (b, h) and runs every
+// contraction on one batched MFMA GEMM (`bgemm`, LDS-staged, any operand orientation):
 //   S  = (q+u)c . k^T            BD = (q+v)c . p^T          (log2 units, as the forward)
 //   P  = softmax_j(S[i][j] + BD[i][T'-1-i+j]) with the pad / context mask      (rel_shift :159-170)
 //   dP = dctx . V^T,   dS = P * (dP - rowsum(P * dP))                          (natural-log units)
@@ -472,29 +474,43 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
     }
   }
   block_rows<false>(D, red, fin, w, nw, lane);
-  const long img = (long)bh * Tp * sld;
-  bf16_t* Gb = G + ((long)h * B + b) * Tp * gld;
+  // Stage the block's P and dS rows (bf16) in LDS -- the BD images are dead: every wave read its own
+  // before the first row reduction's barrier -- then write whole rows as 8-byte runs: P and dS rows
+  // (the [T', sld) tail as zeros) and the skewed G rows, zeros included.
+  const int SP = 64 * nw;
+  bf16_t* Ps = (bf16_t*)bd_all;
+  bf16_t* dSs = Ps + 32 * SP;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int i = i0 + acc_row(e, lane);
-    if (i >= Tp) continue;
+    const int row = acc_row(e, lane);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int j = 64 * w + 32 * c + l32;
-      const float ds = sc[c][e] * (dp[c][e] - D[e]);
-      if (j < Tp) {
-        Pg[img + (long)i * sld + j] = f2bf(sc[c][e]);
-        dSg[img + (long)i * sld + j] = f2bf(ds);
-      }
-      const int r = Tp - 1 - i + j;
-      if (r < gld) Gb[(long)i * gld + r] = f2bf(j < Tp ? ds : 0.0f);
+      Ps[row * SP + j] = f2bf(sc[c][e]);
+      dSs[row * SP + j] = f2bf(sc[c][e] * (dp[c][e] - D[e]));
     }
   }
-  // G positions no key of this block reaches: [0, T'-1-i) and [T'-1-i + 64 nw, gld)
-  const int span = 64 * nw;
-  for (int idx = threadIdx.x; idx < 32 * (int)gld; idx += blockDim.x) {
-    const int il = idx / (int)gld, r = idx - il * (int)gld, i = i0 + il;
-    if (i < Tp && (r < Tp - 1 - i || r >= Tp - 1 - i + span)) Gb[(long)i * gld + r] = 0;
+  __syncthreads();
+  const long img = (long)bh * Tp * sld;
+  bf16_t* Gb = G + ((long)h * B + b) * Tp * gld;
+  const int cps = (int)(sld / 4), cpg = (int)(gld / 4);
+  for (int il = w; il < 32 && i0 + il < Tp; il += nw) {
+    const int i = i0 + il, sh = Tp - 1 - i;
+    const bf16_t* pr = Ps + il * SP;
+    const bf16_t* dr = dSs + il * SP;
+    for (int c = lane; c < cps; c += 64) {
+      *(uint2*)(Pg + img + (long)i * sld + 4 * c) = *(const uint2*)(pr + 4 * c);
+      *(uint2*)(dSg + img + (long)i * sld + 4 * c) = *(const uint2*)(dr + 4 * c);
+    }
+    for (int c = lane; c < cpg; c += 64) {
+      uint32_t v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * c + e - sh;
+        v[e] = (j >= 0 && j < Tp) ? (uint32_t)dr[j] : 0u;
+      }
+      *(uint2*)(Gb + (long)i * gld + 4 * c) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+    }
   }
 }
 
