@@ -581,6 +581,96 @@ __global__ __launch_bounds__(256) void im2col_t_kernel(const T* __restrict__ x1,
     if (r < rows_pad && m < ld) st_f<T>(dst + (long)r * ld + m, v);
   }
 }
+// 8 consecutive compute-type values <-> fp32 (16-byte bf16 / 2 x 16-byte fp32 accesses)
+template <typename T> CFM_DEV void ld8(const T* p, float* v);
+template <> CFM_DEV void ld8<float>(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> CFM_DEV void ld8<bf16_t>(const bf16_t* p, float* v) { Vec16<bf16_t>::to_f32(*(const uint4*)p, v); }
+template <typename T> CFM_DEV void st8(T* p, const float* v);
+template <> CFM_DEV void st8<float>(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <> CFM_DEV void st8<bf16_t>(bf16_t* p, const float* v) { *(uint4*)p = Vec16<bf16_t>::from_f32(v); }
+
+// col2im_relu_kernel for C % 8 == 0: one thread per 8 channels of an input pixel (index math once
+// per pixel, 16-byte loads of X1 and of each contributing dCol tap, 2 x 16-byte fp32 stores).
+template <typename T>
+__global__ __launch_bounds__(256) void col2im_relu_vec_kernel(const T* __restrict__ dcol, const T* __restrict__ x1,
+                                                              int B, int T1, int F1, int T2, int F2, int C,
+                                                              float* __restrict__ dy1) {
+  const int C8 = C >> 3;
+  const long n = (long)B * T1 * F1 * C8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long p = i / C8;
+    const int c = (int)(i - p * C8) * 8;
+    const int f1 = (int)(p % F1);
+    const int bt = (int)(p / F1);
+    const int t1 = bt % T1, b = bt / T1;
+    float xv[8], s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    ld8<T>(x1 + p * C + c, xv);
+    bool any = false;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) any |= xv[e] > 0.0f;
+    if (any) {
+      for (int kt = 0; kt < 3; ++kt) {
+        const int tt = t1 + 1 - kt;
+        if (tt < 0 || (tt & 1) || (tt >> 1) >= T2) continue;
+        for (int kf = 0; kf < 3; ++kf) {
+          const int ff = f1 + 1 - kf;
+          if (ff < 0 || (ff & 1) || (ff >> 1) >= F2) continue;
+          const long m = ((long)b * T2 + (tt >> 1)) * F2 + (ff >> 1);
+          float v[8];
+          ld8<T>(dcol + m * 9 * C + (long)(3 * kt + kf) * C + c, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] += v[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = xv[e] > 0.0f ? s[e] : 0.0f;
+    st8<float>(dy1 + p * C + c, s);
+  }
+}
+
+// im2col_t_kernel for C % 8 == 0 and ld % 8 == 0: 64 (tap, ci) rows x 64 pixels per block; 16-byte
+// loads of 8 channels of an X1 pixel, 16-byte stores of 8 pixels of a destination row.
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_t_vec_kernel(const T* __restrict__ x1, int T1, int F1, int T2, int F2,
+                                                           int C, int M2, T* __restrict__ dst, long ld, int rows_pad) {
+  __shared__ float tile[64][65];   // [row r - r0][pixel m - m0]
+  const int r0 = blockIdx.y * 64, m0 = blockIdx.x * 64;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {   // load: pixel m = m0 + (idx >> 3), rows r0 + 8 (idx & 7) .. +7
+    const int idx = q * 256 + threadIdx.x;
+    const int ml = idx >> 3, rl = 8 * (idx & 7);
+    const int m = m0 + ml, r = r0 + rl;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (m < M2 && r < 9 * C) {
+      const int tap = r / C, ci = r - tap * C, kt = tap / 3, kf = tap - kt * 3;
+      const int f2 = m % F2, bt = m / F2, t2 = bt % T2, b = bt / T2;
+      const int ti = 2 * t2 - 1 + kt, fi = 2 * f2 - 1 + kf;
+      if (ti >= 0 && ti < T1 && fi >= 0 && fi < F1) ld8<T>(x1 + (((long)b * T1 + ti) * F1 + fi) * C + ci, v);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tile[rl + e][ml] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {   // store: row r0 + (idx >> 3), pixels m0 + 8 (idx & 7) .. +7
+    const int idx = q * 256 + threadIdx.x;
+    const int rl = idx >> 3, ml = 8 * (idx & 7);
+    const int r = r0 + rl, m = m0 + ml;
+    if (r >= rows_pad || m >= ld) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = r == 9 * C ? (m + e < M2 ? 1.0f : 0.0f) : tile[rl][ml + e];
+    st8<T>(dst + (long)r * ld + m, v);
+  }
+}
+
 // conv1 weight gradient, stage 1: partial[chunk][c][tap] = sum over the chunk's (b, t1) rows and all
 // f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T))
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int F, int T, int T1, int F1,
@@ -1374,7 +1464,15 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   if (Gp(S.i_c2w) || Gp(S.i_c2b)) {   // [dW2 | db2] = dY2^T . [im2col(X1) | 1]
     S.pack(dX2, false, g.C, (int)g.M2, g.C, true, 1.0f, pat, g.M2p, g.C, (int)g.M2p);
     const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C + 4) + 31) / 32));
-    if (dt == DT_F32)
+    const dim3 grid64((unsigned)((g.M2p + 63) / 64), (unsigned)((S.npad(9L * g.C + 4) + 63) / 64));
+    const bool vec = g.C % 8 == 0 && g.M2p % 8 == 0;
+    if (vec && dt == DT_F32)
+      cfm_launch(im2col_t_vec_kernel<float>, grid64, dim3(256), 0, st, S.T_<const float>(S.tp.X1), g.T1, g.F1, g.T2,
+                 g.F2, g.C, (int)g.M2, S.W_<float>(S.wl.i2c), g.M2p, S.npad(9L * g.C + 4));
+    else if (vec)
+      cfm_launch(im2col_t_vec_kernel<bf16_t>, grid64, dim3(256), 0, st, S.T_<const bf16_t>(S.tp.X1), g.T1, g.F1,
+                 g.T2, g.F2, g.C, (int)g.M2, S.W_<bf16_t>(S.wl.i2c), g.M2p, S.npad(9L * g.C + 4));
+    else if (dt == DT_F32)
       cfm_launch(im2col_t_kernel<float>, grid, dim3(256), 0, st, S.T_<const float>(S.tp.X1), g.T1, g.F1, g.T2, g.F2,
                  g.C, (int)g.M2, S.W_<float>(S.wl.i2c), g.M2p, S.npad(9L * g.C + 4));
     else
@@ -1393,7 +1491,13 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     gemm(dt, pa, S.kpad(g.C), (int)g.M2, g.C, wt, S.kpad(g.C), 9 * g.C, e, h->zero_page, st);
     const long n1 = (long)g.B * g.T1 * g.F1 * g.C;
     float* dy1 = S.W_<float>(S.wl.dy1);
-    if (dt == DT_F32)
+    if (g.C % 8 == 0 && dt == DT_F32)
+      cfm_launch(col2im_relu_vec_kernel<float>, dim3(ew_grid(n1 / 8)), dim3(256), 0, st, S.W_<const float>(S.wl.dcol),
+                 S.T_<const float>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
+    else if (g.C % 8 == 0)
+      cfm_launch(col2im_relu_vec_kernel<bf16_t>, dim3(ew_grid(n1 / 8)), dim3(256), 0, st,
+                 S.W_<const bf16_t>(S.wl.dcol), S.T_<const bf16_t>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
+    else if (dt == DT_F32)
       cfm_launch(col2im_relu_kernel<float>, dim3(ew_grid(n1)), dim3(256), 0, st, S.W_<const float>(S.wl.dcol),
                  S.T_<const float>(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, dy1);
     else
