@@ -77,12 +77,10 @@ unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n 
 // 64x64 LDS tiles; 16-byte (fp32) / 8-byte (bf16) source loads along source rows and 16-byte stores
 // along destination rows when the strides and base pointers allow (src_vec / dst_vec).
 template <typename Tin, typename Tout>
-__global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src, long src_ld, int rows, int cols,
-                                                      int transpose, float scale, int fn, Drop drop,
-                                                      Tout* __restrict__ dst, long dst_ld, int rows_pad,
-                                                      int cols_pad, int ones_row, int src_vec, int dst_vec) {
-  __shared__ float tile[64][65];                      // [dst row][dst col] of this block
-  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+CFM_DEV void tpack_tile(float (*tile)[65], int bx, int by, const Tin* __restrict__ src, long src_ld, int rows,
+                        int cols, int transpose, float scale, int fn, Drop drop, Tout* __restrict__ dst, long dst_ld,
+                        int rows_pad, int cols_pad, int ones_row, int src_vec, int dst_vec) {
+  const int i0 = by * 64, j0 = bx * 64;
   const int sr0 = transpose ? j0 : i0, sc0 = transpose ? i0 : j0;
   const int c4 = threadIdx.x & 15, r = threadIdx.x >> 4;
 #pragma unroll
@@ -141,6 +139,43 @@ __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src,
         if (dj + e < cols_pad) st_f<Tout>(dp + e, o[e]);
     }
   }
+}
+
+template <typename Tin, typename Tout>
+__global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src, long src_ld, int rows, int cols,
+                                                      int transpose, float scale, int fn, Drop drop,
+                                                      Tout* __restrict__ dst, long dst_ld, int rows_pad,
+                                                      int cols_pad, int ones_row, int src_vec, int dst_vec) {
+  __shared__ float tile[64][65];                      // [dst row][dst col] of this block
+  tpack_tile<Tin, Tout>(tile, blockIdx.x, blockIdx.y, src, src_ld, rows, cols, transpose, scale, fn, drop, dst, dst_ld,
+                        rows_pad, cols_pad, ones_row, src_vec, dst_vec);
+}
+
+// Up to 16 fp32 -> compute-type (or fp32) packs of parameters in one launch: a layer's weight
+// matrices and zero-padded bias rows, each job a tpack over its own range of grid blocks.
+struct PackJob {
+  const float* src;
+  void* dst;
+  int ld_src, rows, cols, tr, ld_dst, rows_pad, cols_pad, out_f32, src_vec, dst_vec, tiles_x, tile0;
+};
+struct PackList {
+  PackJob j[16];
+  int count;
+};
+template <typename T>
+__global__ __launch_bounds__(256) void tpack_multi_kernel(PackList l) {
+  __shared__ float tile[64][65];
+  int k = 0;
+  while (k + 1 < l.count && (int)blockIdx.x >= l.j[k + 1].tile0) ++k;
+  const PackJob& J = l.j[k];
+  const int t = (int)blockIdx.x - J.tile0, by = t / J.tiles_x, bx = t - by * J.tiles_x;
+  const Drop none{0, 0, 1.0f};
+  if (J.out_f32)
+    tpack_tile<float, float>(tile, bx, by, J.src, J.ld_src, J.rows, J.cols, J.tr, 1.0f, 0, none, (float*)J.dst,
+                             J.ld_dst, J.rows_pad, J.cols_pad, -1, J.src_vec, J.dst_vec);
+  else
+    tpack_tile<float, T>(tile, bx, by, J.src, J.ld_src, J.rows, J.cols, J.tr, 1.0f, 0, none, (T*)J.dst, J.ld_dst,
+                         J.rows_pad, J.cols_pad, -1, J.src_vec, J.dst_vec);
 }
 
 // dst[i] = i < N && src ? src[i] : 0 for i < npad (GEMM bias arrays, zero-padded to the N granule)
@@ -823,12 +858,13 @@ int wgrad_splits(int N, int K, long rows) {
   return (int)std::max<long>(1, std::min<long>(s, 16));
 }
 
+enum { WT_FF1_W2 = 0, WT_FF1_W1, WT_FF2_W2, WT_FF2_W1, WT_PW2, WT_PW1, WT_OUT };
 struct Ws {
   // forward
-  long w1, b1, w2, b2, wqkv, bqkv, uv, wout, bout, wpos, wpw1, bpw1, dww, wpw2, bpw2, wc2, bc2, wsub, bsub;
+  long w1, b1, w2, b2, w1b, b1b, w2b, b2b, wqkv, bqkv, uv, wout, bout, wpos, wpw1, bpw1, dww, wpw2, bpw2, wc2, bc2, wsub, bsub;
   long u, br, dwo, gt, s1, s2, sync;
   // backward
-  long gA, gB, dbr, dU, pa, pat, pbt, wt, part, dqkv, dctx, dP, dpre, dG, dD, red;
+  long gA, gB, dbr, dU, pa, pat, pbt, wt, wtl[7], part, dqkv, dctx, dP, dpre, dG, dD, red;
   long dX2, dcol, i2c, dy1, c1part, gtmp, attws;
   long total;
 };
@@ -844,6 +880,10 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.b1 = a.take(np(dff) * 4);
   w.w2 = a.take(np(d) * kp(dff) * es);
   w.b2 = a.take(np(d) * 4);
+  w.w1b = a.take(np(dff) * kp(d) * es);
+  w.b1b = a.take(np(dff) * 4);
+  w.w2b = a.take(np(d) * kp(dff) * es);
+  w.b2b = a.take(np(d) * 4);
   w.wqkv = a.take(np(3 * HP) * kp(d) * es);
   w.bqkv = a.take(np(3 * HP) * 4);
   w.uv = a.take(2 * HP * 4);
@@ -879,6 +919,10 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.pbt = a.take(KT * g.Mq * es);                                      // x^T [Kpad][Mp]
   w.wt = a.take(std::max({np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(3 * d), np(d) * kp(2 * d),
                           np((long)g.F2 * g.C) * kp(d), np(9L * g.C) * kp(g.C)}) * es);
+  // a layer's transposed weights for its dgrad GEMMs, packed in one launch (WT_* order)
+  const long wtl_sz[7] = {np(dff) * kp(d), np(d) * kp(dff), np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(d),
+                          np(d) * kp(2 * d), np(d) * kp(d)};
+  for (int i = 0; i < 7; ++i) w.wtl[i] = a.take(wtl_sz[i] * es);
   long part = 0;
   auto upd = [&](long N, long K, long rows) { part = std::max(part, (long)wgrad_splits((int)N, (int)K, rows) * N * K); };
   upd(dff, d + 4, M); upd(d, dff + 4, M); upd(3 * d, d + 4, M); upd(d, d + 4, M); upd(2 * d, d + 4, M);
@@ -956,6 +1000,35 @@ struct Step {
       cfm_launch(tpack_kernel<float, bf16_t>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
                  fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row, sv, dv);
     }
+  }
+  // one-launch parameter packs (tpack_multi_kernel)
+  struct Batch {
+    PackList l;
+    int tiles = 0;
+    Batch() { std::memset(&l, 0, sizeof(l)); }
+  };
+  void job(Batch& b, const float* src, int ld_src, int rows, int cols, bool tr, void* dst, long ld_dst, int rp, int cp,
+           bool f32) const {
+    if (b.l.count == 16) flush(b);
+    PackJob& j = b.l.j[b.l.count++];
+    const int des = (f32 || g.dt == DT_F32) ? 4 : 2;
+    j.src = src; j.dst = dst; j.ld_src = ld_src; j.rows = rows; j.cols = cols; j.tr = tr ? 1 : 0;
+    j.ld_dst = (int)ld_dst; j.rows_pad = rp; j.cols_pad = cp; j.out_f32 = f32 ? 1 : 0;
+    j.src_vec = (ld_src % 4 == 0 && ((uintptr_t)src % 16) == 0) ? 1 : 0;
+    j.dst_vec = (ld_dst % (16 / des) == 0 && ((uintptr_t)dst % 16) == 0) ? 1 : 0;
+    j.tiles_x = (cp + 63) / 64;
+    j.tile0 = b.tiles;
+    b.tiles += j.tiles_x * ((rp + 63) / 64);
+  }
+  void jobW(Batch& b, const float* w, int N, int K, void* dst) const { job(b, w, K, N, K, false, dst, kpad(K), npad(N), kpad(K), false); }
+  void jobWt(Batch& b, const float* w, int N, int K, void* dst) const { job(b, w, K, N, K, true, dst, kpad(N), npad(K), kpad(N), false); }
+  void jobBias(Batch& b, const float* bias, int N, float* dst) const { job(b, bias, N, 1, N, false, dst, npad(N), 1, npad(N), true); }
+  void flush(Batch& b) const {
+    if (b.l.count == 0) return;
+    if (g.dt == DT_F32) cfm_launch(tpack_multi_kernel<float>, dim3(b.tiles), dim3(256), 0, st, b.l);
+    else cfm_launch(tpack_multi_kernel<bf16_t>, dim3(b.tiles), dim3(256), 0, st, b.l);
+    std::memset(&b.l, 0, sizeof(b.l));
+    b.tiles = 0;
   }
   // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
   void packW(const float* w, int N, int K, void* dst) const {
@@ -1142,16 +1215,33 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
     const TapeLayer& t = S.tp.lay[l];
     float* X[5];
     for (int i = 0; i < 5; ++i) X[i] = S.T_<float>(t.x[i]);
+    // this layer's linear weights and biases, packed in one launch
+    {
+      Step::Batch b;
+      const long sw1[2] = {S.wl.w1, S.wl.w1b}, sb1[2] = {S.wl.b1, S.wl.b1b}, sw2[2] = {S.wl.w2, S.wl.w2b},
+                 sb2[2] = {S.wl.b2, S.wl.b2b};
+      for (int f = 0; f < 2; ++f) {
+        S.jobW(b, S.prm(q.ff_w1[f]), g.dff, d, S.W_(sw1[f]));
+        S.jobBias(b, S.prm(q.ff_b1[f]), g.dff, S.W_<float>(sb1[f]));
+        S.jobW(b, S.prm(q.ff_w2[f]), d, g.dff, S.W_(sw2[f]));
+        S.jobBias(b, S.prm(q.ff_b2[f]), d, S.W_<float>(sb2[f]));
+      }
+      S.jobW(b, S.prm(q.o_w), d, d, S.W_(S.wl.wout));
+      S.jobBias(b, S.prm(q.o_b), d, S.W_<float>(S.wl.bout));
+      S.jobW(b, S.prm(q.pw1_w), 2 * d, d, S.W_(S.wl.wpw1));
+      S.jobBias(b, S.prm(q.pw1_b), 2 * d, S.W_<float>(S.wl.bpw1));
+      S.jobW(b, S.prm(q.pw2_w), d, d, S.W_(S.wl.wpw2));
+      S.jobBias(b, S.prm(q.pw2_b), d, S.W_<float>(S.wl.bpw2));
+      S.flush(b);
+    }
     // ---- FFN1 / FFN2 (conformer_modules.py:99-101, 116-118, 183-200) ----
     auto ffn = [&](int f, float* xin, void* hn, long z, float* xout) {
-      S.packW(S.prm(q.ff_w1[f]), g.dff, d, S.W_(S.wl.w1));
-      S.bias(S.prm(q.ff_b1[f]), g.dff, S.W_<float>(S.wl.b1));
-      S.packW(S.prm(q.ff_w2[f]), d, g.dff, S.W_(S.wl.w2));
-      S.bias(S.prm(q.ff_b2[f]), d, S.W_<float>(S.wl.b2));
-      GemmEpi e = S.epi(EPI_STORE, S.W_<float>(S.wl.b1));
+      const long w1 = f ? S.wl.w1b : S.wl.w1, b1 = f ? S.wl.b1b : S.wl.b1;
+      const long w2 = f ? S.wl.w2b : S.wl.w2, b2 = f ? S.wl.b2b : S.wl.b2;
+      GemmEpi e = S.epi(EPI_STORE, S.W_<float>(b1));
       e.C = S.T_(z);
       e.ldc = g.dff;
-      gemm(dt, hn, d, M, d, S.W_(S.wl.w1), S.kpad(d), g.dff, e, h->zero_page, st);
+      gemm(dt, hn, d, M, d, S.W_(w1), S.kpad(d), g.dff, e, h->zero_page, st);
       const long n = (long)M * g.dff;
       const Drop di = S.drop(site(l, f ? 4 : 0));
       if (dt == DT_F32)
@@ -1160,7 +1250,7 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       else
         cfm_launch(swish_drop_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z), n, di,
                    S.W_<bf16_t>(S.wl.u));
-      S.gemm_f32out(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(S.wl.w2), d, S.W_<float>(S.wl.b2), 1.0f, br, d, false);
+      S.gemm_f32out(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 1.0f, br, d, false);
       cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)xin, (const float*)br, 0.5f,
                  n_md, S.drop(site(l, f ? 5 : 1)), xout);
     };
@@ -1187,8 +1277,6 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       gemm(dt, S.T_(t.hn[1]), d, M, d, S.W_(S.wl.wqkv), S.kpad(d), (int)(3 * HP), e, h->zero_page, st);
       rel_pos_attention(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B, g.Tp, H,
                         g.dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, S.T_(t.ctx), d, st);
-      S.packW(S.prm(q.o_w), d, d, S.W_(S.wl.wout));
-      S.bias(S.prm(q.o_b), d, S.W_<float>(S.wl.bout));
       S.gemm_f32out(S.T_(t.ctx), d, M, d, S.W_(S.wl.wout), d, S.W_<float>(S.wl.bout), 1.0f, br, d, false);
       cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[1], (const float*)br, 1.0f,
                  n_md, S.drop(site(l, 2)), X[2]);
@@ -1198,8 +1286,6 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
     layernorm(dt, X[2], M, d, S.prm(q.ln_w[LN_CONV]), S.prm(q.ln_b[LN_CONV]), nullptr, nullptr, nullptr,
               S.T_(t.hn[2]), 0, st);
     {
-      S.packW(S.prm(q.pw1_w), 2 * d, d, S.W_(S.wl.wpw1));
-      S.bias(S.prm(q.pw1_b), 2 * d, S.W_<float>(S.wl.bpw1));
       float* pre = S.T_<float>(t.pre);
       S.gemm_f32out(S.T_(t.hn[2]), d, M, d, S.W_(S.wl.wpw1), 2 * d, S.W_<float>(S.wl.bpw1), 1.0f, pre, 2 * d, false);
       if (dt == DT_F32)
@@ -1237,8 +1323,6 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
         cfm_launch(bn_swish_kernel<bf16_t>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dwo,
                    (const float*)mean, (const float*)rstd, S.prm(q.bn_w), S.prm(q.bn_b), (long)M, d,
                    S.T_<float>(t.xhat), S.T_<bf16_t>(t.s));
-      S.packW(S.prm(q.pw2_w), d, d, S.W_(S.wl.wpw2));
-      S.bias(S.prm(q.pw2_b), d, S.W_<float>(S.wl.bpw2));
       S.gemm_f32out(S.T_(t.s), d, M, d, S.W_(S.wl.wpw2), d, S.W_<float>(S.wl.bpw2), 1.0f, br, d, false);
       cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[2], (const float*)br, 1.0f,
                  n_md, S.drop(site(l, 3)), X[3]);
@@ -1282,11 +1366,15 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   //   dx (M, K) fp32 (ldx; accumulate or overwrite), dW (N, K) -> G[gw], db -> G[gb]
   //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
   auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
-                        float* dx, long ldx, bool acc, int gw, int gb) {
+                        float* dx, long ldx, bool acc, int gw, int gb, const void* wtp) {
     S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
     if (dx) {
-      S.packWt(w, N, K, wt);
-      S.gemm_f32out(pa, S.kpad(N), M, N, wt, K, nullptr, 1.0f, dx, ldx, acc);
+      const void* W = wtp;   // prepacked by the layer's batch, or packed here
+      if (!W) {
+        S.packWt(w, N, K, wt);
+        W = wt;
+      }
+      S.gemm_f32out(pa, S.kpad(N), M, N, W, K, nullptr, 1.0f, dx, ldx, acc);
     }
     const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
     if (want_w || want_b) {   // [dW | db] = dy^T . [x | 1]
@@ -1320,6 +1408,25 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     const TapeLayer& t = S.tp.lay[l];
     const float* X[5];
     for (int i = 0; i < 5; ++i) X[i] = S.T_<const float>(t.x[i]);
+    // the layer's transposed weights for every dgrad GEMM (W_q/W_k/W_v stacked into wt), one launch
+    void* WT[7];
+    for (int i = 0; i < 7; ++i) WT[i] = S.W_(S.wl.wtl[i]);
+    {
+      Step::Batch b;
+      S.jobWt(b, S.prm(q.ff_w2[0]), d, g.dff, WT[WT_FF1_W2]);
+      S.jobWt(b, S.prm(q.ff_w1[0]), g.dff, d, WT[WT_FF1_W1]);
+      S.jobWt(b, S.prm(q.ff_w2[1]), d, g.dff, WT[WT_FF2_W2]);
+      S.jobWt(b, S.prm(q.ff_w1[1]), g.dff, d, WT[WT_FF2_W1]);
+      S.jobWt(b, S.prm(q.pw2_w), d, d, WT[WT_PW2]);
+      S.jobWt(b, S.prm(q.pw1_w), 2 * d, d, WT[WT_PW1]);
+      S.jobWt(b, S.prm(q.o_w), d, d, WT[WT_OUT]);
+      const long ldw = S.kpad(3L * d);
+      const int wi[3] = {q.q_w, q.k_w, q.v_w};
+      for (int p = 0; p < 3; ++p)   // Wt[i][p*d + o] = W_p[o][i]
+        S.job(b, S.prm(wi[p]), d, d, d, true, (char*)wt + (long)p * d * es, ldw, S.npad(d),
+              p == 2 ? (int)(ldw - 2L * d) : d, false);
+      S.flush(b);
+    }
     // norm_out: gB = d x4
     ln_bwd(X[4], q.ln_w[LN_OUT], q.ln_b[LN_OUT], gA, gB, false);
 
@@ -1330,7 +1437,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
                  S.drop(site(l, f ? 5 : 1)), dbr);
       const Drop di = S.drop(site(l, f ? 4 : 0));
       // linear2 (input u = dropout(swish(z)) recomputed from z)
-      linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f]);
+      linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f],
+                 WT[f ? WT_FF2_W2 : WT_FF1_W2]);
       const long n = (long)M * g.dff;
       if (dt == DT_F32)
         cfm_launch(swish_drop_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z),
@@ -1339,7 +1447,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         cfm_launch(swish_drop_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z),
                    (const float*)dU, n, di, dU);
       float* dhn = S.W_<float>(S.wl.dctx);
-      linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f], q.ff_b1[f]);
+      linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f], q.ff_b1[f],
+                 WT[f ? WT_FF2_W1 : WT_FF1_W1]);
       ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true);
     };
     ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, gB);   // gB = d x3
@@ -1349,7 +1458,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
                  S.drop(site(l, 3)), dbr);
       float* dS = S.W_<float>(S.wl.dD);
-      linear_bwd(dbr, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b);
+      linear_bwd(dbr, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b,
+                 WT[WT_PW2]);
       float* dZ = S.W_<float>(S.wl.dG);
       const float* xhat = S.T_<const float>(t.xhat);
       cfm_launch(bn_swish_bwd_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dS, xhat, S.prm(q.bn_w),
@@ -1381,7 +1491,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       if (s2 != CFM_OK) fail(s2, std::string("glu backward: ") + g_last_error);
       float* dhn = S.W_<float>(S.wl.dctx);
       linear_bwd(dpre, 2 * d, S.prm(q.pw1_w), d, S.T_(t.hn[2]), d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.pw1_w,
-                 q.pw1_b);
+                 q.pw1_b, WT[WT_PW1]);
       ln_bwd(X[2], q.ln_w[LN_CONV], q.ln_b[LN_CONV], dhn, gB, true);   // gB = d x2
     }
 
@@ -1390,7 +1500,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
                  S.drop(site(l, 2)), dbr);
       float* dctx = S.W_<float>(S.wl.dctx);
-      linear_bwd(dbr, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b);
+      linear_bwd(dbr, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b,
+                 WT[WT_OUT]);
       float* dqkv = S.W_<float>(S.wl.dqkv);
       float* dP = S.W_<float>(S.wl.dP);
       const int dk = g.dk;
@@ -1407,11 +1518,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       // q/k/v: biases, input gradient through [Wq; Wk; Wv], stacked weight gradient
       S.pack(dqkv, false, 3L * d, M, 3 * d, false, 1.0f, pa, S.kpad(3L * d), M, S.kpad(3L * d));
       {
-        const long ldw = S.kpad(3L * d);
-        const int wi[3] = {q.q_w, q.k_w, q.v_w};
-        for (int p = 0; p < 3; ++p)   // Wt[i][p*d + o] = W_p[o][i]
-          S.pack(S.prm(wi[p]), false, d, d, d, true, 1.0f, (char*)wt + (long)p * d * es, ldw, S.npad(d),
-                 p == 2 ? (int)(ldw - 2L * d) : d);
+        const int wi[3] = {q.q_w, q.k_w, q.v_w};   // their W^T is in wt (the layer's batch)
         float* dhn = dctx;   // dctx consumed
         S.gemm_f32out(pa, S.kpad(3L * d), M, 3 * d, wt, d, nullptr, 1.0f, dhn, d, false);
         const int bi3[3] = {q.q_b, q.k_b, q.v_b};
