@@ -151,6 +151,71 @@ __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src,
                         rows_pad, cols_pad, ones_row, src_vec, dst_vec);
 }
 
+// Both packs of a dense fp32 output gradient dy (rows x cols) from one read: dA = dy in the compute
+// type ([rpA][ldA], the dgrad GEMM's A operand) and dT = dy^T ([rpT][ldT], the wgrad GEMM's A
+// operand), zero outside dy.  The grid covers the larger of the two extents per dimension.
+template <typename Tout>
+__global__ __launch_bounds__(256) void tpack2_kernel(const float* __restrict__ src, long src_ld, int rows, int cols,
+                                                       Tout* __restrict__ dA, long ldA, int rpA, int cpA,
+                                                       Tout* __restrict__ dT, long ldT, int rpT, int cpT,
+                                                       int src_vec, int vecA, int vecT) {
+  __shared__ float tile[64][65];   // [src row][src col]
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int c4 = threadIdx.x & 15, r = threadIdx.x >> 4;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int rr = r + 16 * pass, cc = 4 * c4;
+    const int si = i0 + rr, sj = j0 + cc;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (si < rows) {
+      const float* sp = src + (long)si * src_ld + sj;
+      if (src_vec && sj + 3 < cols) {
+        const float4 t = *(const float4*)sp;
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (sj + e < cols) v[e] = sp[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[rr][cc + e] = v[e];
+  }
+  __syncthreads();
+  constexpr int VE = 16 / (int)sizeof(Tout);
+  constexpr int CPR = 64 / VE, RPP = 256 / CPR;
+  const int q = threadIdx.x % CPR, k0 = threadIdx.x / CPR;
+  for (int k = k0; k < 64; k += RPP) {
+    float o[VE];
+    const int ai = i0 + k, aj = j0 + q * VE;   // dA[ai][aj ..]
+    if (ai < rpA && aj < cpA) {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) o[e] = tile[k][q * VE + e];
+      Tout* dp = dA + (long)ai * ldA + aj;
+      if (vecA && aj + VE <= cpA) {
+        *(uint4*)dp = Vec16<Tout>::from_f32(o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VE; ++e)
+          if (aj + e < cpA) st_f<Tout>(dp + e, o[e]);
+      }
+    }
+    const int ti = j0 + k, tj = i0 + q * VE;   // dT[ti][tj ..] = dy[tj ..][ti]
+    if (ti < rpT && tj < cpT) {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) o[e] = tile[q * VE + e][k];
+      Tout* dp = dT + (long)ti * ldT + tj;
+      if (vecT && tj + VE <= cpT) {
+        *(uint4*)dp = Vec16<Tout>::from_f32(o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < VE; ++e)
+          if (tj + e < cpT) st_f<Tout>(dp + e, o[e]);
+      }
+    }
+  }
+}
+
 // Up to 16 fp32 -> compute-type (or fp32) packs of parameters in one launch: a layer's weight
 // matrices and zero-padded bias rows, each job a tpack over its own range of grid blocks.
 struct PackJob {
@@ -1030,6 +1095,22 @@ struct Step {
     std::memset(&b.l, 0, sizeof(b.l));
     b.tiles = 0;
   }
+  // pack(dy, .., dA, lA, rA, cA) and pack(dy, transposed, .., dT, lT, rT, cT) in one launch
+  void pack2(const float* src, long ld, int rows, int cols, void* dA, long lA, int rA, int cA, void* dT, long lT, int rT,
+             int cT) const {
+    const int des = g.dt == DT_F32 ? 4 : 2;
+    const int gx = (std::max(cA, rT) + 63) / 64, gy = (std::max(rA, cT) + 63) / 64;
+    if (gx <= 0 || gy <= 0) return;
+    const int sv = (ld % 4 == 0 && ((uintptr_t)src % 16) == 0) ? 1 : 0;
+    const int va = (lA % (16 / des) == 0 && ((uintptr_t)dA % 16) == 0) ? 1 : 0;
+    const int vt = (lT % (16 / des) == 0 && ((uintptr_t)dT % 16) == 0) ? 1 : 0;
+    if (g.dt == DT_F32)
+      cfm_launch(tpack2_kernel<float>, dim3(gx, gy), dim3(256), 0, st, src, ld, rows, cols, (float*)dA, lA, rA, cA,
+                 (float*)dT, lT, rT, cT, sv, va, vt);
+    else
+      cfm_launch(tpack2_kernel<bf16_t>, dim3(gx, gy), dim3(256), 0, st, src, ld, rows, cols, (bf16_t*)dA, lA, rA, cA,
+                 (bf16_t*)dT, lT, rT, cT, sv, va, vt);
+  }
   // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
   void packW(const float* w, int N, int K, void* dst) const {
     pack(w, false, K, N, K, false, 1.0f, dst, kpad(K), npad(N), kpad(K));
@@ -1367,7 +1448,11 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
   auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
                         float* dx, long ldx, bool acc, int gw, int gb, const void* wtp) {
-    S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
+    const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
+    if (dx && (want_w || want_b))
+      S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq);
+    else if (dx)
+      S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
     if (dx) {
       const void* W = wtp;   // prepacked by the layer's batch, or packed here
       if (!W) {
@@ -1376,9 +1461,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       }
       S.gemm_f32out(pa, S.kpad(N), M, N, W, K, nullptr, 1.0f, dx, ldx, acc);
     }
-    const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
     if (want_w || want_b) {   // [dW | db] = dy^T . [x | 1]
-      S.pack(dy, false, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
+      if (!dx) S.pack(dy, false, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
       S.pack(xin, true, ldxin, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, xfn, xdr, want_b ? K : -1);
       S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(gw) : nullptr, want_b ? Gp(gb) : nullptr);
     }
