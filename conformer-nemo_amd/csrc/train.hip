@@ -914,10 +914,29 @@ Tape tape_layout(const cfm_encoder* h, const Geo& g) {
 // Tile of a weight-gradient GEMM: 256x256 (tile 11, 3x the arithmetic intensity of 64x128) for the
 // very long contractions (the conv2 weight gradient over 160 000 im2col rows), 64x128 (the shape
 // picker's choice) otherwise.  The split count targets a few tiles per CU for either.
-int wgrad_tile(int N, int K, long rows) { return (rows >= 32768 && N >= 256 && K >= 256) ? 11 : -1; }
+// Weight-gradient GEMM tile: 256x256 for the 160k-row conv2 gradient; CFM_WGRAD_TILE picks another
+// gemm.hip tile id for the M-row layer gradients (A/B measurements; default: pick_tile's 64x128).
+int g_wgrad_tile = [] { const char* e = getenv("CFM_WGRAD_TILE"); return e ? atoi(e) : -1; }();
+int wgrad_tile(int N, int K, long rows) {
+  if (N < 256 || K < 256) return -1;
+  if (rows >= 32768) return 11;
+  return g_wgrad_tile;
+}
+void tile_dims(int t, int& bm, int& bn) {
+  switch (t) {
+    case 0: case 8: bm = 128; bn = 128; return;
+    case 1: case 9: bm = 256; bn = 128; return;
+    case 7: case 11: bm = 256; bn = 256; return;
+    case 10: bm = 128; bn = 256; return;
+    default: bm = 64; bn = 128; return;
+  }
+}
 int wgrad_splits(int N, int K, long rows) {
-  const bool big = wgrad_tile(N, K, rows) == 11;
-  const long tiles = big ? (long)((N + 255) / 256) * ((K + 255) / 256) : (long)((N + 63) / 64) * ((K + 127) / 128);
+  const int t = wgrad_tile(N, K, rows);
+  int bm, bn;
+  tile_dims(t, bm, bn);
+  const bool big = t >= 7;   // one block per CU
+  const long tiles = (long)((N + bm - 1) / bm) * ((K + bn - 1) / bn);
   long s = ((big ? 512 : 768) + tiles - 1) / tiles;
   s = std::min<long>(s, std::max<long>(1, rows / 256));
   return (int)std::max<long>(1, std::min<long>(s, 16));
