@@ -452,11 +452,11 @@ void colred(const float* src, const float* y, const float* mean, long ld, int M,
   cfm_launch(colred_final_kernel, dim3((N + 15) / 16), b, 0, st, (const float*)ws, nch, N, alpha, out, accumulate);
 }
 
-// LayerNorm backward (eps 1e-5, biased variance; torch.nn.LayerNorm) for 8 rows per wave, 32 rows per
+// LayerNorm backward (eps 1e-5, biased variance; torch.nn.LayerNorm) for 4 rows per wave, 16 rows per
 // block, with the weight/bias gradient column partials reduced in-block (fixed order):
 //   dx (+)= rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 //   pw[blk][c] = sum over the block's rows of dy * xhat,  pb[blk][c] = sum of dy
-constexpr int kLnRowsPerWave = 8;
+constexpr int kLnRowsPerWave = 4;
 template <int E4>
 __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ dy, int M, int d,
@@ -475,21 +475,34 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restri
     ab[e] = make_float4(0, 0, 0, 0);
   }
   const float inv_d = 1.0f / (float)d;
+  // the next row's x / dy loads are issued before this row's reductions (one row in flight per wave)
+  const int row0 = (blockIdx.x * 4 + wv) * kLnRowsPerWave;
+  float4 xn[E4], dn[E4];
+  auto load_row = [&](int row) {
+    const float4* xr = (const float4*)(x + (long)min(row, M - 1) * d);
+    const float4* dr = (const float4*)(dy + (long)min(row, M - 1) * d);
+#pragma unroll
+    for (int e = 0; e < E4; ++e) {
+      const int g = min(lane + 64 * e, d4 - 1);
+      xn[e] = xr[g];
+      dn[e] = dr[g];
+    }
+  };
+  load_row(row0);
   for (int i = 0; i < kLnRowsPerWave; ++i) {
-    const int row = (blockIdx.x * 4 + wv) * kLnRowsPerWave + i;
+    const int row = row0 + i;
     if (row >= M) break;
-    const float4* xr = (const float4*)(x + (long)row * d);
-    const float4* dr = (const float4*)(dy + (long)row * d);
     float4 xv[E4], dv[E4];
     float sx = 0.0f;
 #pragma unroll
     for (int e = 0; e < E4; ++e) {
-      const int g = min(lane + 64 * e, d4 - 1);
       const bool ok = lane + 64 * e < d4;
-      xv[e] = ok ? xr[g] : make_float4(0, 0, 0, 0);
-      dv[e] = ok ? dr[g] : make_float4(0, 0, 0, 0);
-      sx += xv[e].x + xv[e].y + xv[e].z + xv[e].w;
+      xv[e] = ok ? xn[e] : make_float4(0, 0, 0, 0);
+      dv[e] = ok ? dn[e] : make_float4(0, 0, 0, 0);
     }
+    if (i + 1 < kLnRowsPerWave) load_row(row + 1);
+#pragma unroll
+    for (int e = 0; e < E4; ++e) sx += xv[e].x + xv[e].y + xv[e].z + xv[e].w;
     const float mean = wave_sum(sx) * inv_d;
     float q = 0.0f;
 #pragma unroll
