@@ -56,6 +56,24 @@ enum Epilogue {
   EPI_QKV = 6,         // packed cols [q | k | v]: C = [q+u | q+v | k] (ldc = 3*H*dkp), v -> Vt[(b*H+h)][d][t]
 };
 
+// Dropout masks (training): keep element e iff hash(key, e) >= thr, thr = p * 2^32; kept values are
+// scaled by 1 / (1 - p).  The hash is a function of the element index only, so a mask is recomputed
+// wherever it is needed (forward epilogue, backward) instead of being stored.
+struct Drop {
+  uint32_t thr;    // 0 = no dropout
+  uint32_t key;    // per (step, site)
+  float scale;     // 1 / (1 - p)
+};
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float drop_mul(const Drop& d, uint64_t e) {
+  if (d.thr == 0) return 1.0f;
+  const uint32_t h = mix32((uint32_t)e ^ mix32(d.key ^ (uint32_t)(e >> 32) * 0x9e3779b9u));
+  return h >= d.thr ? d.scale : 0.0f;
+}
+
 struct GemmEpi {
   int mode;
   const float* bias;   // [Npad] fp32 (may be null)
@@ -69,6 +87,8 @@ struct GemmEpi {
   float qscale;        // EPI_QKV: (q + u), (q + v) are written pre-multiplied by log2(e) / sqrt(dk)
   int out_scalar;      // EPI_SCALE_F32: element stores (fp32 rows whose stride is not a multiple of 4)
   int wt;              // set by gemm(): 16-byte output stores write-through (sc1), see store16_wt
+  const float* Xin;    // EPI_RESID: residual input (null: X, updated in place)
+  Drop drop;           // EPI_RESID: dropout on the branch, mask index m * ldx + n (thr 0: none)
 };
 
 struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)

@@ -189,10 +189,11 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     const bool colok = n < p.N;
     float4 xv[NP];
     if constexpr (EPI == EPI_RESID) {
+      const float* XI = e.Xin ? e.Xin : e.X;
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
         const int m = min(m0 + r0 + q * RPP, p.M - 1);
-        xv[q] = *(const float4*)(e.X + xoff + (long)m * e.ldx + nc);
+        xv[q] = *(const float4*)(XI + xoff + (long)m * e.ldx + nc);
       }
     }
 #pragma unroll
@@ -202,8 +203,16 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       const float4 a = *(const float4*)(img + r * TL::EPS + cc * 4);
       float4 o;
       if constexpr (EPI == EPI_RESID) {
-        o.x = xv[q].x + a.x * e.alpha; o.y = xv[q].y + a.y * e.alpha;
-        o.z = xv[q].z + a.z * e.alpha; o.w = xv[q].w + a.w * e.alpha;
+        if (e.drop.thr) {   // training: x_out = x_in + alpha * dropout(branch)
+          const uint64_t i = (uint64_t)m * e.ldx + n;
+          o.x = xv[q].x + (e.alpha * a.x) * drop_mul(e.drop, i);
+          o.y = xv[q].y + (e.alpha * a.y) * drop_mul(e.drop, i + 1);
+          o.z = xv[q].z + (e.alpha * a.z) * drop_mul(e.drop, i + 2);
+          o.w = xv[q].w + (e.alpha * a.w) * drop_mul(e.drop, i + 3);
+        } else {
+          o.x = xv[q].x + a.x * e.alpha; o.y = xv[q].y + a.y * e.alpha;
+          o.z = xv[q].z + a.z * e.alpha; o.w = xv[q].w + a.w * e.alpha;
+        }
       } else {
         o.x = a.x * e.alpha; o.y = a.y * e.alpha; o.z = a.z * e.alpha; o.w = a.w * e.alpha;
       }

@@ -36,20 +36,6 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // dropout masks: keep(e) iff hash(seed, site, e) >= thr, thr = p * 2^32; kept values * 1/(1-p)
 // ---------------------------------------------------------------------------------------------
-struct Drop {
-  uint32_t thr;    // 0 = no dropout
-  uint32_t key;    // per (step, site)
-  float scale;     // 1 / (1 - p)
-};
-CFM_DEV uint32_t mix32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x;
-}
-CFM_DEV float drop_mul(const Drop& d, uint64_t e) {
-  if (d.thr == 0) return 1.0f;
-  const uint32_t h = mix32((uint32_t)e ^ mix32(d.key ^ (uint32_t)(e >> 32) * 0x9e3779b9u));
-  return h >= d.thr ? d.scale : 0.0f;
-}
 inline uint32_t host_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
@@ -1183,6 +1169,16 @@ struct Step {
     e.alpha = alpha;
     return e;
   }
+  // xout = xin + alpha * dropout(A . W^T + b), the dropout and residual in the GEMM epilogue
+  void gemm_resid_drop(const void* A, long lda, int M, int K, const void* Wp, int N, const float* b, float alpha,
+                       const float* xin, float* xout, long ld, Drop dr) const {
+    GemmEpi e = epi(EPI_RESID, b, alpha);
+    e.X = xout;
+    e.ldx = ld;
+    e.Xin = xin;
+    e.drop = dr;
+    gemm(g.dt, A, lda, M, K, Wp, kpad(K), N, e, h->zero_page, st);
+  }
   void gemm_f32out(const void* A, long lda, int M, int K, const void* Wp, int N, const float* b, float alpha,
                    float* X, long ldx, bool accumulate) const {
     GemmEpi e = epi(accumulate ? EPI_RESID : EPI_SCALE_F32, b, alpha);
@@ -1320,7 +1316,6 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
                            (long)M * d, dr, xcur);
   }
   const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
-  float* br = S.W_<float>(S.wl.br);
   const long n_md = (long)M * d;
 
   for (int l = 0; l < g.L; ++l) {
@@ -1363,9 +1358,8 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       else
         cfm_launch(swish_drop_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z), n, di,
                    S.W_<bf16_t>(S.wl.u));
-      S.gemm_f32out(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 1.0f, br, d, false);
-      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)xin, (const float*)br, 0.5f,
-                 n_md, S.drop(site(l, f ? 5 : 1)), xout);
+      S.gemm_resid_drop(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 0.5f, xin, xout, d,
+                        S.drop(site(l, f ? 5 : 1)));
     };
     layernorm(dt, X[0], M, d, S.prm(q.ln_w[LN_FF1]), S.prm(q.ln_b[LN_FF1]), nullptr, nullptr, nullptr, S.T_(t.hn[0]),
               0, st);
@@ -1390,9 +1384,8 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       gemm(dt, S.T_(t.hn[1]), d, M, d, S.W_(S.wl.wqkv), S.kpad(d), (int)(3 * HP), e, h->zero_page, st);
       rel_pos_attention(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B, g.Tp, H,
                         g.dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, S.T_(t.ctx), d, st);
-      S.gemm_f32out(S.T_(t.ctx), d, M, d, S.W_(S.wl.wout), d, S.W_<float>(S.wl.bout), 1.0f, br, d, false);
-      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[1], (const float*)br, 1.0f,
-                 n_md, S.drop(site(l, 2)), X[2]);
+      S.gemm_resid_drop(S.T_(t.ctx), d, M, d, S.W_(S.wl.wout), d, S.W_<float>(S.wl.bout), 1.0f, X[1], X[2], d,
+                        S.drop(site(l, 2)));
     }
 
     // ---- convolution module (conformer_modules.py:112-114, 160-180) ----
@@ -1436,9 +1429,8 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
         cfm_launch(bn_swish_kernel<bf16_t>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dwo,
                    (const float*)mean, (const float*)rstd, S.prm(q.bn_w), S.prm(q.bn_b), (long)M, d,
                    S.T_<float>(t.xhat), S.T_<bf16_t>(t.s));
-      S.gemm_f32out(S.T_(t.s), d, M, d, S.W_(S.wl.wpw2), d, S.W_<float>(S.wl.bpw2), 1.0f, br, d, false);
-      cfm_launch(resid_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)X[2], (const float*)br, 1.0f,
-                 n_md, S.drop(site(l, 3)), X[3]);
+      S.gemm_resid_drop(S.T_(t.s), d, M, d, S.W_(S.wl.wpw2), d, S.W_<float>(S.wl.bpw2), 1.0f, X[2], X[3], d,
+                        S.drop(site(l, 3)));
     }
     layernorm(dt, X[3], M, d, S.prm(q.ln_w[LN_FF2]), S.prm(q.ln_b[LN_FF2]), nullptr, nullptr, nullptr, S.T_(t.hn[3]),
               0, st);
