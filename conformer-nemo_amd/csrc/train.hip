@@ -68,36 +68,40 @@ CFM_DEV void tpack_tile(float (*tile)[65], int bx, int by, const Tin* __restrict
                         int rows_pad, int cols_pad, int ones_row, int src_vec, int dst_vec) {
   const int i0 = by * 64, j0 = bx * 64;
   const int sr0 = transpose ? j0 : i0, sc0 = transpose ? i0 : j0;
-  const int c4 = threadIdx.x & 15, r = threadIdx.x >> 4;
+  // 16-byte source loads: 4 fp32 or 8 bf16 values per thread and pass
+  constexpr int VI = sizeof(Tin) == 2 ? 8 : 4, TPR = 64 / VI, LPP = 256 / TPR;
+  const int cv = threadIdx.x % TPR, r = threadIdx.x / TPR;
 #pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    const int rr = r + 16 * pass, cc = 4 * c4;
+  for (int pass = 0; pass < 64 / LPP; ++pass) {
+    const int rr = r + LPP * pass, cc = VI * cv;
     const int si = sr0 + rr, sj = sc0 + cc;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    float v[VI];
+#pragma unroll
+    for (int e = 0; e < VI; ++e) v[e] = 0.0f;
     if (si < rows) {
       const Tin* sp = src + (long)si * src_ld + sj;
-      if (src_vec && sj + 3 < cols) {
-        if constexpr (sizeof(Tin) == 4) {
-          const float4 t = *(const float4*)sp;
-          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        } else {
-          const uint2 t = *(const uint2*)sp;
-          v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
-          v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+      if (src_vec == 2 && sj + VI - 1 < cols) {
+        Vec16<Tin>::to_f32(*(const uint4*)sp, v);
+      } else if (sizeof(Tin) == 2 && src_vec == 1 && sj + VI - 1 < cols) {   // 8-byte aligned bf16 rows
+#pragma unroll
+        for (int h = 0; h < VI / 4; ++h) {
+          const uint2 t = *(const uint2*)(sp + 4 * h);
+          v[4 * h] = __uint_as_float(t.x << 16); v[4 * h + 1] = __uint_as_float(t.x & 0xffff0000u);
+          v[4 * h + 2] = __uint_as_float(t.y << 16); v[4 * h + 3] = __uint_as_float(t.y & 0xffff0000u);
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < VI; ++e)
           if (sj + e < cols) v[e] = ld_f<Tin>(sp + e);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < VI; ++e) {
         if (fn == 1 && sj + e < cols) v[e] = swishf(v[e]) * drop_mul(drop, (uint64_t)si * cols + sj + e);
         v[e] *= scale;
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < VI; ++e) {
       if (transpose) tile[cc + e][rr] = v[e];
       else tile[rr][cc + e] = v[e];
     }
@@ -436,6 +440,31 @@ void colred(const float* src, const float* y, const float* mean, long ld, int M,
   else if (f == 1) cfm_launch(colred_partial_kernel<1>, g1, b, 0, st, src, y, mean, ld, M, N, ws);
   else cfm_launch(colred_partial_kernel<2>, g1, b, 0, st, src, y, mean, ld, M, N, ws);
   cfm_launch(colred_final_kernel, dim3((N + 15) / 16), b, 0, st, (const float*)ws, nch, N, alpha, out, accumulate);
+}
+
+// Two independent column reductions of [nchunks][N] partials in one launch (grid.y = 0, 1; a null
+// output is skipped): the LayerNorm weight and bias gradients.
+__global__ __launch_bounds__(256) void colred_final2_kernel(const float* __restrict__ p0, float* __restrict__ o0,
+                                                            const float* __restrict__ p1, float* __restrict__ o1,
+                                                            int nchunks, int N) {
+  __shared__ float red[16][17];
+  const float* partial = blockIdx.y ? p1 : p0;
+  float* out = blockIdx.y ? o1 : o0;
+  if (out == nullptr) return;
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + c;
+  const int nc = min(n, N - 1);
+  float s = 0.0f;
+#pragma unroll 8
+  for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][c];
+    out[n] = v;
+  }
 }
 
 // LayerNorm backward (eps 1e-5, biased variance; torch.nn.LayerNorm) for 4 rows per wave, 16 rows per
@@ -1071,7 +1100,9 @@ struct Step {
     const dim3 grid((cp + 63) / 64, (rp + 63) / 64), block(256);
     const int ses = (g.dt != DT_F32 && src_ct) ? 2 : 4;           // source element bytes
     const int des = g.dt == DT_F32 ? 4 : 2;
-    const int sv = (ld % 4 == 0 && ((uintptr_t)src % (4 * ses)) == 0) ? 1 : 0;
+    // 2: 16-byte source runs; 1: 8-byte (bf16) runs; 0: element loads
+    const int sv = (ld % (16 / ses) == 0 && ((uintptr_t)src % 16) == 0) ? 2
+                   : (ld % 4 == 0 && ((uintptr_t)src % (4 * ses)) == 0) ? 1 : 0;
     const int dv = (dld % (16 / des) == 0 && ((uintptr_t)dst % 16) == 0) ? 1 : 0;
     if (g.dt == DT_F32) {
       cfm_launch(tpack_kernel<float, float>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
@@ -1097,7 +1128,7 @@ struct Step {
     const int des = (f32 || g.dt == DT_F32) ? 4 : 2;
     j.src = src; j.dst = dst; j.ld_src = ld_src; j.rows = rows; j.cols = cols; j.tr = tr ? 1 : 0;
     j.ld_dst = (int)ld_dst; j.rows_pad = rp; j.cols_pad = cp; j.out_f32 = f32 ? 1 : 0;
-    j.src_vec = (ld_src % 4 == 0 && ((uintptr_t)src % 16) == 0) ? 1 : 0;
+    j.src_vec = (ld_src % 4 == 0 && ((uintptr_t)src % 16) == 0) ? 2 : 0;
     j.dst_vec = (ld_dst % (16 / des) == 0 && ((uintptr_t)dst % 16) == 0) ? 1 : 0;
     j.tiles_x = (cp + 63) / 64;
     j.tile0 = b.tiles;
@@ -1502,8 +1533,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     else if (E4 <= 2) cfm_launch(ln_bwd_fused_kernel<2>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
     else if (E4 <= 4) cfm_launch(ln_bwd_fused_kernel<4>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
     else cfm_launch(ln_bwd_fused_kernel<8>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
-    if (Gp(wi)) cfm_launch(colred_final_kernel, dim3((d + 15) / 16), blk, 0, st, (const float*)pw, nblk, d, 1.0f, Gp(wi), 0);
-    if (Gp(bi)) cfm_launch(colred_final_kernel, dim3((d + 15) / 16), blk, 0, st, (const float*)pb, nblk, d, 1.0f, Gp(bi), 0);
+    if (Gp(wi) || Gp(bi))
+      cfm_launch(colred_final2_kernel, dim3((d + 15) / 16, 2), blk, 0, st, (const float*)pw, Gp(wi), (const float*)pb,
+                 Gp(bi), nblk, d);
   };
 
   // dy (B, d, T') -> gA (B*T', d)
