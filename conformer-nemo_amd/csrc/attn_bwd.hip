@@ -140,28 +140,37 @@ __global__ __launch_bounds__(256) void bgemm2_kernel(BgArgs a) {
   // (idx = 256 q + tid).  Otherwise the thread loads a 4x4 micro-block -- 4 k rows of 4 consecutive
   // operand rows r = 4 (tid & 15) .. +3 at k = 4 (tid >> 4) .. +3 -- and transposes it in registers:
   // v[4 kk + e] holds (r + e, k + kk).
+  // Interior threads (every run in range) issue their four vector loads in one branch-free block;
+  // only threads on a tile edge take the element-wise path (a per-load condition would make hipcc
+  // wait for each load before the next, cdna_hip_programming.md §5).
   auto loadop = [&](auto* P, long sr, long sk, bool kc, int r0, int R, int k0, float* v) {
     using TS = typename std::remove_cv<typename std::remove_pointer<decltype(P)>::type>::type;
+    const bool full = kc ? (r0 + ((3 * 256 + tid) >> 4) < R && k0 + 4 * (tid & 15) + 3 < KZ)
+                         : (k0 + 4 * (tid >> 4) + 3 < KZ && r0 + 4 * (tid & 15) + 3 < R);
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (kc) {
+          const int idx = q * 256 + tid;
+          Quad<TS>::ld(P + (r0 + (idx >> 4)) * sr + k0 + 4 * (idx & 15), v + 4 * q);
+        } else {
+          Quad<TS>::ld(P + r0 + 4 * (tid & 15) + (k0 + 4 * (tid >> 4) + q) * sk, v + 4 * q);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float* o = v + 4 * q;
       if (kc) {
         const int idx = q * 256 + tid;
         const int r = r0 + (idx >> 4), k = k0 + 4 * (idx & 15);
-        if (r < R && k + 3 < KZ) {
-          Quad<TS>::ld(P + r * sr + k, o);
-        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (r < R && k + e < KZ) ? ld_f(P + r * sr + (k + e)) : 0.0f;
-        }
+        for (int e = 0; e < 4; ++e) o[e] = (r < R && k + e < KZ) ? ld_f(P + r * sr + (k + e)) : 0.0f;
       } else {
         const int r = r0 + 4 * (tid & 15), k = k0 + 4 * (tid >> 4) + q;
-        if (k < KZ && r + 3 < R) {
-          Quad<TS>::ld(P + r + k * sk, o);
-        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (r + e < R && k < KZ) ? ld_f(P + (r + e) + k * sk) : 0.0f;
-        }
+        for (int e = 0; e < 4; ++e) o[e] = (r + e < R && k < KZ) ? ld_f(P + (r + e) + k * sk) : 0.0f;
       }
     }
   };
