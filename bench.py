@@ -422,7 +422,7 @@ def run_decode(args, world, rank, dev, dist, barrier):
     from nemo.collections.asr.parts.submodules.rnnt_greedy_decoding import GreedyBatchedRNNTInfer
     torch.manual_seed(0)
     d, H, L, B, T, V = 512, 8, args.layers, 16, 1600, 1024
-    blank_bias = float(os.environ.get("BLANK_BIAS", "1.5"))
+    blank_bias = float(os.environ.get("BLANK_BIAS", "1.1"))
     enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
     enc.set_compute_mode(args.compute)
     dec = RNNTDecoder(prednet=dict(pred_hidden=640, pred_rnn_layers=1), vocab_size=V).to(dev).eval()
