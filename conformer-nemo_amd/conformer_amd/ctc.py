@@ -92,12 +92,23 @@ def ctc_loss(log_probs: torch.Tensor, targets: torch.Tensor, input_lengths: torc
     lp = log_probs.detach().to(torch.float32).contiguous()
     B, T, C = lp.shape
     dev = lp.device
-    tg = targets.to(device=dev, dtype=torch.int32).contiguous()
+    tl = target_lengths.to(device=dev, dtype=torch.int32).contiguous()
+    tg = targets.to(device=dev, dtype=torch.int32)
     if tg.dim() == 1:
-        tg = tg.view(B, -1)
+        # torch's 1-D form: the utterances' targets concatenated (length sum(target_lengths)) ->
+        # padded (B, max(target_lengths)) through the cumulative offsets
+        tl64 = tl.to(torch.int64)
+        U1 = int(tl64.max().item()) if B > 0 else 0
+        if tg.numel() != int(tl64.sum().item()):
+            raise ValueError(f"1-D targets hold {tg.numel()} labels but target_lengths sum to {int(tl64.sum())}")
+        start = torch.cumsum(tl64, 0) - tl64
+        col = torch.arange(max(U1, 1), device=dev, dtype=torch.int64)
+        idx = (start[:, None] + col[None, :]).clamp_(max=max(tg.numel() - 1, 0))
+        tg = torch.where(col[None, :] < tl64[:, None], tg[idx] if tg.numel() else torch.zeros_like(idx, dtype=torch.int32),
+                         torch.zeros((), dtype=torch.int32, device=dev))[:, :U1]
+    tg = tg.contiguous()
     U = tg.shape[1]
     il = input_lengths.to(device=dev, dtype=torch.int32).contiguous()
-    tl = target_lengths.to(device=dev, dtype=torch.int32).contiguous()
     nll = torch.empty(B, dtype=torch.float32, device=dev)
     grad = torch.empty_like(lp) if want_grad else None
     n = lib.cfm_ctc_loss_workspace_size(B, T, C, U)

@@ -105,6 +105,10 @@ class NativeEncoder:
     def set_max_audio_length(self, n: int) -> None:
         _lib.check(self.lib.cfm_encoder_set_max_audio_length(self.handle, int(n)), "set_max_audio_length")
 
+    def set_pad_mask(self, on: bool) -> None:
+        """enable_pad_mask (conformer_encoder.py:301-305): off -> conv module runs with pad_mask=None."""
+        _lib.check(self.lib.cfm_encoder_set_pad_mask(self.handle, 1 if on else 0), "set_pad_mask")
+
     def set_microbatches(self, n: int) -> None:
         """Split each forward's batch over up to n concurrent streams (bitwise-identical results)."""
         _lib.check(self.lib.cfm_encoder_set_microbatches(self.handle, int(n)), "set_microbatches")

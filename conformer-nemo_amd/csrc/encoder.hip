@@ -632,7 +632,7 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
       {
         TM(ST_PW1);
         GemmEpi e = epi_of(EPI_GLU_MASK, Wf(Lw.pw1_b));
-        e.C = ws + wl.G; e.ldc = d; e.lens = lens; e.Tp = Tp;
+        e.C = ws + wl.G; e.ldc = d; e.lens = h->use_pad_mask ? lens : nullptr; e.Tp = Tp;
         gemm(dt, Hn, d, M, d, W(Lw.pw1_w), (int)h->kpad(d), d, e, h->zero_page, st);
         TM(ST_DWCONV);
         if (h->cfg.conv_norm_type == 0) {
@@ -743,6 +743,13 @@ cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t
     if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
     if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
     run_split(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream);
+  });
+}
+
+cfm_status cfm_encoder_set_pad_mask(cfm_encoder* h, int on) {
+  return guarded([&] {
+    if (!h) fail(CFM_ERR_INVALID_ARG, "null handle");
+    h->use_pad_mask = on != 0;
   });
 }
 

@@ -244,7 +244,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     const int c = n0 / 2 + oc_local;                 // output channel
     int lenq[NP];
 #pragma unroll
-    for (int q = 0; q < NP; ++q) lenq[q] = e.lens[min(m0 + r0 + q * RPP, p.M - 1) / e.Tp];
+    for (int q = 0; q < NP; ++q) lenq[q] = e.lens ? e.lens[min(m0 + r0 + q * RPP, p.M - 1) / e.Tp] : e.Tp;
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;

@@ -37,6 +37,20 @@ from nemo.core.classes import Exportable
 from nemo.core.classes.module import NeuralModule
 from nemo.core.neural_types import AcousticEncodedRepresentation, LengthsType, NeuralType, SpectrogramType
 
+# Structural generation: bumped whenever any module registers or replaces a parameter or buffer
+# (torch's global registration hooks), and by ConformerEncoder.load_state_dict / _apply.  The
+# encoder's cached parameter list is rebuilt only when it changes.
+_STRUCT_GEN = [0]
+
+
+def _bump_struct_gen(*_args):
+    _STRUCT_GEN[0] += 1
+
+
+nn.modules.module.register_module_parameter_registration_hook(_bump_struct_gen)
+nn.modules.module.register_module_buffer_registration_hook(_bump_struct_gen)
+nn.modules.module.register_module_module_registration_hook(_bump_struct_gen)
+
 __all__ = ["ConformerEncoder"]
 
 
@@ -150,7 +164,26 @@ class ConformerEncoder(NeuralModule, Exportable):
 
     # ---- native plumbing -----------------------------------------------------------------------
     def _weight_tensors(self):
-        return {k: v for k, v in self.state_dict(keep_vars=True).items() if torch.is_floating_point(v)}
+        """Name -> tensor of every floating-point parameter / buffer, cached: the state_dict walk
+        (~3.4 ms at Large-17) runs only after a structural change (a parameter or buffer registered
+        or replaced anywhere, load_state_dict, .to()/.cuda()); each forward then checks only the
+        (data_ptr, _version) pairs of the cached tensors (~0.2 ms)."""
+        gen = _STRUCT_GEN[0]
+        cache = self.__dict__.get("_wcache")
+        if cache is None or cache[0] != gen:
+            tensors = {k: v for k, v in self.state_dict(keep_vars=True).items() if torch.is_floating_point(v)}
+            cache = (gen, tensors, tuple(tensors.values()))
+            self.__dict__["_wcache"] = cache
+        return cache[1]
+
+    def _weight_version(self):
+        self._weight_tensors()
+        return tuple((t.data_ptr(), t._version) for t in self.__dict__["_wcache"][2])
+
+    def load_state_dict(self, *args, **kwargs):
+        _STRUCT_GEN[0] += 1
+        self._native_versions = {}
+        return super().load_state_dict(*args, **kwargs)
 
     def _native_for(self, device: torch.device):
         from conformer_amd import NativeEncoder, make_cfg
@@ -164,7 +197,7 @@ class ConformerEncoder(NeuralModule, Exportable):
                     enc.set_max_audio_length(self.max_audio_length)
             self._native[key] = enc
         tensors = self._weight_tensors()
-        version = tuple((t.data_ptr(), t._version) for t in tensors.values())
+        version = self._weight_version()
         if self._native_versions.get(key) != version:
             with torch.cuda.device(key[0]):
                 enc.set_weights(tensors)
@@ -209,6 +242,7 @@ class ConformerEncoder(NeuralModule, Exportable):
         return y, ylen
 
     def _apply(self, fn, *args, **kwargs):
+        _STRUCT_GEN[0] += 1
         self._native_versions = {}
         return super()._apply(fn, *args, **kwargs)
 
@@ -220,11 +254,17 @@ class ConformerEncoder(NeuralModule, Exportable):
 
     @typecheck()
     def forward_for_export(self, audio_signal, length=None):
-        if not self.use_pad_mask:
-            raise NotImplementedError("enable_pad_mask(False) is not supported by the native path")
         if not audio_signal.is_cuda:
             raise RuntimeError("ConformerEncoder (MI355X-native) expects audio_signal on a ROCm GPU")
         if self.training:
+            if not self.use_pad_mask:
+                raise NotImplementedError("enable_pad_mask(False) is an inference switch (conformer_encoder.py:301-302); "
+                                          "the native training step always applies the pad mask")
             return self._train_forward(audio_signal, length)
+        if torch.is_grad_enabled() and audio_signal.requires_grad:
+            # eval-mode native forward builds no autograd graph: refuse rather than drop upstream gradients
+            raise RuntimeError("ConformerEncoder eval forward does not propagate gradients to audio_signal; "
+                               "use .train() for the differentiable native path or torch.no_grad() for inference")
         enc = self._native_for(audio_signal.device)
+        enc.set_pad_mask(self.use_pad_mask)
         return enc.forward(audio_signal, length)

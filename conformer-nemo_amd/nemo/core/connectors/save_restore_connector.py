@@ -181,6 +181,24 @@ _BLOCKS = (("preprocessor", "preprocessor"), ("spec_augmentation", "spec_augment
            ("decoder", "decoder"), ("joint", "joint"))
 
 
+# `_target_` values restore_modules will instantiate: the drop-in modules this package provides
+# under the reference's import paths (and nothing else — a .nemo config is untrusted input).
+RESTORABLE_TARGETS = frozenset({
+    "nemo.collections.asr.modules.ConformerEncoder",
+    "nemo.collections.asr.modules.conformer_encoder.ConformerEncoder",
+    "nemo.collections.asr.modules.AudioToMelSpectrogramPreprocessor",
+    "nemo.collections.asr.modules.audio_preprocessing.AudioToMelSpectrogramPreprocessor",
+    "nemo.collections.asr.modules.SpectrogramAugmentation",
+    "nemo.collections.asr.modules.audio_preprocessing.SpectrogramAugmentation",
+    "nemo.collections.asr.modules.ConvASRDecoder",
+    "nemo.collections.asr.modules.conv_asr.ConvASRDecoder",
+    "nemo.collections.asr.modules.RNNTDecoder",
+    "nemo.collections.asr.modules.rnnt.RNNTDecoder",
+    "nemo.collections.asr.modules.RNNTJoint",
+    "nemo.collections.asr.modules.rnnt.RNNTJoint",
+})
+
+
 def _subdict(sd: Dict[str, torch.Tensor], prefix: str) -> Dict[str, torch.Tensor]:
     p = prefix + "."
     return {k[len(p):]: v for k, v in sd.items() if k.startswith(p)}
@@ -193,7 +211,7 @@ def restore_modules(restore_path: str, map_location=None, strict: bool = True,
     Returns (conf, modules) with modules keyed by the reference model's attribute names.  Blocks
     whose `_target_` this package does not provide (e.g. an LSTM `RNNTDecoder`) are skipped, and
     their weights stay in the checkpoint untouched."""
-    from nemo.core.classes.common import Serialization
+    from nemo.core.classes.common import Serialization, _locate
 
     conn = connector or SaveRestoreConnector()
     conf, sd = conn.load_config_and_state_dict(restore_path, map_location="cpu")
@@ -209,10 +227,21 @@ def restore_modules(restore_path: str, map_location=None, strict: bool = True,
                 block["feat_in"] = mods["encoder"]._feat_out
             if block.get("num_classes", 0) < 1 and block.get("vocabulary") is not None:
                 block["num_classes"] = len(block["vocabulary"])
+        target = block.get("_target_")
+        if target not in RESTORABLE_TARGETS:
+            # Only this package's drop-in classes are ever instantiated from a checkpoint's config:
+            # an arbitrary `_target_` (e.g. a function of the standard library) is never resolved.
+            if strict and target is not None and str(target).split(".")[0] != "nemo":
+                raise ValueError(f"refusing to instantiate {attr}._target_={target!r} from {restore_path}: "
+                                 f"not one of this package's drop-in modules")
+            continue
         try:
-            m = Serialization.from_config_dict(block)
+            klass = _locate(target)
         except (ImportError, AttributeError, ModuleNotFoundError):
             continue                                   # not a drop-in of this package
+        if not (isinstance(klass, type) and issubclass(klass, torch.nn.Module)):
+            raise ValueError(f"{attr}._target_={target!r} does not name an nn.Module")
+        m = Serialization.from_config_dict(block)
         sub = _subdict(sd, attr)
         if sub or strict:
             m.load_state_dict(sub, strict=strict)

@@ -97,6 +97,11 @@ int64_t cfm_encoder_param_numel(const cfm_encoder* h, int i);
 cfm_status cfm_encoder_set_max_audio_length(cfm_encoder* h, int max_audio_length);
 int cfm_encoder_max_audio_length(const cfm_encoder* h);
 
+/* enable_pad_mask (conformer_encoder.py:301-305): on = 0 runs the layers with pad_mask = None, i.e.
+ * the convolution module does not zero padded frames after the GLU (conformer_modules.py:165-166);
+ * the attention mask is unchanged.  Default on. */
+cfm_status cfm_encoder_set_pad_mask(cfm_encoder* h, int on);
+
 /* Micro-batch concurrency (default 2, env CFM_MICROBATCH): the batch is split into up to n parts
  * (each >= 4 utterances) that run on library-owned streams forked from / joined into `stream`.
  * Outputs are bitwise identical for any n. */

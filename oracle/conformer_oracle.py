@@ -279,6 +279,8 @@ def encoder_forward(x_bft: np.ndarray, lengths: Optional[np.ndarray], sd: Dict[s
     x, pos_emb = rel_positional_encoding(x, pe, center, xscale)
     Tp = x.shape[1]
     pad_mask, att_mask = make_masks(Tp, lengths, cfg.get("att_context_size") or (-1, -1))
+    if not cfg.get("use_pad_mask", True):   # enable_pad_mask(False): pad_mask = None (conformer_encoder.py:269-272)
+        pad_mask = None
     for i in range(cfg["n_layers"]):
         x = conformer_layer(x, att_mask, pos_emb, pad_mask, sd, f"layers.{i}.", cfg["n_heads"],
                             cfg.get("conv_norm_type", "batch_norm"))

@@ -103,3 +103,21 @@ def test_dropin_decoder_and_loss_modules():
     assert rel_l2(enc.grad.cpu().numpy(), z["grad_enc"]) <= 1e-4
     assert rel_l2(dec.decoder_layers[0].weight.grad.cpu().numpy()[:, :, 0], z["grad_w"]) <= 1e-4
     assert rel_l2(dec.decoder_layers[0].bias.grad.cpu().numpy(), z["grad_b"]) <= 1e-4
+
+
+@pytest.mark.parametrize("path", CASES, ids=[os.path.basename(p)[:-4] for p in CASES])
+def test_ctc_loss_concatenated_targets(path):
+    """torch's 1-D target form (utterances' labels concatenated, length sum(target_lengths)) gives
+    the same losses and gradients as the padded (B, U) form (no silent reshape)."""
+    from conformer_amd.ctc import ctc_loss
+    z = np.load(path)
+    tg, tl = z["targets"], z["tgt_len"]
+    flat = np.concatenate([tg[b, :tl[b]] for b in range(tg.shape[0])]).astype(tg.dtype)
+    args = (_t(z["in_len"]), _t(tl), int(z["blank"]), True)
+    nll, grad = ctc_loss(_t(z["log_probs"]), _t(tg), *args)
+    nll1, grad1 = ctc_loss(_t(z["log_probs"]), _t(flat), *args)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(nll.cpu().numpy(), nll1.cpu().numpy())
+    np.testing.assert_array_equal(grad.cpu().numpy(), grad1.cpu().numpy())
+    with pytest.raises(ValueError):
+        ctc_loss(_t(z["log_probs"]), _t(flat[:-1]), *args)

@@ -29,8 +29,11 @@ _CFG_KEYS = ("feat_out", "subsampling_conv_channels", "ff_expansion_factor", "at
 def native(cfg, compute):
     from conformer_amd import NativeEncoder, make_cfg
     kw = {k: cfg[k] for k in _CFG_KEYS if k in cfg}
-    return NativeEncoder(make_cfg(cfg.get("feat_in", 80), cfg["n_layers"], cfg["d_model"], n_heads=cfg["n_heads"], **kw),
-                         compute=compute)
+    enc = NativeEncoder(make_cfg(cfg.get("feat_in", 80), cfg["n_layers"], cfg["d_model"], n_heads=cfg["n_heads"], **kw),
+                        compute=compute)
+    if not cfg.get("use_pad_mask", True):   # enable_pad_mask(False) golden (enc_tiny_nopadmask)
+        enc.set_pad_mask(False)
+    return enc
 
 
 def run(enc, sd, x, lens):
@@ -144,3 +147,35 @@ def test_dropin_module_forward():
         enc.layers[-1].norm_out.weight.mul_(1.5)
     y2, _ = enc(audio_signal=x, length=ln)
     assert rel_l2(y2.cpu().numpy(), z["y"]) > 1e-3
+    # a Parameter object replaced (not updated in place): the cached weight list is rebuilt
+    w = enc.layers[-1].norm_out.weight
+    enc.layers[-1].norm_out.weight = torch.nn.Parameter(w.detach() / 1.5)
+    y3, _ = enc(audio_signal=x, length=ln)
+    check(y3.cpu().numpy(), z["y"], "fp32")
+    # eval forward on an input that wants gradients refuses instead of silently dropping them
+    with pytest.raises(RuntimeError):
+        enc(audio_signal=x.clone().requires_grad_(True), length=ln)
+
+
+def test_dropin_enable_pad_mask():
+    """enable_pad_mask(False) (conformer_encoder.py:301-305) through the drop-in module against the
+    reference run with the pad mask disabled (enc_tiny_nopadmask); switching back restores it."""
+    from nemo.collections.asr.modules import ConformerEncoder
+    z = np.load(os.path.join(GOLDEN, "enc_tiny_nopadmask.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(feat_in=80, n_layers=cfg["n_layers"], d_model=cfg["d_model"], n_heads=cfg["n_heads"])
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref_sd = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref_sd[k].shape) for k, v in sd.items()})
+    enc = enc.cuda().eval()
+    enc.set_compute_mode("fp32")
+    x, ln = torch.from_numpy(z["x"]).cuda(), torch.from_numpy(z["lengths"]).cuda()
+    assert enc.enable_pad_mask(False) is True
+    with torch.no_grad():
+        y, _ = enc(audio_signal=x, length=ln)
+    check(y.cpu().numpy(), z["y"], "fp32")
+    enc.enable_pad_mask(True)
+    with torch.no_grad():
+        y2, _ = enc(audio_signal=x, length=ln)
+    yr, _ = O.encoder_forward(z["x"], z["lengths"], sd, dict(cfg, use_pad_mask=True))
+    check(y2.cpu().numpy(), yr, "fp32")

@@ -144,3 +144,21 @@ def test_restored_encoder_reproduces_reference_outputs(tmp_path):
     y, yl = enc(audio_signal=torch.from_numpy(z["x"]).cuda(), length=torch.from_numpy(z["lengths"]).cuda())
     assert rel_l2(y.cpu().numpy(), z["y"]) < 1e-3
     np.testing.assert_array_equal(yl.cpu().numpy(), z["y_len"])
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_restore_refuses_foreign_targets(tmp_path, strict):
+    """A .nemo config is untrusted input: a `_target_` outside this package's drop-in modules is
+    never resolved or called (subprocess.getoutput as an encoder target)."""
+    from nemo.core.connectors import SaveRestoreConnector, restore_modules
+    marker = tmp_path / "pwned_marker"
+    cfg = {"model": {"encoder": {"_target_": "subprocess.getoutput", "cmd": f"touch {marker}"}}}
+    path = str(tmp_path / "evil.nemo")
+    SaveRestoreConnector().save_to(cfg, {}, path)
+    if strict:
+        with pytest.raises(ValueError, match="refusing"):
+            restore_modules(path, strict=True)
+    else:
+        _, mods = restore_modules(path, strict=False)
+        assert "encoder" not in mods
+    assert not marker.exists()
