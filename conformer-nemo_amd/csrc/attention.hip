@@ -19,6 +19,7 @@
 // probabilities (the -10000-filled entries underflow to 0 in fp32); rows i >= len are fully masked
 // in the reference, whose probabilities are then zeroed (:107) -> their output is exactly 0.
 #include <cstdlib>
+#include <stdexcept>
 
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -38,6 +39,10 @@ struct AttnParams {
   int ctx_left, ctx_right;
   // (q + u), (q + v) arrive pre-scaled by log2(e)/sqrt(dk): scores are in log2 units
   char* out; long ldo;
+  // natural layout (bf16 LDS kernel only): qk rows are [q | k | v] as the QKV GEMM stores them
+  // (bias added, heads padded to dkp); the kernel forms (q + u)*c, (q + v)*c itself from `uv`
+  // ([u | v], fp32, H*dkp each) and transposes V into its LDS image while staging.
+  const float* uv; float qscale;
 };
 
 constexpr int BDS = 32;   // fp32 row stride of the 64x32 BD^T image (conflict-free skewed reads)
@@ -326,7 +331,7 @@ CFM_DEV_HOST_INLINE LdsGeom lds_geom(int Tp, int dkp, int vt_rows, int nw) {
 
 // PF: prefetch the next key tile's P rows into registers (8*NS VGPRs; with NW = 8, two waves per
 // SIMD must fit 256 registers: on for dk <= 64).
-template <int NS, int ND, int NW, bool PF>
+template <int NS, int ND, int NW, bool PF, bool QN>
 __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   using T = bf16_t;
   constexpr int SE = 16;
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
     constexpr int BATCH = 8;
     const int kchunks = p.dkp / 8;                          // 16-byte chunks per K row
     const int kn = g.tp32 * kchunks;
-    const T* kbase = qk + rowbase * p.ldqk + (long)(2 * p.H + h) * p.dkp;
+    const T* kbase = qk + rowbase * p.ldqk + (long)((QN ? 1 : 2) * p.H + h) * p.dkp;
     for (int i0 = tid; i0 < kn; i0 += NW * 64 * BATCH) {
       uint4 v[BATCH];
 #pragma unroll
@@ -368,6 +373,43 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
         if (i < kn) *(uint4*)(Ks + r * g.ks + c * 16) = r < Tp ? v[u] : make_uint4(0, 0, 0, 0);
       }
     }
+    if constexpr (QN) {
+      // V rows [t][dd] -> LDS Vs[dd][t]: a job = 2 consecutive keys x 8 channels (two 16-byte row
+      // loads) -> 8 dwords, one per channel row, holding the key pair.  Consecutive lanes take
+      // consecutive key pairs, so each ds_write_b32 wave-instruction covers one channel row's
+      // consecutive dwords (conflict-free).  Keys >= T' and channels >= dkp are zero.
+      const T* vbase = qk + rowbase * p.ldqk + (long)(2 * p.H + h) * p.dkp;
+      const int npair = g.tp32 / 2, nchunk = p.vt_rows / 8;
+      const int vn = npair * nchunk;
+      for (int i0 = tid; i0 < vn; i0 += NW * 64 * (BATCH / 2)) {
+        uint4 va[BATCH / 2], vb[BATCH / 2];
+#pragma unroll
+        for (int u = 0; u < BATCH / 2; ++u) {
+          const int i = min(i0 + u * NW * 64, vn - 1);
+          const int c = i / npair, tp = i - c * npair;
+          const int t0 = min(2 * tp, Tp - 1), t1 = min(2 * tp + 1, Tp - 1), cc = min(c, p.dkp / 8 - 1);
+          va[u] = *(const uint4*)(vbase + (long)t0 * p.ldqk + cc * 8);
+          vb[u] = *(const uint4*)(vbase + (long)t1 * p.ldqk + cc * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < BATCH / 2; ++u) {
+          const int i = i0 + u * NW * 64;
+          if (i >= vn) continue;
+          const int c = i / npair, tp = i - c * npair;
+          const bool ok_c = c < p.dkp / 8;
+          const uint32_t ma = (ok_c && 2 * tp < Tp) ? 0x0000ffffu : 0u;
+          const uint32_t mb = (ok_c && 2 * tp + 1 < Tp) ? 0xffff0000u : 0u;
+          const uint32_t wa[4] = {va[u].x, va[u].y, va[u].z, va[u].w};
+          const uint32_t wb[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
+          char* dst = Vs + (c * 8) * g.vs + tp * 4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            *(uint32_t*)(dst + (2 * e) * g.vs) = ((wa[e] & 0xffffu) & ma) | ((wb[e] << 16) & mb);
+            *(uint32_t*)(dst + (2 * e + 1) * g.vs) = ((wa[e] >> 16) & ma) | ((wb[e] & 0xffff0000u) & mb);
+          }
+        }
+      }
+    } else {
     const T* vt_head = (const T*)p.Vt + ((long)b * p.H + h) * p.vt_rows * p.Tpad;
     const int vchunks = g.tp32 / 4;                         // 8-byte chunks (4 keys) per Vt row
     const int vn = p.vt_rows * vchunks;
@@ -392,6 +434,7 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
         if (i < vn) *(uint2*)(Vs + r * g.vs + c * 8) = w;
       }
     }
+    }
   }
   __syncthreads();
 
@@ -402,11 +445,29 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
     {
       const int i = min(i0 + col, Tp - 1);
       const T* qrow = qk + (rowbase + i) * p.ldqk + (long)h * p.dkp;
+      if constexpr (QN) {
+        const float* ub = p.uv + h * p.dkp;
+        const float* vb = p.uv + (long)p.H * p.dkp + h * p.dkp;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int d0 = s * SE + hsel * (SE / 2);
-        qu[s] = *(const uint4*)(qrow + d0);
-        qv[s] = *(const uint4*)(qrow + (long)p.H * p.dkp + d0);
+        for (int s = 0; s < NS; ++s) {
+          const int d0 = s * SE + hsel * (SE / 2);
+          float q[8], a[8], c[8];
+          Vec16<bf16_t>::to_f32(*(const uint4*)(qrow + d0), q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            a[e] = (q[e] + ub[d0 + e]) * p.qscale;
+            c[e] = (q[e] + vb[d0 + e]) * p.qscale;
+          }
+          qu[s] = Vec16<bf16_t>::from_f32(a);
+          qv[s] = Vec16<bf16_t>::from_f32(c);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const int d0 = s * SE + hsel * (SE / 2);
+          qu[s] = *(const uint4*)(qrow + d0);
+          qv[s] = *(const uint4*)(qrow + (long)p.H * p.dkp + d0);
+        }
       }
     }
     f32x16 o[ND];
@@ -503,15 +564,15 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
 
 // launches the LDS-resident kernel if its image fits; returns false otherwise.  8 waves per block
 // (one 32-query tile each at T' <= 256, two waves per SIMD) when the image fits, else 4.
-template <int NS>
+template <int NS, bool QN>
 bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   constexpr int DKP = NS * 16;
   constexpr int ND = (DKP + 31) / 32;
   constexpr int LDS_MAX = 160 * 1024;
   static bool attr_set = [] {
-    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4, true>,
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 4, true, QN>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 8, (NS <= 4)>,
+    (void)hipFuncSetAttribute((const void*)rel_attn_lds_kernel<NS, ND, 8, (NS <= 4), QN>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     return true;
   }();
@@ -520,14 +581,19 @@ bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
   const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
   if (force_nw != 4 && g8.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, (NS <= 4)>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, (NS <= 4), QN>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
     return true;
   }
   if (g4.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 4, true>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 4, true, QN>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
     return true;
   }
   return false;
+}
+
+bool lds_path_fits(int Tp, int dkp) {
+  const int vt_rows = (dkp + 31) / 32 * 32;
+  return lds_geom(Tp, dkp, vt_rows, 4).bytes <= 160 * 1024;
 }
 
 template <typename T, int NS>
@@ -565,11 +631,45 @@ void launch_t(const AttnParams& p, dim3 grid, hipStream_t st) {
 
 }  // namespace
 
+bool attn_natural_layout(int dtype, int Tp, int dkp) {
+  static const bool lds_ok = [] { const char* s = getenv("CFM_ATTN_STREAM"); return !(s && atoi(s)); }();
+  static const bool nat_ok = [] { const char* s = getenv("CFM_ATTN_NATURAL"); return !(s && !atoi(s)); }();
+  if (dtype != DT_BF16 || !lds_ok || !nat_ok) return false;
+  if (dkp != 16 && dkp != 32 && dkp != 48 && dkp != 64 && dkp != 128) return false;
+  return lds_path_fits(Tp, dkp);
+}
+
+void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, float qscale, const void* P, long ldp,
+                               const int32_t* lens, int B, int Tp, int H, int dk, int dkp, int ctx_left,
+                               int ctx_right, void* out, long ldo, hipStream_t st) {
+  if (B <= 0 || Tp <= 0) return;
+  AttnParams p;
+  p.qk = (const char*)qkv; p.ldqk = ldqkv;
+  p.Vt = nullptr; p.vt_rows = (dkp + 31) / 32 * 32; p.Tpad = 0;
+  p.P = (const char*)P; p.ldp = ldp;
+  p.lens = lens;
+  p.Tp = Tp; p.H = H; p.dk = dk; p.dkp = dkp;
+  p.ctx_left = ctx_left; p.ctx_right = ctx_right;
+  p.out = (char*)out; p.ldo = ldo;
+  p.uv = uv; p.qscale = qscale;
+  bool done = false;
+  switch (dkp) {
+    case 16: done = launch_lds<1, true>(p, B, st); break;
+    case 32: done = launch_lds<2, true>(p, B, st); break;
+    case 48: done = launch_lds<3, true>(p, B, st); break;
+    case 64: done = launch_lds<4, true>(p, B, st); break;
+    case 128: done = launch_lds<8, true>(p, B, st); break;
+    default: break;
+  }
+  if (!done) throw std::runtime_error("rel_pos_attention_natural: shape does not fit the LDS kernel");
+}
+
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
                        long ldp, const int32_t* lens, int B, int Tp, int H,
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
   AttnParams p;
+  p.uv = nullptr; p.qscale = 1.0f;
   p.qk = (const char*)qk; p.ldqk = ldqk;
   p.Vt = (const char*)Vt; p.vt_rows = vt_rows; p.Tpad = Tpad;
   p.P = (const char*)P; p.ldp = ldp;
@@ -586,11 +686,11 @@ void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int
   if (lds_ok) {
     bool done = false;
     switch (dkp) {
-      case 16: done = launch_lds<1>(p, B, st); break;
-      case 32: done = launch_lds<2>(p, B, st); break;
-      case 48: done = launch_lds<3>(p, B, st); break;
-      case 64: done = launch_lds<4>(p, B, st); break;
-      case 128: done = launch_lds<8>(p, B, st); break;
+      case 16: done = launch_lds<1, false>(p, B, st); break;
+      case 32: done = launch_lds<2, false>(p, B, st); break;
+      case 48: done = launch_lds<3, false>(p, B, st); break;
+      case 64: done = launch_lds<4, false>(p, B, st); break;
+      case 128: done = launch_lds<8, false>(p, B, st); break;
       default: break;
     }
     if (done) return;

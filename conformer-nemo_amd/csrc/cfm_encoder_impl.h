@@ -36,7 +36,7 @@ struct cfm_encoder {
   char* pe = nullptr;
   int max_len = 0;
   // micro-batch concurrency: the batch is split into `microbatches` parts run on their own streams
-  int microbatches = 2;
+  int microbatches = 1;
   // enable_pad_mask (conformer_encoder.py:301-305): false -> the conv module's GLU output is not
   // zeroed at padded frames (pad_mask=None, conformer_modules.py:165-166); attention masks stay.
   bool use_pad_mask = true;

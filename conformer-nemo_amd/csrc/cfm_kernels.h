@@ -129,6 +129,14 @@ void transpose_out(const float* X, int B, int Tp, int d, float* y_bdt, hipStream
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
                        long ldp, const int32_t* lens, int B, int Tp, int H,
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
+// Natural-layout variant (bf16, LDS-resident kernel; attn_natural_layout() says when it applies):
+// qkv rows are [q | k | v] exactly as a plain bias GEMM stores them (heads padded to dkp); uv =
+// [pos_bias_u | pos_bias_v] (fp32, H*dkp each); the kernel forms (q+u)*qscale, (q+v)*qscale and
+// transposes V while staging it into LDS.
+bool attn_natural_layout(int dtype, int Tp, int dkp);
+void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, float qscale, const void* P, long ldp,
+                               const int32_t* lens, int B, int Tp, int H, int dk, int dkp, int ctx_left,
+                               int ctx_right, void* out, long ldo, hipStream_t st);
 // q, k, v (M, H*dk), p (2T'-1, H*dk) in the compute type -> the qk / Vt / P layouts above, at ws,
 // ws + qk_bytes, ws + qk_bytes + vt_bytes (what the QKV and pos GEMM epilogues write in the encoder).
 void attn_relayout(int dt, const void* q, const void* k, const void* v, const void* p, const float* pos_u,

@@ -610,7 +610,17 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
       // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
       TM(ST_LN);
       layernorm(dt, X, M, d, Wf(Lw.ln_w[1]), Wf(Lw.ln_b[1]), nullptr, nullptr, nullptr, Hn, 0, st);
-      {
+      if (attn_natural_layout(dt, Tp, dkp)) {
+        // plain bias GEMM into [q | k | v]; the attention kernel adds u / v, scales and transposes V
+        TM(ST_QKV);
+        GemmEpi e = epi_of(EPI_STORE, Wf(Lw.qkv_b));
+        e.C = ws + wl.QK; e.ldc = 3L * H * dkp;
+        gemm(dt, Hn, d, M, d, W(Lw.qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
+        TM(ST_ATTN);
+        rel_pos_attention_natural(ws + wl.QK, 3L * H * dkp, Wf(Lw.uv), attn_qscale(h->dk),
+                                  Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk, dkp,
+                                  h->cfg.att_context_left, h->cfg.att_context_right, ws + wl.O, d, st);
+      } else {
         TM(ST_QKV);
         GemmEpi e = epi_of(EPI_QKV, Wf(Lw.qkv_b));
         e.C = ws + wl.QK; e.ldc = 3L * H * dkp; e.qk_cols = 2 * H * dkp; e.uv = Wf(Lw.uv);
@@ -621,6 +631,8 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         rel_pos_attention(dt, ws + wl.QK, 3L * H * dkp, ws + wl.Vt, h->vt_rows, wl.Tpad,
                           Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk,
                           dkp, h->cfg.att_context_left, h->cfg.att_context_right, ws + wl.O, d, st);
+      }
+      {
         TM(ST_OUTPROJ);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.out_b), 1.0f);
         r.X = X; r.ldx = d;
@@ -908,8 +920,30 @@ extern "C" cfm_status cfm_op_rel_attention(int dtype, const void* q, const void*
     const long qk_bytes = round_up(M * 3 * H * dkp * es, 256);
     const long vt_bytes = round_up((long)B * H * vt_rows * Tpad * es, 256);
     hipStream_t st = (hipStream_t)stream;
-    attn_relayout(dt, q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
     char* w = (char*)ws;
+    if (attn_natural_layout(dt, Tp, dkp)) {
+      // the encoder's bf16 layout: [q | k | v] rows (heads padded), [u | v] fp32, P padded
+      const long ld = 3L * H * dkp;
+      const dim3 g(1024), b(256);
+      bf16_t* QKV = (bf16_t*)w;
+      float* UV = (float*)(w + qk_bytes);
+      bf16_t* P = (bf16_t*)(w + qk_bytes + vt_bytes);
+      cfm_launch(pad_heads_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)q, M, H, dk, dkp, QKV, ld, (const float*)nullptr, 1.0f);
+      cfm_launch(pad_heads_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)k, M, H, dk, dkp, QKV + (long)H * dkp, ld,
+                 (const float*)nullptr, 1.0f);
+      cfm_launch(pad_heads_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)v, M, H, dk, dkp, QKV + 2L * H * dkp, ld,
+                 (const float*)nullptr, 1.0f);
+      cfm_launch(pad_heads_kernel<float>, g, b, 0, st, pos_u, 1L, H, dk, dkp, UV, (long)H * dkp, (const float*)nullptr, 1.0f);
+      cfm_launch(pad_heads_kernel<float>, g, b, 0, st, pos_v, 1L, H, dk, dkp, UV + (long)H * dkp, (long)H * dkp,
+                 (const float*)nullptr, 1.0f);
+      cfm_launch(pad_heads_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)p, 2L * Tp - 1, H, dk, dkp, P, (long)H * dkp,
+                 (const float*)nullptr, 1.0f);
+      rel_pos_attention_natural(QKV, ld, UV, attn_qscale(dk), P, (long)H * dkp, lens, B, Tp, H, dk, dkp, ctx_left,
+                                ctx_right, out, (long)H * dk, st);
+      HIP_OK(hipGetLastError());
+      return;
+    }
+    attn_relayout(dt, q, k, v, p, pos_u, pos_v, B, Tp, H, dk, dkp, vt_rows, Tpad, (char*)ws, qk_bytes, vt_bytes, st);
     rel_pos_attention(dt, w, 3L * H * dkp, w + qk_bytes, vt_rows, Tpad, w + qk_bytes + vt_bytes, (long)H * dkp, lens,
                       B, Tp, H, dk, dkp, ctx_left, ctx_right, out, (long)H * dk, st);
     HIP_OK(hipGetLastError());

@@ -21,6 +21,9 @@
 // Epilogue: the fp32 accumulators are staged through LDS and written back row-major with 16-byte
 // vector accesses (bias, activation, GLU, residual read-modify-write all vectorised).
 #include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
 #include <cstdlib>
 #include <type_traits>
 
@@ -38,10 +41,13 @@ namespace {
 //   One glds wave-instruction fills 1 KiB = RPI rows x BK bytes; the 16-byte slots of a row are
 //   XOR-swizzled by (row / (16 / SLOTS)) % SLOTS so each 16-lane ds_read_b128 group hits 16
 //   distinct bank positions.
-template <int BM_, int BN_, int WM_, int WN_, int NS_, int EP_ = 1, int BK_ = 128>
+// KG_ = K-groups: the block's waves form KG groups of WM x WN that split every K-step's 32-byte
+// substeps between them (2 waves per SIMD on a 4-wave output tiling); the groups' accumulators
+// are summed through the LDS image before the epilogue (fixed order: bitwise reproducible).
+template <int BM_, int BN_, int WM_, int WN_, int NS_, int EP_ = 1, int BK_ = 128, int KG_ = 1>
 struct Tile {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NSTAGE = NS_, EP = EP_, BKB = BK_;
-  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NSTAGE = NS_, EP = EP_, BKB = BK_, KG = KG_;
+  static constexpr int NW = WM * WN * KG, NT = 64 * NW;
   static constexpr int MR = BM / WM / 32, NR = BN / WN / 32;
   static constexpr int SLOTS = BKB / 16, RPI = 1024 / BKB, SWDIV = 16 / SLOTS;
   static constexpr int GA = BM / RPI / NW, GB = BN / RPI / NW;     // glds per thread per stage
@@ -53,6 +59,7 @@ struct Tile {
   static_assert(BKB == 64 || BKB == 128, "stage depth");
   static_assert(GEMM_BK_BYTES % BKB == 0, "packed K granule");
   static_assert(WM % EP == 0, "epilogue passes split the wave rows");
+  static_assert(KG == 1 || (KG == 2 && EP == 1 && (BKB / 32) % 2 == 0), "K-groups");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
   static CFM_DEV int swz(int row) { return (row / SWDIV) % SLOTS; }
 };
@@ -71,6 +78,11 @@ using T128x128d = Tile<128, 128, 2, 2, 8, 1, 64>;   // 4 waves, 8 x 16 KiB
 using T256x128d = Tile<256, 128, 4, 2, 5, 1, 64>;   // 8 waves, 5 x 24 KiB, wave tile 64 x 64
 using T128x256d = Tile<128, 256, 2, 4, 5, 1, 64>;   // 8 waves, 5 x 24 KiB, wave tile 64 x 64
 using T256x256w = Tile<256, 256, 2, 4, 2, 2, 128>;  // 8 waves, 2 x 64 KiB
+using T128x128k = Tile<128, 128, 2, 2, 3, 1, 128, 2>;  // 8 waves = 2 K-groups x 4, 3 x 32 KiB, wave tile 64 x 64
+using T128x128k2 = Tile<128, 128, 2, 2, 2, 1, 128, 2>; // as above, 2 x 32 KiB (2 blocks / CU by LDS)
+using T128x128k4 = Tile<128, 128, 2, 2, 4, 1, 128, 2>; // as above, 4 x 32 KiB
+using T128x256k = Tile<128, 256, 2, 2, 3, 1, 128, 2>;  // 8 waves = 2 K-groups x 4, 3 x 48 KiB, wave tile 64 x 128
+using T64x128k = Tile<64, 128, 2, 2, 3, 1, 128, 2>;    // 8 waves = 2 K-groups x 4, 3 x 24 KiB, wave tile 32 x 64
 
 // ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
 CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
@@ -115,7 +127,9 @@ struct ALoadDense {
       s.row_ptr[i] = (m < M) ? A + (long)m * lda_b : nullptr;
     }
   }
-  CFM_DEV const void* src(const State& s, int i, long kb) const {
+  // kb0: the K-step's first byte (wave-uniform); lo: this lane's byte offset within the step
+  CFM_DEV const void* src(const State& s, int i, long kb0, int lo) const {
+    const long kb = kb0 + lo;
     return (s.row_ptr[i] != nullptr && kb < kbytes) ? (const void*)(s.row_ptr[i] + kb) : (const void*)zero;
   }
 };
@@ -126,6 +140,7 @@ template <int G>
 struct ALoadConv {
   static constexpr bool kConv = true;   // conv2 + ReLU only
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
+  int tap_steps;   // tapb / 128 when a 3x3 tap spans whole 128-byte K-steps (C*es % 128 == 0), else 0
   struct State { const char* base[G]; uint32_t valid[G]; };
   CFM_DEV void shift_k(long) {}   // never split
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
@@ -151,9 +166,20 @@ struct ALoadConv {
       s.valid[i] = v;
     }
   }
-  CFM_DEV const void* src(const State& s, int i, long kb) const {
-    const int tap = (int)(kb / tapb);
-    const long cb = kb - (long)tap * tapb;
+  CFM_DEV const void* src(const State& s, int i, long kb0, int lo) const {
+    int tap;
+    long cb;
+    if (tap_steps > 0) {
+      // the whole K-step lies in one tap: tap and the tap's byte offset are wave-uniform (scalar
+      // unit, 32-bit), only the validity bit and the address add are per lane
+      const int k0 = __builtin_amdgcn_readfirstlane((int)kb0);
+      tap = __builtin_amdgcn_readfirstlane(k0 / (int)tapb);
+      cb = (long)(k0 - tap * (int)tapb) + lo;
+    } else {
+      const long kb = kb0 + lo;
+      tap = (int)(kb / tapb);
+      cb = kb - (long)tap * tapb;
+    }
     if (tap >= 9 || !((s.valid[i] >> tap) & 1u)) return zero;
     const int kt = tap / 3, kf = tap - kt * 3;
     return s.base[i] + ((long)kt * F1 + kf) * tapb + cb;
@@ -389,7 +415,8 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int kg = wave / (TL::WM * TL::WN);
+  const int wm = (wave % (TL::WM * TL::WN)) / TL::WN, wn = wave % TL::WN;
 
   // XCD-aware bijective remap: blocks sharing an XCD (bid % 8) get a contiguous tile range.
   const int nblocks = p.Mtiles * p.Ntiles;
@@ -424,7 +451,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     const uint32_t sb = smem_base + slot * TL::STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < TL::GA; ++i)
-      glds16_asm(aload.src(ast, i, kb0 + aslot[i]), sb + (i * TL::NW + wave) * 1024);
+      glds16_asm(aload.src(ast, i, kb0, aslot[i]), sb + (i * TL::NW + wave) * 1024);
 #pragma unroll
     for (int i = 0; i < TL::GB; ++i)
       glds16_asm(wrow[i] + kb0, sb + TL::BM * TL::BKB + (i * TL::NW + wave) * 1024);
@@ -442,9 +469,10 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   const int sw = TL::swz(lane & 31);       // rows are 32-aligned + (lane & 31)
 
   const int nk = (p.probe & 4) ? 1 : p.kb / TL::BKB;
-  constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB, KSUB = TL::BKB / 32;
+  constexpr int NS = TL::NSTAGE, G = TL::GA + TL::GB, KSUB = TL::BKB / 32 / TL::KG;
+  const int kk0 = kg * KSUB;   // this K-group's first substep of every K-step
   auto read_frags = [&](const char* Sb, int kk, uint4* af, uint4* bf) {
-    const int so = ((2 * kk + hsel) ^ sw) * 16;
+    const int so = ((2 * (kk0 + kk) + hsel) ^ sw) * 16;
 #pragma unroll
     for (int i = 0; i < TL::MR; ++i) af[i] = *(const uint4*)(Sb + (a_row0 + i * 32) * TL::BKB + so);
 #pragma unroll
@@ -504,6 +532,33 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   raw_barrier();                         // every wave is done reading the ring
   float* img = (float*)smem;
   const int col = lane & 31;
+  if constexpr (TL::KG == 2) {
+    // K-group 1 hands its partial sums to K-group 0 through the image (then group 0 owns the tile)
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j) {
+          const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr)
+            img[(wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane)) * TL::EPS + cl] = acc[i][j][rr];
+        }
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j) {
+          const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr)
+            acc[i][j][rr] += img[(wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane)) * TL::EPS + cl];
+        }
+    }
+    __syncthreads();
+  }
   float bcol[TL::NR];                    // bias arrays are zero-padded to the N granule (GEMM_BN)
 #pragma unroll
   for (int j = 0; j < TL::NR; ++j) bcol[j] = 0.0f;
@@ -515,7 +570,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
   for (int pass = 0; pass < TL::EP; ++pass) {
     if (pass > 0) __syncthreads();       // the previous pass has read the image
-    if (wm / WPP == pass) {
+    if (wm / WPP == pass && kg == 0) {
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
@@ -563,6 +618,7 @@ struct ConvArgs {
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
   template <class AL> void fill(AL& al) const {
     al.X1 = X1; al.T1 = T1; al.F1 = F1; al.T2 = T2; al.F2 = F2; al.tapb = tapb; al.M = M; al.zero = zero;
+    al.tap_steps = (tapb % 128 == 0 && tapb * 9 < (1L << 31)) ? (int)(tapb / 128) : 0;
   }
 };
 
@@ -582,12 +638,44 @@ int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) :
 // Automatic choice (tools/gemm_bench.py, MI355X, bf16): the implicit conv and the wide FFN-up
 // GEMM run best on 256x256 (tile 11); the N = 512 layer GEMMs on 64x128 at 3 blocks / CU (tile 5);
 // the GLU GEMM on 256x128.
-int pick_tile(int dtype, int M, int Nw, int epi, bool conv) {
+// CFM_TILES="epi:tile[@minM[k minK]],..." overrides the bf16 choice per epilogue id (A/B
+// measurements; epilogue ids as in cfm_kernels.h, 9 = the implicit conv); the first entry whose
+// minM <= M and minK <= K wins.
+struct TileRule { int epi, tile, min_m, min_k; };
+const std::vector<TileRule>& tile_rules() {
+  static const std::vector<TileRule> rules = [] {
+    std::vector<TileRule> r;
+    const char* s = getenv("CFM_TILES");
+    while (s && *s) {
+      TileRule t{-1, -1, 0, 0};
+      if (sscanf(s, "%d:%d@%dk%d", &t.epi, &t.tile, &t.min_m, &t.min_k) >= 2) r.push_back(t);
+      s = strchr(s, ',');
+      if (s) ++s;
+    }
+    return r;
+  }();
+  return rules;
+}
+
+int pick_tile(int dtype, int M, int Nw, int epi, bool conv, int K = 0) {
   if (g_tile_override >= 0) return g_tile_override;
   if (dtype == DT_BF16) {
+    for (const TileRule& t : tile_rules())
+      if (t.epi == (conv ? 9 : epi) && M >= t.min_m && K >= t.min_k) return t.tile;
+  }
+  if (dtype == DT_BF16) {
+    // forward A/B on MI355X (tools/fwd_ab.sh, single stream, B=32 T=1000): the N = 512 residual
+    // GEMMs (FFN linear2, linear_out, pointwise_conv2) run best on 128x128 tiles (one per CU, the
+    // fewest L2 -> LDS bytes per CU) with two K-groups of 4 waves (two waves per SIMD) and a
+    // 4-deep ring: 5.48 -> 5.20 ms per forward against 256x128 / 128x128 one-group tiles (the 4-deep
+    // ring another 1.4 % over 3-deep)
     if (conv) return 11;
     if (Nw >= 2048 && M >= 4096) return 11;
     if (epi == EPI_GLU_MASK) return 1;
+    // K-grouped tiles split each 128-byte K-step's substeps {0,1} | {2,3} between the groups, so
+    // the small-M residual tile must be K-grouped the same way: an utterance's output is then
+    // bitwise independent of the batch it runs in (tests/test_gpu_encoder.py)
+    if (epi == EPI_RESID) return M >= 4096 ? 14 : 16;
     return 5;
   }
   if (conv || (long)M * Nw >= (long)32 << 20) return 1;
@@ -615,6 +703,11 @@ void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
       case 9: setup(256, 128); launch_epi<T, T256x128d, AL>(p, args, st); return;
       case 10: setup(128, 256); launch_epi<T, T128x256d, AL>(p, args, st); return;
       case 11: setup(256, 256); launch_epi<T, T256x256w, AL>(p, args, st); return;
+      case 12: setup(128, 128); launch_epi<T, T128x128k, AL>(p, args, st); return;
+      case 13: setup(128, 128); launch_epi<T, T128x128k2, AL>(p, args, st); return;
+      case 14: setup(128, 128); launch_epi<T, T128x128k4, AL>(p, args, st); return;
+      case 15: setup(128, 256); launch_epi<T, T128x256k, AL>(p, args, st); return;
+      case 16: setup(64, 128); launch_epi<T, T64x128k, AL>(p, args, st); return;
       default: break;
     }
   }
@@ -661,7 +754,7 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
   p.probe = g_gemm_probe;
-  int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false);
+  int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false, K);
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
 }

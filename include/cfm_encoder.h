@@ -102,7 +102,7 @@ int cfm_encoder_max_audio_length(const cfm_encoder* h);
  * the attention mask is unchanged.  Default on. */
 cfm_status cfm_encoder_set_pad_mask(cfm_encoder* h, int on);
 
-/* Micro-batch concurrency (default 2, env CFM_MICROBATCH): the batch is split into up to n parts
+/* Micro-batch concurrency (default 1, env CFM_MICROBATCH): the batch is split into up to n parts
  * (each >= 4 utterances) that run on library-owned streams forked from / joined into `stream`.
  * Outputs are bitwise identical for any n. */
 cfm_status cfm_encoder_set_microbatches(cfm_encoder* h, int n);
