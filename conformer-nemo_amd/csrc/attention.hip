@@ -43,6 +43,7 @@ struct AttnParams {
   // (bias added, heads padded to dkp); the kernel forms (q + u)*c, (q + v)*c itself from `uv`
   // ([u | v], fp32, H*dkp each) and transposes V into its LDS image while staging.
   const float* uv; float qscale;
+  int vec_out;   // 16-byte output stores through LDS (env CFM_ATTN_VECOUT=0 turns them off: A/B)
 };
 
 constexpr int BDS = 32;   // fp32 row stride of the 64x32 BD^T image (conflict-free skewed reads)
@@ -543,18 +544,45 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     T* out = (T*)p.out;
+    if (ND <= 2 && p.vec_out && p.dk == ND * 32 && p.ldo % 8 == 0) {
+      // the wave's 32 x dk output tile goes through its (now free) BD image as fp32, then leaves as
+      // 16-byte rows of 8 bf16 (4 stores per lane instead of 16 * ND two-byte stores)
+      constexpr int OW = ND * 32;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = acc_row(r, lane);
-      const int ig = i0 + i;
-      const float l = row_s[i];
-      const bool valid = ig < len && l > 0.0f;
-      const float inv = valid ? 1.0f / l : 0.0f;
-      if (ig >= Tp) continue;
+      for (int r = 0; r < 16; ++r) {
+        const int i = acc_row(r, lane);
+        const float l = row_s[i];
+        const bool valid = i0 + i < len && l > 0.0f;
+        const float inv = valid ? 1.0f / l : 0.0f;
 #pragma unroll
-      for (int n = 0; n < ND; ++n) {
-        const int d = n * 32 + col;
-        if (d < p.dk) st_f<T>(out + (rowbase + ig) * p.ldo + (long)h * p.dk + d, valid ? o[n][r] * inv : 0.0f);
+        for (int n = 0; n < ND; ++n) bd_s[i * OW + n * 32 + col] = valid ? o[n][r] * inv : 0.0f;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      constexpr int CH = OW / 8;   // 16-byte chunks per row
+#pragma unroll
+      for (int q = 0; q < 32 * CH / 64; ++q) {
+        const int j = lane + 64 * q, i = j / CH, c8 = j - i * CH;
+        if (i0 + i >= Tp) continue;
+        const float4 a = *(const float4*)(bd_s + i * OW + c8 * 8);
+        const float4 b2 = *(const float4*)(bd_s + i * OW + c8 * 8 + 4);
+        const float f[8] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w};
+        *(uint4*)(out + (rowbase + i0 + i) * p.ldo + (long)h * p.dk + c8 * 8) = Vec16<bf16_t>::from_f32(f);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = acc_row(r, lane);
+        const int ig = i0 + i;
+        const float l = row_s[i];
+        const bool valid = ig < len && l > 0.0f;
+        const float inv = valid ? 1.0f / l : 0.0f;
+        if (ig >= Tp) continue;
+#pragma unroll
+        for (int n = 0; n < ND; ++n) {
+          const int d = n * 32 + col;
+          if (d < p.dk) st_f<T>(out + (rowbase + ig) * p.ldo + (long)h * p.dk + d, valid ? o[n][r] * inv : 0.0f);
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -652,6 +680,8 @@ void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, flo
   p.ctx_left = ctx_left; p.ctx_right = ctx_right;
   p.out = (char*)out; p.ldo = ldo;
   p.uv = uv; p.qscale = qscale;
+  static const int vec_out = [] { const char* e = getenv("CFM_ATTN_VECOUT"); return e ? atoi(e) : 1; }();
+  p.vec_out = vec_out;
   bool done = false;
   switch (dkp) {
     case 16: done = launch_lds<1, true>(p, B, st); break;
@@ -669,7 +699,7 @@ void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int
                        int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
   AttnParams p;
-  p.uv = nullptr; p.qscale = 1.0f;
+  p.uv = nullptr; p.qscale = 1.0f; p.vec_out = 1;
   p.qk = (const char*)qk; p.ldqk = ldqk;
   p.Vt = (const char*)Vt; p.vt_rows = vt_rows; p.Tpad = Tpad;
   p.P = (const char*)P; p.ldp = ldp;

@@ -59,7 +59,7 @@ struct Tile {
   static_assert(BKB == 64 || BKB == 128, "stage depth");
   static_assert(GEMM_BK_BYTES % BKB == 0, "packed K granule");
   static_assert(WM % EP == 0, "epilogue passes split the wave rows");
-  static_assert(KG == 1 || (KG == 2 && EP == 1 && (BKB / 32) % 2 == 0), "K-groups");
+  static_assert(KG == 1 || (EP == 1 && (BKB / 32) % KG == 0), "K-groups");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
   static CFM_DEV int swz(int row) { return (row / SWDIV) % SLOTS; }
 };
@@ -83,6 +83,7 @@ using T128x128k2 = Tile<128, 128, 2, 2, 2, 1, 128, 2>; // as above, 2 x 32 KiB (
 using T128x128k4 = Tile<128, 128, 2, 2, 4, 1, 128, 2>; // as above, 4 x 32 KiB
 using T128x256k = Tile<128, 256, 2, 2, 3, 1, 128, 2>;  // 8 waves = 2 K-groups x 4, 3 x 48 KiB, wave tile 64 x 128
 using T64x128k = Tile<64, 128, 2, 2, 3, 1, 128, 2>;    // 8 waves = 2 K-groups x 4, 3 x 24 KiB, wave tile 32 x 64
+using T128x128q = Tile<128, 128, 2, 2, 4, 1, 128, 4>;  // 16 waves = 4 K-groups x 4, 4 x 32 KiB, wave tile 64 x 64
 
 // ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
 CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
@@ -532,30 +533,36 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   raw_barrier();                         // every wave is done reading the ring
   float* img = (float*)smem;
   const int col = lane & 31;
-  if constexpr (TL::KG == 2) {
-    // K-group 1 hands its partial sums to K-group 0 through the image (then group 0 owns the tile)
-    if (kg == 1) {
+  if constexpr (TL::KG > 1) {
+    // the other K-groups hand their partial sums to K-group 0 through the image, in a fixed order
+    // (img = p1; img += p2; ...; acc0 += img): bitwise reproducible, the same for every tile with
+    // the same K-grouping
+    auto img_at = [&](int i, int j, int rr) -> float& {
+      return img[(wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane)) * TL::EPS + wn * (TL::BN / TL::WN) + j * 32 +
+                 col];
+    };
 #pragma unroll
-      for (int i = 0; i < TL::MR; ++i)
+    for (int g = 1; g < TL::KG; ++g) {
+      if (kg == g) {
 #pragma unroll
-        for (int j = 0; j < TL::NR; ++j) {
-          const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+        for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-          for (int rr = 0; rr < 16; ++rr)
-            img[(wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane)) * TL::EPS + cl] = acc[i][j][rr];
-        }
+          for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+              if (g == 1) img_at(i, j, rr) = acc[i][j][rr];
+              else img_at(i, j, rr) += acc[i][j][rr];
+            }
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (kg == 0) {
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < TL::NR; ++j) {
-          const int cl = wn * (TL::BN / TL::WN) + j * 32 + col;
+        for (int j = 0; j < TL::NR; ++j)
 #pragma unroll
-          for (int rr = 0; rr < 16; ++rr)
-            acc[i][j][rr] += img[(wm * (TL::BM / TL::WM) + i * 32 + acc_row(rr, lane)) * TL::EPS + cl];
-        }
+          for (int rr = 0; rr < 16; ++rr) acc[i][j][rr] += img_at(i, j, rr);
     }
     __syncthreads();
   }
@@ -708,6 +715,7 @@ void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
       case 14: setup(128, 128); launch_epi<T, T128x128k4, AL>(p, args, st); return;
       case 15: setup(128, 256); launch_epi<T, T128x256k, AL>(p, args, st); return;
       case 16: setup(64, 128); launch_epi<T, T64x128k, AL>(p, args, st); return;
+      case 17: setup(128, 128); launch_epi<T, T128x128q, AL>(p, args, st); return;
       default: break;
     }
   }
