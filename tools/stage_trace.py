@@ -21,6 +21,7 @@ EPI_STAGE = {"0": "pos_gemm", "2": "ffn_up_gemm", "4": "subsample_linear", "5": 
 def stage_of(name, state):
     if name.startswith("calc_length"):
         state["resid"] = 0
+        state["pos_done"] = False
         return "lengths"
     if name.startswith("conv1_kernel"):
         return "conv1"
@@ -40,6 +41,13 @@ def stage_of(name, state):
             s = RESID_ORDER[state["resid"] % 4]
             state["resid"] += 1
             return s
+        if m.group(1) == "0":
+            # plain-store GEMMs: the first of a forward is the position projection, the others are
+            # the layers' QKV projections (natural-layout attention, bf16)
+            if not state.get("pos_done"):
+                state["pos_done"] = True
+                return "pos_gemm"
+            return "qkv_gemm"
         return EPI_STAGE.get(m.group(1), "gemm_other")
     return None
 
