@@ -74,36 +74,98 @@ def pmc_traffic(stage, B, T, L, compute):
 
 
 def cpu_baseline(enc, B, T, budget_s):
-    """Oracle (numpy restatement of the reference) on the host cores, bounded sample."""
+    """The reference encoder's arithmetic on the host cores: oracle/conformer_torch_cpu.py, a torch-CPU
+    restatement of the reference forward (bitwise equal to the imported reference and within 10 % of
+    its time in the survey container: profiles/r02_cpu_baseline_check.txt), fp32, eval,
+    torch.no_grad, the timed encoder's weights, batched utterances of T frames; 1 warm-up + min of 3.
+    The batch is cut so that the sample stays near `budget_s` seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
-    import conformer_oracle as O  # CPU baseline leg only
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    sd = {k: v.detach().float().cpu().numpy() for k, v in enc.state_dict().items() if v.is_floating_point()}
+    import conformer_torch_cpu as TC  # CPU baseline leg only
+    threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items() if v.is_floating_point()}
     cfg = dict(d_model=512, n_heads=8, n_layers=17)
-    g = np.random.default_rng(0)
-    x = g.standard_normal((1, 80, T), dtype=np.float32)
-    frames, t0, runs = 0, time.perf_counter(), 0
-    while True:
-        O.encoder_forward(x, np.array([T]), sd, cfg)
-        frames += T
-        runs += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
+    g = torch.Generator().manual_seed(0)
+    t_start = time.perf_counter()
+    Bs = 2
+    x = torch.randn(Bs, 80, T, generator=g)
+    t0 = time.perf_counter()
+    TC.encoder_forward(x, None, sd, cfg)                    # warm-up at a small batch: sizes the sample
+    per_utt = (time.perf_counter() - t0) / Bs
+    Bs = int(max(1, min(B, budget_s / 4.0 / max(per_utt, 1e-6))))
+    x = torch.randn(Bs, 80, T, generator=g)
+    TC.encoder_forward(x, None, sd, cfg)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        TC.encoder_forward(x, None, sd, cfg)
+        ts.append(time.perf_counter() - t0)
+    total = time.perf_counter() - t_start
+    torch.set_num_threads(prev)
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
     except (OSError, StopIteration):
         pass
-    return {"value": round(frames / dt, 1), "unit": "audio-frames/s", "cores": int(cores), "kind": "port",
+    return {"value": round(Bs * T / min(ts), 1), "unit": "audio-frames/s", "cores": int(threads), "kind": "port",
             "cpu_model": cpu_model,
-            "sample": f"oracle/conformer_oracle.py numpy fp32, Large-17, {runs} x (B=1, T={T}) utterances, {dt:.1f} s"}
+            "sample": f"oracle/conformer_torch_cpu.py (torch-CPU restatement of the reference, fp32 eval), "
+                      f"Large-17, B={Bs} x T={T} per forward, min of 3 after a warm-up, {total:.1f} s in all"}
+
+
+def parity_and_fp32(dev, B, T, steps=5):
+    """What the bf16 headline hides (rank 0, after the timed loop):
+    * the error of both compute modes at the timed shape against the REFERENCE encoder: the two
+      reference utterances of tests/golden/enc_large17.npz (Large-17, outputs of the reference
+      ConformerEncoder, fp32 CPU) embedded at positions 5 and 30 of a B x T batch, weights from the
+      golden's seed recipe (tests/golden/recipe.py) -> relL2 per compute mode (north-star gate: fp32
+      relL2 <= 1e-3);
+    * the fp32 parity mode's own throughput at the same shape (v_mfma_f32_32x32x2_f32 contractions)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from recipe import make_state_dict  # fixture recipe (checker only)
+    from nemo.collections.asr.modules import ConformerEncoder
+    z = np.load(os.path.join(ROOT, "tests", "golden", "enc_large17.npz"))
+    cfg = dict(d_model=512, n_heads=8, n_layers=17)
+    sd = make_state_dict(cfg, int(z["seed"]))
+    enc = ConformerEncoder(feat_in=80, n_layers=17, d_model=512, n_heads=8)
+    ref_sd = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref_sd[k].shape) for k, v in sd.items()})
+    enc = enc.to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(B, 80, T, device=dev, generator=g)
+    ln = torch.full((B,), T, dtype=torch.int64, device=dev)
+    slots = [5 % B, 30 % B]
+    for i, s in enumerate(slots):
+        x[s] = torch.from_numpy(z["x"][i]).to(dev)
+        ln[s] = int(z["lengths"][i])
+    out = {"reference": "tests/golden/enc_large17.npz: reference ConformerEncoder outputs (fp32, CPU) for 2 "
+                        f"utterances embedded in the B={B} x T={T} batch", "gate_fp32_relL2": 1e-3}
+    yref = torch.from_numpy(z["y"]).to(dev, torch.float64)
+    for compute in ("bf16", "fp32"):
+        enc.set_compute_mode(compute)
+        with torch.inference_mode():
+            y, yl = enc(audio_signal=x, length=ln)
+            y = y[slots].to(torch.float64)
+            out[f"{compute}_relL2"] = float((y - yref).norm() / yref.norm())
+            out[f"{compute}_max_abs_err_over_max_ref"] = float((y - yref).abs().max() / yref.abs().max())
+            if compute == "fp32":
+                for _ in range(2):
+                    enc(audio_signal=x, length=ln)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    enc(audio_signal=x, length=ln)
+                torch.cuda.synchronize(dev)
+                ms = 1000.0 * (time.perf_counter() - t0) / steps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops
+    tf = encoder_flops(B, T, 512, 17) / (ms * 1e-3) / 1e12
+    fp32 = {"ms_per_step": round(ms, 3), "value": round(B * T / (ms * 1e-3), 1), "unit": "audio-frames/s",
+            "TFLOP/s": round(tf, 1), "frac_of_fp32_mfma_peak": round(tf / PEAK["fp32"], 4), "steps": steps}
+    return out, fp32
 
 
 def max_over_ranks(elapsed, dev, dist):
@@ -128,7 +190,10 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1000)
     ap.add_argument("--layers", type=int, default=17)
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU oracle timing (0 = skip)")
+    ap.add_argument("--cpu-budget", type=float, default=16.0,
+                    help="seconds of CPU-baseline timing (torch-CPU restatement of the reference; 0 = skip)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the bf16/fp32 relL2 against the reference golden and the fp32-mode throughput line")
     ap.add_argument("--no-breakdown", action="store_true")
     ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "mel", "decode"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
@@ -237,6 +302,9 @@ def main():
         total_flop = encoder_flops(B, T, d, L)
         # the CPU baseline is a rank-0, N=1 measurement (a multi-GPU job reports the GPU lines only)
         cpu = cpu_baseline(enc, B, T, args.cpu_budget) if (args.cpu_budget > 0 and world == 1) else None
+        parity, fp32_line = (None, None)
+        if not args.no_parity and L == 17 and d == 512:
+            parity, fp32_line = parity_and_fp32(dev, B, T)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -249,6 +317,8 @@ def main():
                             "TFLOP/s_per_gpu": round(total_flop / (ms_step * 1e-3) / 1e12, 1),
                             "frac_of_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
             "cpu_baseline": cpu,
+            "parity": parity,
+            "fp32_parity_mode": fp32_line,
             "breakdown": breakdown,
         }
         print(json.dumps(out), flush=True)
