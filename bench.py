@@ -339,8 +339,9 @@ def run_train(args, world, rank, dev, dist, barrier):
     from nemo.collections.asr.modules import ConformerEncoder, ConvASRDecoder
     torch.manual_seed(0)
     d, H, L, B, T, V, U = 512, 8, args.layers, args.batch, args.seq, args.vocab, 60
+    # conformer_ctc_bpe.yaml:130-132 regularisation, unchanged: dropout 0.1, dropout_emb 0.0, dropout_att 0.1
     enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H, dropout=0.1, dropout_emb=0.0,
-                           dropout_att=0.0).to(dev).train()
+                           dropout_att=0.1).to(dev).train()
     dec = ConvASRDecoder(feat_in=d, num_classes=V).to(dev).train()
     for m in (enc, dec):
         m.set_compute_mode(args.compute)
@@ -392,6 +393,7 @@ def run_train(args, world, rank, dev, dist, barrier):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
             "config": {"workload": f"Conformer-CTC-Large training step (encoder d512/8 heads/{L} layers, dropout 0.1, "
+                                   f"dropout_att 0.1, "
                                    f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss "
                                    f"U={U}, AdamW), B={B}/GPU, T={T}",
                        "global_batch": B * world, "seq_len": T,

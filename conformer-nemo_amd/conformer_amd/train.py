@@ -87,11 +87,12 @@ class EncoderTrainer:
         return ALLREDUCE_FN(cb)
 
     # ---- step ------------------------------------------------------------------------------------
-    def _opts(self, dropout: float, seed: int, update_running_stats: bool, bn_momentum: float) -> CfmTrainOpts:
+    def _opts(self, dropout: float, seed: int, update_running_stats: bool, bn_momentum: float,
+              dropout_emb: float = 0.0, dropout_att: float = 0.0) -> CfmTrainOpts:
         o = CfmTrainOpts()
         o.dropout = float(dropout)
-        o.dropout_emb = 0.0
-        o.dropout_att = 0.0
+        o.dropout_emb = float(dropout_emb)
+        o.dropout_att = float(dropout_att)
         o.bn_momentum = float(bn_momentum)
         o.update_running_stats = 1 if update_running_stats else 0
         o.world = self.world
@@ -123,7 +124,8 @@ class EncoderTrainer:
                 raise ValueError(f"{n}: parameters must be contiguous fp32 tensors on {self.device}")
 
     def forward(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor], params: Sequence[torch.Tensor],
-                dropout: float = 0.0, seed: int = 0, update_running_stats: bool = True, bn_momentum: float = 0.1):
+                dropout: float = 0.0, seed: int = 0, update_running_stats: bool = True, bn_momentum: float = 0.1,
+                dropout_emb: float = 0.0, dropout_att: float = 0.0):
         from .runtime import encoded_length
         self.check_params(params)
         x = x_bft.detach().to(self.device, torch.float32).contiguous()
@@ -138,13 +140,14 @@ class EncoderTrainer:
         tape = torch.empty(int(self.lib.cfm_train_tape_size(self.native.handle, B, T)), dtype=torch.uint8,
                            device=self.device)
         ws = self._workspace(B, T)
-        o = self._opts(dropout, seed, update_running_stats, bn_momentum)
+        o = self._opts(dropout, seed, update_running_stats, bn_momentum, dropout_emb, dropout_att)
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_forward(self.native.handle, self._ptrs(params), len(params), x.data_ptr(),
                                               None if ln is None else ln.data_ptr(), B, T, ctypes.byref(o),
                                               y.data_ptr(), ylen.data_ptr(), tape.data_ptr(), tape.numel(),
                                               ws.data_ptr(), ws.numel(), st), "cfm_train_forward")
-        state = dict(tape=tape, B=B, T=T, dropout=dropout, seed=seed, bn_momentum=bn_momentum, x=x, ln=ln)
+        state = dict(tape=tape, B=B, T=T, dropout=dropout, seed=seed, bn_momentum=bn_momentum, x=x, ln=ln,
+                     dropout_emb=dropout_emb, dropout_att=dropout_att)
         return y, ylen, state
 
     def backward(self, dy_bdt: torch.Tensor, state: Dict, params: Sequence[torch.Tensor],
@@ -152,7 +155,8 @@ class EncoderTrainer:
         dy = dy_bdt.detach().to(self.device, torch.float32).contiguous()
         grads = [torch.empty_like(p) if w else None for p, w in zip(params, want)]
         ws = self._workspace(state["B"], state["T"])
-        o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"])
+        o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"], state["dropout_emb"],
+                       state["dropout_att"])
         tape = state["tape"]
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
@@ -165,8 +169,9 @@ class EncoderTrainer:
 class _EncoderTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, trainer: EncoderTrainer, x, lengths, cfg: Tuple, *params):
-        dropout, seed, update_stats, momentum = cfg
-        y, ylen, state = trainer.forward(x, lengths, params, dropout, seed, update_stats, momentum)
+        dropout, seed, update_stats, momentum, dropout_emb, dropout_att = cfg
+        y, ylen, state = trainer.forward(x, lengths, params, dropout, seed, update_stats, momentum, dropout_emb,
+                                         dropout_att)
         ctx.trainer = trainer
         ctx.state = state
         ctx.params = params
@@ -185,7 +190,11 @@ class _EncoderTrainFn(torch.autograd.Function):
 
 def encoder_train_forward(trainer: EncoderTrainer, x: torch.Tensor, lengths: Optional[torch.Tensor],
                           params: Sequence[torch.Tensor], dropout: float, seed: int,
-                          update_running_stats: bool = True, bn_momentum: float = 0.1):
-    """Differentiable native train-mode encoder forward: returns (y (B, d, T'), lengths (B,) int32)."""
+                          update_running_stats: bool = True, bn_momentum: float = 0.1,
+                          dropout_emb: float = 0.0, dropout_att: float = 0.0):
+    """Differentiable native train-mode encoder forward: returns (y (B, d, T'), lengths (B,) int32).
+    dropout: embedding / FFN / residual-branch dropout; dropout_emb: positional-embedding dropout
+    (multi_head_attention.py:316); dropout_att: attention-probability dropout (:111)."""
     return _EncoderTrainFn.apply(trainer, x, lengths, (float(dropout), int(seed), bool(update_running_stats),
-                                                       float(bn_momentum)), *params)
+                                                       float(bn_momentum), float(dropout_emb), float(dropout_att)),
+                                 *params)

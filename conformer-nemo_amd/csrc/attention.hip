@@ -44,7 +44,20 @@ struct AttnParams {
   // ([u | v], fp32, H*dkp each) and transposes V into its LDS image while staging.
   const float* uv; float qscale;
   int vec_out;   // 16-byte output stores through LDS (env CFM_ATTN_VECOUT=0 turns them off: A/B)
+  // training: dropout on the attention probabilities (multi_head_attention.py:111, p_attn =
+  // dropout(attn)); element (b, h, i, j) is kept iff its counter hash passes (drop_mul), so the
+  // backward regenerates the same mask.  thr = 0: no dropout.
+  Drop adrop;
 };
+
+// P^T tile (rows = keys j0 + acc_row(r), lane = query iq) *= dropout mask of (b*H + h, iq, key):
+// the softmax denominator keeps the undropped sum (dropout acts on normalised probabilities).
+CFM_DEV void drop_tile(f32x16& st, const Drop& dr, long bh, int Tp, int iq, int j0, int lane) {
+  if (dr.thr == 0) return;
+  const uint64_t base = ((uint64_t)bh * Tp + (uint64_t)min(iq, Tp - 1)) * (uint64_t)Tp + j0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) st[r] *= drop_mul(dr, base + acc_row(r, lane));
+}
 
 constexpr int BDS = 32;   // fp32 row stride of the 64x32 BD^T image (conflict-free skewed reads)
 
@@ -259,6 +272,7 @@ __global__ __launch_bounds__(64) void rel_attn_kernel(AttnParams p) {
     // scores for this lane's query and its 16 keys, then the online softmax
     const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane);
     softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
+    drop_tile(st, p.adrop, (long)b * p.H + h, Tp, iq, j0, lane);
     if (j0 + 32 > Tp) {   // keys >= T' read Vt padding (unspecified): force those V entries to 0
 #pragma unroll
       for (int n = 0; n < ND; ++n)
@@ -522,6 +536,7 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
       __builtin_amdgcn_wave_barrier();
       const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane, (k & 1) << 5);
       softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
+      drop_tile(st, p.adrop, bh, Tp, iq, j0, lane);
       uint2 v[ND][4];
 #pragma unroll
       for (int n = 0; n < ND; ++n)
@@ -680,6 +695,7 @@ void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, flo
   p.ctx_left = ctx_left; p.ctx_right = ctx_right;
   p.out = (char*)out; p.ldo = ldo;
   p.uv = uv; p.qscale = qscale;
+  p.adrop = Drop{0u, 0u, 1.0f};
   static const int vec_out = [] { const char* e = getenv("CFM_ATTN_VECOUT"); return e ? atoi(e) : 1; }();
   p.vec_out = vec_out;
   bool done = false;
@@ -696,10 +712,12 @@ void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, flo
 
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
                        long ldp, const int32_t* lens, int B, int Tp, int H,
-                       int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st) {
+                       int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st,
+                       Drop adrop) {
   if (B <= 0 || Tp <= 0) return;
   AttnParams p;
   p.uv = nullptr; p.qscale = 1.0f; p.vec_out = 1;
+  p.adrop = adrop;
   p.qk = (const char*)qk; p.ldqk = ldqk;
   p.Vt = (const char*)Vt; p.vt_rows = vt_rows; p.Tpad = Tpad;
   p.P = (const char*)P; p.ldp = ldp;

@@ -311,17 +311,21 @@ __global__ __launch_bounds__(256) void attn_probs_kernel(float* __restrict__ S, 
 
 // One wave per row: dS = P * (dP - sum_j P dP) into dP; the skewed copy G (layout [h][b][i][r],
 // all r < gld written) gets dS at r = T'-1-i+j and zero elsewhere.
-__global__ __launch_bounds__(256) void attn_dscore_kernel(const float* __restrict__ P, float* __restrict__ dP,
+// With attention dropout (adrop.thr != 0) dP here is the gradient of the DROPPED probabilities:
+// dP <- dP * mask / (1 - p) first, and P <- P * mask / (1 - p) at the end (the dv GEMM's operand).
+__global__ __launch_bounds__(256) void attn_dscore_kernel(float* __restrict__ P, float* __restrict__ dP,
                                                           long sld, float* __restrict__ G, long gld, int B, int H,
-                                                          int Tp) {
+                                                          int Tp, Drop adrop) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= (long)B * H * Tp) return;
   const int i = (int)(row % Tp);
   const long bh = row / Tp;
   const int h = (int)(bh % H), b = (int)(bh / H);
-  const float* p = P + row * sld;
+  float* p = P + row * sld;
   float* dp = dP + row * sld;
+  if (adrop.thr)
+    for (int j = lane; j < Tp; j += 64) dp[j] *= drop_mul(adrop, (uint64_t)row * Tp + j);
   float D = 0.0f;
   for (int j = lane; j < Tp; j += 64) D += p[j] * dp[j];
   D = wave_sum(D);
@@ -332,6 +336,8 @@ __global__ __launch_bounds__(256) void attn_dscore_kernel(const float* __restric
     g[r] = (j >= 0 && j < Tp) ? p[j] * (dp[j] - D) : 0.0f;
   }
   for (int j = lane; j < Tp; j += 64) dp[j] = p[j] * (dp[j] - D);
+  if (adrop.thr)
+    for (int j = lane; j < Tp; j += 64) p[j] *= drop_mul(adrop, (uint64_t)row * Tp + j);
 }
 
 // Row reduction over one block's 32 query rows for values held in 32x32 accumulator layout
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
     const bf16_t* __restrict__ qk, long ldqk, const bf16_t* __restrict__ Vt, int vt_rows, int Tpad,
     const bf16_t* __restrict__ pos, long ldp, const float* __restrict__ dctx, long ld_dctx,
     const int32_t* __restrict__ lens, int B, int Tp, int H, int dkp, int cl, int cr, bf16_t* __restrict__ Pg,
-    bf16_t* __restrict__ dSg, long sld, bf16_t* __restrict__ G, long gld) {
+    bf16_t* __restrict__ dSg, long sld, bf16_t* __restrict__ G, long gld, Drop adrop) {
   constexpr int BDP = 97;                       // row pitch (floats) of a wave's BD image
   extern __shared__ float bd_all[];             // [nw][32][BDP]
   __shared__ float red[8 * 32], fin[32];
@@ -471,6 +477,15 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
     }
   }
   block_rows<false>(sum, red, fin, w, nw, lane);
+  // attention dropout: dp is the gradient of the dropped probabilities -> chain through the mask
+  if (adrop.thr) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const uint64_t rb = ((uint64_t)bh * Tp + (uint64_t)min(i0 + acc_row(e, lane), Tp - 1)) * (uint64_t)Tp;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) dp[c][e] *= drop_mul(adrop, rb + (uint64_t)(64 * w + 32 * c + l32));
+    }
+  }
   float D[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -492,10 +507,12 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int row = acc_row(e, lane);
+    const uint64_t rb = ((uint64_t)bh * Tp + (uint64_t)min(i0 + row, Tp - 1)) * (uint64_t)Tp;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int j = 64 * w + 32 * c + l32;
-      Ps[row * SP + j] = f2bf(sc[c][e]);
+      // P goes to the dv GEMM: the dropped probabilities (the forward's P.V operand)
+      Ps[row * SP + j] = f2bf(adrop.thr ? sc[c][e] * drop_mul(adrop, rb + j) : sc[c][e]);
       dSs[row * SP + j] = f2bf(sc[c][e] * (dp[c][e] - D[e]));
     }
   }
@@ -574,7 +591,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
                                 const void* P, long ldp, const int32_t* lens, int B, int Tp, int H, int dk, int dkp,
                                 int ctx_left, int ctx_right, const float* dctx, long ld_dctx, float* dq, float* dk_,
                                 float* dv, long ld_dqkv, float* dpos, long ld_dpos, float* du, float* dvb, char* ws,
-                                hipStream_t st) {
+                                hipStream_t st, Drop adrop) {
   if (B <= 0 || Tp <= 0) return;
   const BwdGeom g(B, Tp, H, dk);
   float* S = (float*)ws;                          // scores -> P
@@ -606,7 +623,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     auto go = [&](auto kern) {
       if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       cfm_launch(kern, grid, block, lds, st, q16, ldqk, (const bf16_t*)Vt, vt_rows, Tpad, (const bf16_t*)P, ldp, dctx,
-                 ld_dctx, lens, B, Tp, H, dkp, ctx_left, ctx_right, P16, dS16, g.sld, G16, g.gld);
+                 ld_dctx, lens, B, Tp, H, dkp, ctx_left, ctx_right, P16, dS16, g.sld, G16, g.gld, adrop);
     };
     switch (dkp / 16) {
       case 1: go(attn_bwd_scores_kernel<1>); break;
@@ -647,7 +664,7 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     a.M = Tp; a.N = Tp; a.K = dk; a.Z2 = H; a.alpha = 1.0f; a.accumulate = 0;
     bgemm(dt, a, OP_F32, OP_CT, Z, st);
   }
-  if (!fused) cfm_launch(attn_dscore_kernel, dim3(rows_blocks), dim3(256), 0, st, (const float*)S, dP, g.sld, BD, g.gld, B, H, Tp);
+  if (!fused) cfm_launch(attn_dscore_kernel, dim3(rows_blocks), dim3(256), 0, st, S, dP, g.sld, BD, g.gld, B, H, Tp, adrop);
   float* G = BD;
   // d(q+u) = dS . k / sqrt(dk) -> dq
   {

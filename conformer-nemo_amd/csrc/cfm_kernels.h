@@ -126,9 +126,11 @@ void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, co
 void transpose_out(const float* X, int B, int Tp, int d, float* y_bdt, hipStream_t st);
 // qk: [(q+u)*c | (q+v)*c | k] per row (ldqk = 3*H*dkp, c = log2(e)/sqrt(dk)), written by the EPI_QKV
 // GEMM epilogue; the softmax then runs in base 2 on unscaled score sums.
+// adrop: training-mode dropout of the attention probabilities (multi_head_attention.py:111).
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,
                        long ldp, const int32_t* lens, int B, int Tp, int H,
-                       int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st);
+                       int dk, int dkp, int ctx_left, int ctx_right, void* out, long ldo, hipStream_t st,
+                       Drop adrop = Drop{0u, 0u, 1.0f});
 // Natural-layout variant (bf16, LDS-resident kernel; attn_natural_layout() says when it applies):
 // qkv rows are [q | k | v] exactly as a plain bias GEMM stores them (heads padded to dkp); uv =
 // [pos_bias_u | pos_bias_v] (fp32, H*dkp each); the kernel forms (q+u)*qscale, (q+v)*qscale and
@@ -150,7 +152,7 @@ void rel_pos_attention_backward(int dtype, const void* qk, long ldqk, const void
                                 const void* P, long ldp, const int32_t* lens, int B, int Tp, int H, int dk, int dkp,
                                 int ctx_left, int ctx_right, const float* dctx, long ld_dctx, float* dq, float* dk_,
                                 float* dv, long ld_dqkv, float* dpos, long ld_dpos, float* du, float* dvb, char* ws,
-                                hipStream_t st);
+                                hipStream_t st, Drop adrop = Drop{0u, 0u, 1.0f});
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
 
 // ---- backward building blocks (backward.hip) ----

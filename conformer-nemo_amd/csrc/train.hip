@@ -324,6 +324,13 @@ __global__ __launch_bounds__(256) void scale_drop_kernel(const float* x, float a
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     y[i] = alpha * x[i] * drop_mul(drop, (uint64_t)i);
 }
+// dropout_emb on the positional-embedding window (multi_head_attention.py:316, RelPositionalEncoding
+// returns dropout_emb(pos_emb)): one mask for every layer, in the compute type (linear_pos's A operand)
+template <typename T>
+__global__ __launch_bounds__(256) void pe_drop_kernel(const T* __restrict__ pe, long n, Drop drop, T* __restrict__ out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    st_f<T>(out + i, ld_f<T>(pe + i) * drop_mul(drop, (uint64_t)i));
+}
 // GLU(dim=1) + pad mask (conformer_modules.py:162-167): g = a * sigmoid(gate), 0 on padded frames;
 // fp32 for the tape and the compute type for the depthwise conv.
 template <typename T>
@@ -978,6 +985,7 @@ struct Ws {
   // backward
   long gA, gB, dbr, dU, pa, pat, pbt, wt, wtl[7], part, dqkv, dctx, dP, dpre, dG, dD, red;
   long dX2, dcol, i2c, dy1, c1part, gtmp, attws;
+  long ped;   // dropout_emb: the dropped positional window (2T'-1, d) in the compute type
   long total;
 };
 
@@ -1058,6 +1066,7 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.c1part = a.take(c1ch * 10L * g.C * 4 + 4096);
   w.gtmp = a.take(std::max({d * (long)g.F2 * g.C, 9L * g.C * g.C, 3 * d * d + 3 * d}) * 4);
   w.attws = a.take((long)rel_pos_attention_backward_ws(g.B, g.Tp, g.H, g.dk) + 256);
+  w.ped = a.take((long)g.NP * d * es + 64);
   w.total = round_up(a.off, 256);
   return w;
 }
@@ -1093,6 +1102,24 @@ struct Step {
   int kpad(long k) const { return (int)round_up(k, g.kg); }
   int npad(long n) const { return (int)round_up(n, GEMM_BN); }
   Drop drop(int site) const { return make_drop(o->dropout, o->seed, site); }
+  // attention-probability dropout of layer l (site j = 6) and the positional-embedding dropout
+  // (its own site past the layers'); both regenerated bit for bit by the backward
+  Drop drop_att(int l) const { return make_drop(o->dropout_att, o->seed, 1 + 8 * l + 6); }
+  Drop drop_emb() const { return make_drop(o->dropout_emb, o->seed, 1 + 8 * g.L); }
+  // the positional window linear_pos reads: h->pe's slice, or its dropout_emb copy in the workspace
+  const char* pos_window() const {
+    const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * g.d * g.es;
+    const Drop de = drop_emb();
+    if (!de.thr) return pe_slice;
+    const long n = (long)g.NP * g.d;
+    if (g.dt == DT_F32)
+      cfm_launch(pe_drop_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, (const float*)pe_slice, n, de,
+                 W_<float>(wl.ped));
+    else
+      cfm_launch(pe_drop_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, (const bf16_t*)pe_slice, n, de,
+                 W_<bf16_t>(wl.ped));
+    return W_(wl.ped);
+  }
 
   void pack(const void* src, bool src_ct, long ld, int rows, int cols, bool tr, float scale, void* dst, long dld,
             int rp, int cp, int fn = 0, Drop dr = Drop{0, 0, 1.0f}, int ones_row = -1) const {
@@ -1305,8 +1332,8 @@ void check_common(cfm_encoder* h, const float* const* params, int n_params, int 
   if (h->has_out_proj) fail(CFM_ERR_UNSUPPORTED, "training with feat_out projection is not built");
   if (h->K != 31) fail(CFM_ERR_UNSUPPORTED, "training is built for conv_kernel_size 31");
   if (o->dropout < 0.0f || o->dropout >= 1.0f) fail(CFM_ERR_INVALID_ARG, "dropout must be in [0, 1)");
-  if (o->dropout_att != 0.0f) fail(CFM_ERR_UNSUPPORTED, "attention-probability dropout is not built (dropout_att must be 0)");
-  if (o->dropout_emb != 0.0f) fail(CFM_ERR_UNSUPPORTED, "positional-embedding dropout is not built (dropout_emb must be 0)");
+  if (o->dropout_att < 0.0f || o->dropout_att >= 1.0f) fail(CFM_ERR_INVALID_ARG, "dropout_att must be in [0, 1)");
+  if (o->dropout_emb < 0.0f || o->dropout_emb >= 1.0f) fail(CFM_ERR_INVALID_ARG, "dropout_emb must be in [0, 1)");
   if (o->world < 1) fail(CFM_ERR_INVALID_ARG, "world must be >= 1");
   if (h->d % 8 || h->C % 8) fail(CFM_ERR_UNSUPPORTED, "d_model and conv channels must be multiples of 8");
 }
@@ -1346,7 +1373,7 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
     if (dr.thr) cfm_launch(scale_drop_kernel, dim3(ew_grid((long)M * d)), dim3(256), 0, st, (const float*)xcur, 1.0f,
                            (long)M * d, dr, xcur);
   }
-  const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
+  const char* pe_slice = S.pos_window();
   const long n_md = (long)M * d;
 
   for (int l = 0; l < g.L; ++l) {
@@ -1414,7 +1441,8 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       e.Vt = S.T_(t.vt); e.H = H; e.dkp = dkp; e.vt_rows = h->vt_rows; e.Tpad = g.Tpad; e.Tp = g.Tp;
       gemm(dt, S.T_(t.hn[1]), d, M, d, S.W_(S.wl.wqkv), S.kpad(d), (int)(3 * HP), e, h->zero_page, st);
       rel_pos_attention(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B, g.Tp, H,
-                        g.dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, S.T_(t.ctx), d, st);
+                        g.dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, S.T_(t.ctx), d, st,
+                        S.drop_att(l));
       S.gemm_resid_drop(S.T_(t.ctx), d, M, d, S.W_(S.wl.wout), d, S.W_<float>(S.wl.bout), 1.0f, X[1], X[2], d,
                         S.drop(site(l, 2)));
     }
@@ -1498,6 +1526,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   void* wt = S.W_(S.wl.wt);
   const long Mq = g.Mq;
   auto Gp = [&](int i) -> float* { return G ? G[i] : nullptr; };
+  const char* pos_win = S.pos_window();   // the forward's (dropout_emb) positional window
   // Linear y = x W^T + b backward for a dense fp32 output gradient dy (M, N):
   //   dx (M, K) fp32 (ldx; accumulate or overwrite), dW (N, K) -> G[gw], db -> G[gb]
   //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
@@ -1647,10 +1676,12 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       const int dk = g.dk;
       rel_pos_attention_backward(dt, S.T_(t.qk), 3 * HP, S.T_(t.vt), h->vt_rows, g.Tpad, S.T_(t.P), HP, lens, g.B,
                                  g.Tp, H, dk, dkp, h->cfg.att_context_left, h->cfg.att_context_right, dctx, d, dqkv,
-                                 dqkv + d, dqkv + 2 * d, 3L * d, dP, d, Gp(q.pu), Gp(q.pv), S.W_(S.wl.attws), st);
-      // linear_pos (no bias): dWpos = dP^T . pos_emb   (pos_emb rows = the PE window, compute type)
+                                 dqkv + d, dqkv + 2 * d, 3L * d, dP, d, Gp(q.pu), Gp(q.pv), S.W_(S.wl.attws), st,
+                                 S.drop_att(l));
+      // linear_pos (no bias): dWpos = dP^T . pos_emb   (pos_emb rows = the PE window after
+      // dropout_emb, regenerated from the step's seed; compute type)
       if (Gp(q.pos_w)) {
-        const char* pe_slice = h->pe + (long)(h->max_len - g.Tp) * d * es;
+        const char* pe_slice = pos_win;
         S.pack(dP, false, d, g.NP, d, true, 1.0f, pat, Mq, d, (int)Mq);
         S.pack(pe_slice, true, d, g.NP, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
         S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), nullptr);

@@ -99,8 +99,8 @@ typedef int (*cfm_allreduce_fn)(void* user, float* buf, int64_t n, void* stream)
 
 typedef struct cfm_train_opts {
   float dropout;               /* ConformerEncoder(dropout=): embedding, FFN inner and residual-branch dropout */
-  float dropout_emb;           /* must be 0 (positional-embedding dropout not built; yaml default 0.0)      */
-  float dropout_att;           /* must be 0 (attention-probability dropout not built)                        */
+  float dropout_emb;           /* dropout_emb on the positional window (multi_head_attention.py:316)        */
+  float dropout_att;           /* dropout_att on the attention probabilities (multi_head_attention.py:111)   */
   float bn_momentum;           /* nn.BatchNorm1d momentum (0.1)                                               */
   int update_running_stats;    /* 1: update running_mean / running_var in place                              */
   int world;                   /* ranks sharing the BatchNorm statistics (1 = plain BatchNorm1d)             */

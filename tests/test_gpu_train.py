@@ -122,3 +122,68 @@ def test_train_then_eval_uses_updated_running_stats():
         y1, _ = enc.eval()(audio_signal=x, length=ln)
     assert int(enc.layers[0].conv.batch_norm.num_batches_tracked) == 1
     assert not torch.equal(y0, y1)   # eval repacked the in-place-updated running statistics
+
+
+def _enc_drop(z, compute, dropout_att, dropout_emb, dropout=0.0):
+    from nemo.collections.asr.modules import ConformerEncoder
+    from recipe import make_state_dict
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(**cfg, dropout=dropout, dropout_emb=dropout_emb, dropout_att=dropout_att)
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
+    enc.set_compute_mode(compute)
+    return enc.cuda().train()
+
+
+def _step(z, compute, seed, dropout_att, dropout_emb, perturb=None):
+    torch.manual_seed(seed)
+    enc = _enc_drop(z, compute, dropout_att, dropout_emb)
+    if perturb is not None:
+        name, v, h = perturb
+        with torch.no_grad():
+            dict(enc.named_parameters())[name].add_(h * v)
+    x = torch.from_numpy(z["x"]).cuda()
+    ln = torch.from_numpy(z["lengths"]).cuda()
+    y, _ = enc(audio_signal=x, length=ln)
+    loss = (y.double() * torch.from_numpy(z["dy"]).cuda().double()).sum()
+    loss.backward()
+    return enc, y.detach(), float(loss)
+
+
+@pytest.mark.parametrize("case", ["train_tiny", "train_tiny_ctx"])
+def test_attention_and_embedding_dropout(case):
+    """dropout_att (attention probabilities, multi_head_attention.py:111) and dropout_emb (positional
+    window, :316), as conformer_ctc_bpe.yaml:130-132 trains: the masks are a function of the step's
+    seed only (bitwise-reproducible), they change the output, the native backward regenerates them
+    (finite-difference directional derivatives along weights whose gradient flows through the dropped
+    probabilities (linear_q, linear_v) and the dropped positional window (linear_pos)), and the bf16
+    fused attention backward applies the same masks as the fp32 materialised one."""
+    z = np.load(os.path.join(GOLDEN, case + ".npz"))
+    enc, y0, _ = _step(z, "fp32", 7, 0.1, 0.1)
+    _, y1, _ = _step(z, "fp32", 7, 0.1, 0.1)
+    assert torch.equal(y0, y1)
+    _, y_nodrop, _ = _step(z, "fp32", 7, 0.0, 0.0)
+    assert rel_l2(y0.cpu().numpy(), y_nodrop.cpu().numpy()) > 1e-3
+    grads = {n: p.grad.clone() for n, p in enc.named_parameters()}
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for name in ("layers.0.self_attn.linear_q.weight", "layers.0.self_attn.linear_v.weight",
+                 "layers.0.self_attn.linear_pos.weight", "layers.1.self_attn.linear_k.weight"):
+        if name not in grads:
+            continue
+        v = torch.randn(grads[name].shape, device="cuda", generator=g)
+        gd = float((grads[name].double() * v.double()).sum())
+        h = 1e-3
+        lp = _step(z, "fp32", 7, 0.1, 0.1, (name, v, h))[2]
+        lm = _step(z, "fp32", 7, 0.1, 0.1, (name, v, -h))[2]
+        fd = (lp - lm) / (2 * h)
+        assert abs(fd - gd) <= 2e-2 * max(abs(gd), 1.0), (name, fd, gd)
+    # bf16 (fused attention backward) against fp32 (materialised), same seed -> same masks
+    # (linear_k.bias has an analytically zero gradient: relative to a floor of 1e-2 x the largest norm)
+    enc16, _, _ = _step(z, "bf16", 7, 0.1, 0.1)
+    floor = 1e-2 * max(float(g_.norm()) for g_ in grads.values())
+    for n, p in enc16.named_parameters():
+        if "self_attn" in n:
+            ref = grads[n].double()
+            e = float((p.grad.double() - ref).norm()) / max(float(ref.norm()), floor)
+            assert e <= GATE_G["bf16"], (n, e)
