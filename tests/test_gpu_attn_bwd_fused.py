@@ -71,3 +71,32 @@ def test_fused_attention_backward_matches_fp32(case):
             assert float(got["dq"][b * T + L:(b + 1) * T].abs().max()) == 0.0
             assert float(got["dk"][b * T + L:(b + 1) * T].abs().max()) == 0.0
             assert float(got["dv"][b * T + L:(b + 1) * T].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_attention_backward_t250_matches_reference(compute):
+    """The attention backward at the BASELINE shape (T'=250, dk=64, 8 heads, padded second utterance)
+    against the REFERENCE RelPositionMultiHeadAttention's float64 autograd (tests/golden/bwd_attn_t250.npz:
+    identity projections, so its gradients are those of the attention core w.r.t. q, k, v, p).
+    bf16 runs the fused score producer on bf16-rounded operands.  Gates: fp32 1e-3, bf16 2e-2."""
+    import os
+    from conftest import GOLDEN, summary_err
+    from gen_large_goldens import attn_inputs
+    from conformer_amd import _lib
+    z = np.load(os.path.join(GOLDEN, "bwd_attn_t250.npz"))
+    B, T, H = int(z["B"]), int(z["T"]), int(z["H"])
+    d = 512
+    dk = d // H
+    q, k, v, p, dctx, u, vb = (torch.from_numpy(a) for a in attn_inputs(int(z["seed"]), B, T, d))
+    lens = torch.from_numpy(z["lens"]).cuda()
+    dt = 0 if compute == "fp32" else 1
+    cast = (lambda t: t.cuda()) if compute == "fp32" else (lambda t: t.bfloat16().cuda())
+    got = _run(_lib.load(), dt, cast(q), cast(k), cast(v), cast(p), u.cuda(), vb.cuda(), lens, B, T, H, dk, -1, -1,
+               dctx.cuda())
+    torch.cuda.synchronize()
+    gate = 1e-3 if compute == "fp32" else 2e-2
+    for name in ("dq", "dk", "dv", "dp"):
+        es, en, ep = summary_err(name, got[name].cpu().numpy(), z, "ref__")
+        assert es <= gate and en <= gate and ep <= 3 * gate, (name, es, en, ep)
+    for name, key in (("du", "ref__du"), ("dvb", "ref__dvb")):
+        assert rel_l2(got[name].cpu().numpy(), z[key]) <= gate, name

@@ -187,3 +187,44 @@ def test_attention_and_embedding_dropout(case):
             ref = grads[n].double()
             e = float((p.grad.double() - ref).norm()) / max(float(ref.norm()), floor)
             assert e <= GATE_G["bf16"], (n, e)
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_train_step_large_matches_reference(compute):
+    """the training step at the Large shape (d_model 512, 8 heads, dk 64, 512 conv
+    channels, T=1000 -> T'=250, ragged lengths; 2 layers) against the REFERENCE encoder's autograd
+    (tests/golden/train_large.npz, summarised: norm + 4096 seeded samples + 2 projections per tensor).
+    This exercises the shapes the toy goldens never reach: the 160k-row conv2 implicit GEMM and its
+    weight gradient, the fused bf16 attention backward at T'=250 / dk=64, split-K weight gradients.
+    Gates: fp32 1e-3 (sampled relL2 and norm) / 3e-3 (projections); bf16 2e-2 on the output, 6e-2
+    on gradients (projections 1.5x)."""
+    from conftest import summary_err
+    from recipe import make_inputs
+    z = np.load(os.path.join(GOLDEN, "train_large.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    B, T = int(z["B"]), int(z["T"])
+    seed = int(z["seed"])
+    enc = _encoder(z, compute)
+    x, ln = make_inputs(B, T, 80, seed + 100, [int(v) for v in z["lengths"]])
+    y, ylen = enc(audio_signal=torch.from_numpy(x).cuda(), length=torch.from_numpy(ln).cuda())
+    R = np.random.default_rng(seed + 200).standard_normal(tuple(y.shape)).astype(np.float32)
+    assert abs(float(np.abs(R).sum()) - float(z["dy_checksum"])) <= 1e-6 * float(z["dy_checksum"])
+    (y * torch.from_numpy(R).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ylen.cpu().numpy(), z["ylen"])
+    gy = GATE_Y[compute]
+    es, en, ep = summary_err("y", y.detach().cpu().numpy(), z, "out__")
+    assert es <= gy and en <= gy and ep <= 3 * gy, ("y", es, en, ep)
+    gg = GATE_G[compute]
+    worst = (0.0, "")
+    # relative to max(|ref|, 1e-2 x the step's largest gradient norm), as test_train_step_matches_reference
+    floor = 1e-2 * max(float(z[k]) for k in z.files if k.startswith("grad__") and k.endswith("__norm"))
+    for name, p in enc.named_parameters():
+        es, en, ep = summary_err(name, p.grad.cpu().numpy(), z, "grad__", floor)
+        worst = max(worst, (max(es, en), name))
+        assert es <= gg and en <= gg and ep <= (3 if compute == "fp32" else 1.5) * gg, (name, es, en, ep)
+    bufs = dict(enc.named_buffers())
+    for k in z.files:
+        if k.startswith("buf__"):
+            assert rel_l2(bufs[k[len("buf__"):]].cpu().numpy(), z[k]) <= gg, k
+    print(f"train_large/{compute}: worst gradient {worst[1]} {worst[0]:.2e}")
