@@ -319,6 +319,9 @@ __global__ __launch_bounds__(256) void resid_drop_kernel(const float* xin, const
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
     xout[i] = xin[i] + alpha * br[i] * drop_mul(drop, (uint64_t)i);
 }
+__global__ void fill_kernel(float* __restrict__ p, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
 // y = alpha * dropout(x) (in place allowed)
 __global__ __launch_bounds__(256) void scale_drop_kernel(const float* x, float alpha, long n, Drop drop, float* y) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
@@ -585,10 +588,17 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restri
 // BatchNorm (train) + Swish, and their backward
 // ---------------------------------------------------------------------------------------------
 // pass 0: mean = s1 / n; pass 1: rstd from s2 / n and the running-stat update (momentum, unbiased)
-__global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2, double n, int d,
+// n = cnt[0]: the frame count behind the sums -- summed over the ranks with them under SyncBatchNorm
+// (ranks may hold different B x T'), so mean / var / the backward's 1/n use the global count
+// (torch.nn.SyncBatchNorm all-gathers the per-rank counts the same way).  Pass 0 also keeps it at
+// mean[d] (the tape) for the backward.
+__global__ void bn_finalize_kernel(const float* __restrict__ s1, const float* __restrict__ s2,
+                                   const float* __restrict__ cnt, int d,
                                    float momentum, float* __restrict__ mean, float* __restrict__ rstd,
                                    float* __restrict__ run_mean, float* __restrict__ run_var, int pass) {
   const int c = blockIdx.x * 256 + threadIdx.x;
+  const double n = (double)cnt[0];
+  if (pass == 0 && c == 0) mean[d] = cnt[0];
   if (c >= d) return;
   if (pass == 0) {
     mean[c] = (float)((double)s1[c] / n);
@@ -632,8 +642,10 @@ __global__ __launch_bounds__(256) void bn_swish_bwd_kernel(const float* __restri
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ xhat,
                                                            const float* __restrict__ gam, const float* __restrict__ rstd,
                                                            const float* __restrict__ sdy, const float* __restrict__ sdyx,
-                                                           float inv_n, long rows, int d, float* __restrict__ dx) {
+                                                           const float* __restrict__ cnt, long rows, int d,
+                                                           float* __restrict__ dx) {
   const long n = rows * d;
+  const float inv_n = (float)(1.0 / (double)cnt[0]);   // the forward's (global) frame count
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const int c = (int)(i % d);
     dx[i] = gam[c] * rstd[c] * (dy[i] - sdy[c] * inv_n - xhat[i] * sdyx[c] * inv_n);
@@ -936,7 +948,7 @@ Tape tape_layout(const cfm_encoder* h, const Geo& g) {
     l.pre = a.take(M * 2 * d * 4);
     l.g = a.take(M * d * 4);
     l.xhat = a.take(M * d * 4);
-    l.mean = a.take(d * 4);
+    l.mean = a.take((d + 1) * 4);   // + the BatchNorm frame count (global under SyncBatchNorm)
     l.rstd = a.take(d * 4);
     l.s = a.take(M * d * es);
   }
@@ -1025,7 +1037,7 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.gt = a.take(M * d * es);
   w.s1 = a.take(d * 4);
   w.s2 = a.take(d * 4);
-  w.sync = a.take(2 * d * 4);
+  w.sync = a.take((2 * d + 2) * 4);   // [sum x | count] then [sum (x - mean)^2]
   // backward
   const long Kmax = std::max({dff, 3 * d, 2 * d, (long)g.F2 * g.C});
   w.gA = a.take(M * d * 4);
@@ -1469,16 +1481,18 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       float* sy = S.W_<float>(S.wl.sync);
       float* mean = S.T_<float>(t.mean);
       float* rstd = S.T_<float>(t.rstd);
-      const double ntot = (double)M * S.o->world;
+      // [sum x (d) | this rank's frame count] summed over the ranks in one call, then [sum (x-mean)^2]
+      float* sy2 = sy + d + 1;
       colred(dwo, nullptr, nullptr, d, M, d, 0, 1.0f, sy, 0, red, st);
-      S.sync(sy, d);
-      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)sy, ntot,
-                 d, 0.0f, mean, rstd, (float*)nullptr, (float*)nullptr, 0);
-      colred(dwo, nullptr, mean, d, M, d, 2, 1.0f, sy + d, 0, red, st);
-      S.sync(sy + d, d);
+      cfm_launch(fill_kernel, dim3(1), dim3(64), 0, st, sy + d, 1L, (float)M);
+      S.sync(sy, d + 1);
+      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)sy,
+                 (const float*)(sy + d), d, 0.0f, mean, rstd, (float*)nullptr, (float*)nullptr, 0);
+      colred(dwo, nullptr, mean, d, M, d, 2, 1.0f, sy2, 0, red, st);
+      S.sync(sy2, d);
       const bool upd = S.o->update_running_stats != 0;
-      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)(sy + d),
-                 ntot, d, S.o->bn_momentum, mean, rstd, upd ? (float*)S.prm(q.bn_rm) : (float*)nullptr,
+      cfm_launch(bn_finalize_kernel, dim3((d + 255) / 256), dim3(256), 0, st, (const float*)sy, (const float*)sy2,
+                 (const float*)(sy + d), d, S.o->bn_momentum, mean, rstd, upd ? (float*)S.prm(q.bn_rm) : (float*)nullptr,
                  upd ? (float*)S.prm(q.bn_rv) : (float*)nullptr, 1);
       if (dt == DT_F32)
         cfm_launch(bn_swish_kernel<float>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dwo, (const float*)mean,
@@ -1648,7 +1662,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       float* dD = dS;   // dS is dead after dZ
       cfm_launch(bn_bwd_apply_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dZ, xhat, S.prm(q.bn_w),
                  S.T_<const float>(t.rstd), (const float*)sy, (const float*)(sy + d),
-                 (float)(1.0 / ((double)M * S.o->world)), (long)M, d, dD);
+                 S.T_<const float>(t.mean) + d, (long)M, d, dD);
       // depthwise conv backward (dx, dw, db) from the fp32 GLU output
       float* dG = dZ;   // dZ is dead after dD
       const size_t dwws = cfm_op_dwconv_backward_ws_size(g.B, g.Tp, d, g.K);

@@ -29,7 +29,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, case="train_tiny_ctx", rows=None):
     for p in (os.path.join(ROOT, "conformer-nemo_amd"), os.path.join(ROOT, "tests", "golden")):
         sys.path.insert(0, p)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -38,7 +38,7 @@ def _worker(rank, world, port, q):
         from nemo.collections.asr.modules import ConformerEncoder
         from recipe import make_state_dict
         torch.cuda.set_device(0)
-        z = np.load(os.path.join(GOLDEN, "train_tiny_ctx.npz"))
+        z = np.load(os.path.join(GOLDEN, case + ".npz"))
         cfg = json.loads(str(z["cfg_json"]))
         enc = ConformerEncoder(**cfg, dropout=0.0, dropout_emb=0.0, dropout_att=0.0)
         sd = make_state_dict(cfg, int(z["seed"]))
@@ -47,36 +47,44 @@ def _worker(rank, world, port, q):
         enc.set_compute_mode("fp32")
         enc = enc.cuda().train()
         cdist.convert_sync_batchnorm(enc)
-        x = cdist.shard_batch(torch.from_numpy(z["x"]), rank, world).cuda()
-        ln = cdist.shard_batch(torch.from_numpy(z["lengths"]), rank, world).cuda()
-        dy = cdist.shard_batch(torch.from_numpy(z["dy"]), rank, world).cuda()
+        if rows is None:   # equal shares, DDP averaging: the global gradient / world
+            sh = lambda a: cdist.shard_batch(torch.from_numpy(a), rank, world)  # noqa: E731
+            scale = 1.0 / world
+        else:              # unequal shares (rows[r]), summed gradients: the global gradient itself
+            sh = lambda a: torch.from_numpy(a[rows[rank]])  # noqa: E731
+            scale = 1.0
+        x, ln, dy = sh(z["x"]).cuda(), sh(z["lengths"]).cuda(), sh(z["dy"]).cuda()
         y, _ = enc(audio_signal=x, length=ln)
         (y * dy).sum().backward()
-        cdist.allreduce_gradients(enc.parameters())
+        cdist.allreduce_gradients(enc.parameters(), average=rows is None)
         torch.cuda.synchronize()
         worst = 0.0
         floor = 1e-2 * max(float(np.linalg.norm(z[k])) for k in z.files if k.startswith("grad__"))
         params = dict(enc.named_parameters())
         for k in z.files:
             if k.startswith("grad__"):
-                ref_g = z[k] / world
+                ref_g = z[k] * scale
                 got = params[k[len("grad__"):]].grad.cpu().numpy()
-                worst = max(worst, float(np.linalg.norm(got - ref_g) / max(np.linalg.norm(ref_g), floor / world)))
+                worst = max(worst, float(np.linalg.norm(got - ref_g) / max(np.linalg.norm(ref_g), floor * scale)))
         bufs = dict(enc.named_buffers())
         wb = max(float(np.linalg.norm(bufs[k[5:]].cpu().numpy() - z[k]) / np.linalg.norm(z[k]))
                  for k in z.files if k.startswith("buf__"))
-        yl = float(np.linalg.norm(y.detach().cpu().numpy() - cdist.shard_batch(torch.from_numpy(z["y"]), rank,
-                                                                               world).numpy()))
+        yl = float(np.linalg.norm(y.detach().cpu().numpy() - sh(z["y"]).numpy()) / np.linalg.norm(sh(z["y"]).numpy()))
         q.put((rank, worst, wb, yl))
     finally:
         dist.destroy_process_group()
 
 
-def test_dp2_syncbn_gradients_match_global_batch():
+@pytest.mark.parametrize("case,rows", [("train_tiny_ctx", None), ("train_tiny", [[0, 1], [2]])],
+                         ids=["equal_shards", "unequal_shards"])
+def test_dp2_syncbn_gradients_match_global_batch(case, rows):
+    """unequal_shards: rank 0 holds 2 utterances, rank 1 one, so the ranks' BatchNorm
+    frame counts differ; SyncBatchNorm must weight by the global count (as torch.nn.SyncBatchNorm
+    does), giving the global batch's statistics, outputs and (summed) gradients."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case, rows)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -84,4 +92,4 @@ def test_dp2_syncbn_gradients_match_global_batch():
         assert p.exitcode == 0
     for rank, worst, wb, yl in sorted(q.get(timeout=5) for _ in range(world)):
         print(f"rank {rank}: worst grad {worst:.2e}, running stats {wb:.2e}, |dy| {yl:.2e}")
-        assert worst <= 1e-3 and wb <= 1e-4
+        assert worst <= 1e-3 and wb <= 1e-4 and yl <= 1e-4
