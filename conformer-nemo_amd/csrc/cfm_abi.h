@@ -53,5 +53,11 @@ inline uint16_t host_f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+inline float host_bf2f(uint16_t v) {
+  const uint32_t u = (uint32_t)v << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
 
 }  // namespace cfm

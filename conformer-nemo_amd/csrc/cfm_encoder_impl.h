@@ -16,6 +16,12 @@ struct LayerW {
   long qkv_w, qkv_b, out_w, out_b, uv;   // uv: pos_bias_u | pos_bias_v, [H][dkp] each, zero-padded
   long pw1_w, pw1_b, dw_w, dw_b, bn_mean, bn_inv, bn_w, bn_b, pw2_w, pw2_b;
   long ln_w[5], ln_b[5];   // ff1, self_att, conv, ff2, out
+  // LayerNorm-folded copies (cfm_encoder::ln_fold): W' = W * diag(gamma) of norm_self_att (q|k|v),
+  // norm_conv (pointwise_conv1, GLU-packed) and norm_feed_forward2 (linear1), with the epilogue's
+  // column terms c[n] = sum_k W'[n][k] and d[n] = sum_k beta[k] W[n][k] + bias[n] (fp32, [Npad]).
+  long qkv_wf = -1, qkv_lc = -1, qkv_ld = -1;
+  long pw1_wf = -1, pw1_lc = -1, pw1_ld = -1;
+  long ff2_w1f = -1, ff2_lc = -1, ff2_ld = -1;
 };
 
 }  // namespace cfm
@@ -40,6 +46,10 @@ struct cfm_encoder {
   // enable_pad_mask (conformer_encoder.py:301-305): false -> the conv module's GLU output is not
   // zeroed at padded frames (pad_mask=None, conformer_modules.py:165-166); attention masks stay.
   bool use_pad_mask = true;
+  // Eval forward, bf16 mode: norm_self_att / norm_conv / norm_feed_forward2 are folded into the
+  // following GEMM (the residual GEMM before each writes the compute-type rows and per-row granule
+  // statistics); off in the fp32 parity mode (CFM_LN_FOLD=0/1 overrides for A/B).
+  bool ln_fold = false;
   std::vector<hipStream_t> sub_streams;
   std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
   void* zero_page = nullptr;

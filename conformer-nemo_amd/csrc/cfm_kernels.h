@@ -89,7 +89,21 @@ struct GemmEpi {
   int wt;              // set by gemm(): 16-byte output stores write-through (sc1), see store16_wt
   const float* Xin;    // EPI_RESID: residual input (null: X, updated in place)
   Drop drop;           // EPI_RESID: dropout on the branch, mask index m * ldx + n (thr 0: none)
+  // LayerNorm folded into the next GEMM (eval forward, bf16 mode; DESIGN.md §4 "LayerNorm fold").
+  // Producer (EPI_RESID): also writes the new X rows in the compute type to xb (ld ldx) and, per row
+  // and 128-column granule g, the granule's (mean, M2) to ln_out[m * ln_parts + g].
+  void* xb;
+  float2* ln_out;
+  int ln_parts;        // granules per row = ceil(N / 128)
+  // Consumer (any compute-type epilogue): the GEMM ran on A = xb with W' = W * diag(gamma); the
+  // epilogue forms LayerNorm(x) . W^T + b = rstd * (acc - mean * ln_c[n]) + ln_d[n] from the row's
+  // granule partials (ln_in, ln_parts per row, ln_width = d columns in all); bias must be null.
+  const float2* ln_in;
+  int ln_width;
+  const float* ln_c;   // [Npad] sum_k W'[n][k] (of the packed, rounded W')
+  const float* ln_d;   // [Npad] sum_k beta[k] W[n][k] + bias[n]
 };
+constexpr int LN_GRANULE = 128;
 
 struct ConvGeom {      // implicit-GEMM A operand for the 2nd subsampling conv (3x3, stride 2, pad 1)
   const void* X1;      // (B, T1, F1, C) channels-last, compute type

@@ -117,6 +117,30 @@ struct Packer {
     const long np = round_up(n, GEMM_BN);
     return f32(nullptr, np, [=](long i) -> float { return i < n ? src[i] : 0.0f; });
   }
+  // W' = val * diag(gamma) packed as mat(), plus the folded-LayerNorm column terms over the packed
+  // (rounded) W': c[n] = sum_k W'[n][k], d[n] = sum_k beta[k] val(n, k) + bias(n)  ([Npad] fp32)
+  long mat_fold(int N, int K, std::function<float(int, int)> val, const float* gamma, const float* beta,
+                std::function<float(int)> bias, long& c_off, long& d_off) {
+    const long o = mat(N, K, [&](int n, int k) { return val(n, k) * gamma[k]; });
+    const long Npad = round_up(N, GEMM_BN);
+    std::vector<float> c(Npad, 0.0f), dd(Npad, 0.0f);
+    if (!dry) {
+      for (int n = 0; n < N; ++n) {
+        double sc = 0.0, sd = 0.0;
+        for (int k = 0; k < K; ++k) {
+          const float v = val(n, k);
+          const float wq = v * gamma[k];
+          sc += (h->es == 4) ? (double)wq : (double)host_bf2f(host_f2bf(wq));
+          sd += (double)beta[k] * (double)v;
+        }
+        c[n] = (float)sc;
+        dd[n] = (float)(sd + (double)bias(n));
+      }
+    }
+    c_off = f32(nullptr, Npad, [&](long i) { return c[i]; });
+    d_off = f32(nullptr, Npad, [&](long i) { return dd[i]; });
+    return o;
+  }
   // packed [Npad][Kpad] compute-type matrix; val(n, k) for n < N, k < K (others zero)
   long mat(int N, int K, std::function<float(int, int)> val) {
     const long Npad = round_up(N, GEMM_BN), Kp = h->kpad(K);
@@ -179,6 +203,18 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
     Lw.ff2_b1 = pk.bias(get(p + "feed_forward2.linear1.bias"), dff);
     Lw.ff2_w2 = mat_plain(p + "feed_forward2.linear2.weight", d, dff);
     Lw.ff2_b2 = pk.bias(get(p + "feed_forward2.linear2.bias"), d);
+    const float* g_att = get(p + "norm_self_att.weight");
+    const float* b_att = get(p + "norm_self_att.bias");
+    const float* g_conv = get(p + "norm_conv.weight");
+    const float* b_conv = get(p + "norm_conv.bias");
+    const float* g_ff2 = get(p + "norm_feed_forward2.weight");
+    const float* b_ff2 = get(p + "norm_feed_forward2.bias");
+    if (h->ln_fold) {
+      const float* w21 = get(p + "feed_forward2.linear1.weight");
+      const float* b21 = get(p + "feed_forward2.linear1.bias");
+      Lw.ff2_w1f = pk.mat_fold(dff, d, [=](int n, int k) { return w21[(long)n * d + k]; }, g_ff2, b_ff2,
+                               [=](int n) { return b21[n]; }, Lw.ff2_lc, Lw.ff2_ld);
+    }
     // q | k | v with per-head padding dk -> dkp
     const float* wq[3] = {get(p + "self_attn.linear_q.weight"), get(p + "self_attn.linear_k.weight"),
                           get(p + "self_attn.linear_v.weight")};
@@ -193,6 +229,17 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       const int part = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
       return dd < dk ? bq[part][hh * dk + dd] : 0.0f;
     });
+    if (h->ln_fold) {
+      auto qv = [&](int n, int k) -> float {
+        const int part = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
+        return dd < dk ? wq[part][(long)(hh * dk + dd) * d + k] : 0.0f;
+      };
+      auto qb = [&](int n) -> float {
+        const int part = n / (H * dkp), r = n % (H * dkp), hh = r / dkp, dd = r % dkp;
+        return dd < dk ? bq[part][hh * dk + dd] : 0.0f;
+      };
+      Lw.qkv_wf = pk.mat_fold(3 * H * dkp, d, qv, g_att, b_att, qb, Lw.qkv_lc, Lw.qkv_ld);
+    }
     Lw.out_w = mat_plain(p + "self_attn.linear_out.weight", d, d);
     Lw.out_b = pk.bias(get(p + "self_attn.linear_out.bias"), d);
     const float* pu = get(p + "self_attn.pos_bias_u");
@@ -216,6 +263,11 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
       const int s = glu_src((int)n);
       return s < 0 ? 0.0f : b1[s];
     });
+    if (h->ln_fold) {
+      Lw.pw1_wf = pk.mat_fold(64 * G, d, [&](int n, int k) { const int s = glu_src(n); return s < 0 ? 0.0f : w1[(long)s * d + k]; },
+                              g_conv, b_conv, [&](int n) { const int s = glu_src(n); return s < 0 ? 0.0f : b1[s]; },
+                              Lw.pw1_lc, Lw.pw1_ld);
+    }
     const float* dww = get(p + "conv.depthwise_conv.weight");          // (d, 1, K) -> [K][d]
     Lw.dw_w = pk.f32(nullptr, (long)d * K, [&](long i) -> float { return dww[(i % d) * K + i / d]; });
     Lw.dw_b = pk.f32(get(p + "conv.depthwise_conv.bias"), d);
@@ -283,7 +335,7 @@ void ensure_streams(cfm_encoder* h, int n) {
 // workspace layout
 // ---------------------------------------------------------------------------------------------
 struct WsLayout {
-  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, total;
+  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, LS, total;
   int T1, T2, Tp, M, Tpad;
 };
 
@@ -311,6 +363,7 @@ WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
   w.P = take((long)(2 * w.Tp - 1) * h->L * h->H * h->dkp * es + 64);
   w.PN = h->cfg.conv_norm_type == 1 ? take(M * h->d * 4) : -1;
   w.Y = h->has_out_proj ? take(M * h->dout * 4) : -1;
+  w.LS = h->ln_fold ? take(M * ((h->d + LN_GRANULE - 1) / LN_GRANULE) * 8) : -1;   // folded-LayerNorm row partials
   w.total = round_up(off, 256);
   return w;
 }
@@ -384,6 +437,8 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     HIP_OK(hipMemset(h->zero_page, 0, 4096));
     build_pe(h.get(), std::max(cfg->pos_emb_max_len, 1));
     if (const char* mb = getenv("CFM_MICROBATCH")) h->microbatches = std::max(1, std::min(8, atoi(mb)));
+    h->ln_fold = h->dtype == DT_BF16 && h->d % 4 == 0;
+    if (const char* lf = getenv("CFM_LN_FOLD")) h->ln_fold = atoi(lf) != 0 && h->d % 4 == 0;
     ensure_streams(h.get(), 8);
     HIP_OK(hipSetDevice(prev));
     *out = h.release();
@@ -559,6 +614,19 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
     auto Wf = [&](long off) { return (const float*)(h->wbuf + off); };
     float* X = (float*)(ws + wl.X);
     void* Hn = ws + wl.Hn;
+    // LayerNorm fold (bf16 eval): the residual GEMMs ahead of norm_self_att / norm_conv /
+    // norm_feed_forward2 also write the new rows in bf16 to Hn and their granule statistics to LS;
+    // the next GEMM runs on those rows with gamma folded into its weight (GemmEpi::ln_in)
+    const bool fold = h->ln_fold && L > 0;
+    const int lnp = (d + LN_GRANULE - 1) / LN_GRANULE;
+    float2* lns = fold ? (float2*)(ws + wl.LS) : nullptr;
+    auto produce = [&](GemmEpi& r) {
+      if (fold) { r.xb = Hn; r.ln_out = lns; r.ln_parts = lnp; }
+    };
+    auto consume = [&](GemmEpi& e, long lc, long ld) {
+      if (!fold) return;
+      e.bias = nullptr; e.ln_in = lns; e.ln_parts = lnp; e.ln_width = d; e.ln_c = Wf(lc); e.ln_d = Wf(ld);
+    };
 
     // lengths (subsampling.py:164-171) -> out_len_b, used as the pad mask from here on
     TM(ST_LEN);
@@ -605,17 +673,22 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         TM(ST_FFN_DOWN);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff1_b2), 0.5f);
         r.X = X; r.ldx = d;
+        produce(r);
         gemm(dt, ws + wl.U, h->dff, M, h->dff, W(Lw.ff1_w2), (int)h->kpad(h->dff), d, r, h->zero_page, st);
       }
       // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
-      TM(ST_LN);
-      layernorm(dt, X, M, d, Wf(Lw.ln_w[1]), Wf(Lw.ln_b[1]), nullptr, nullptr, nullptr, Hn, 0, st);
+      if (!fold) {
+        TM(ST_LN);
+        layernorm(dt, X, M, d, Wf(Lw.ln_w[1]), Wf(Lw.ln_b[1]), nullptr, nullptr, nullptr, Hn, 0, st);
+      }
+      const long qkv_w = fold ? Lw.qkv_wf : Lw.qkv_w;
       if (attn_natural_layout(dt, Tp, dkp)) {
         // plain bias GEMM into [q | k | v]; the attention kernel adds u / v, scales and transposes V
         TM(ST_QKV);
         GemmEpi e = epi_of(EPI_STORE, Wf(Lw.qkv_b));
         e.C = ws + wl.QK; e.ldc = 3L * H * dkp;
-        gemm(dt, Hn, d, M, d, W(Lw.qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
+        consume(e, Lw.qkv_lc, Lw.qkv_ld);
+        gemm(dt, Hn, d, M, d, W(qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
         TM(ST_ATTN);
         rel_pos_attention_natural(ws + wl.QK, 3L * H * dkp, Wf(Lw.uv), attn_qscale(h->dk),
                                   Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk, dkp,
@@ -626,7 +699,8 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         e.C = ws + wl.QK; e.ldc = 3L * H * dkp; e.qk_cols = 2 * H * dkp; e.uv = Wf(Lw.uv);
         e.qscale = attn_qscale(h->dk);
         e.Vt = ws + wl.Vt; e.H = H; e.dkp = dkp; e.vt_rows = h->vt_rows; e.Tpad = wl.Tpad; e.Tp = Tp;
-        gemm(dt, Hn, d, M, d, W(Lw.qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
+        consume(e, Lw.qkv_lc, Lw.qkv_ld);
+        gemm(dt, Hn, d, M, d, W(qkv_w), (int)h->kpad(d), 3 * H * dkp, e, h->zero_page, st);
         TM(ST_ATTN);
         rel_pos_attention(dt, ws + wl.QK, 3L * H * dkp, ws + wl.Vt, h->vt_rows, wl.Tpad,
                           Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk,
@@ -636,16 +710,20 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         TM(ST_OUTPROJ);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.out_b), 1.0f);
         r.X = X; r.ldx = d;
+        produce(r);
         gemm(dt, ws + wl.O, d, M, d, W(Lw.out_w), (int)h->kpad(d), d, r, h->zero_page, st);
       }
       // ---- convolution module (conformer_modules.py:112-114, 160-180) ----
-      TM(ST_LN);
-      layernorm(dt, X, M, d, Wf(Lw.ln_w[2]), Wf(Lw.ln_b[2]), nullptr, nullptr, nullptr, Hn, 0, st);
+      if (!fold) {
+        TM(ST_LN);
+        layernorm(dt, X, M, d, Wf(Lw.ln_w[2]), Wf(Lw.ln_b[2]), nullptr, nullptr, nullptr, Hn, 0, st);
+      }
       {
         TM(ST_PW1);
         GemmEpi e = epi_of(EPI_GLU_MASK, Wf(Lw.pw1_b));
         e.C = ws + wl.G; e.ldc = d; e.lens = h->use_pad_mask ? lens : nullptr; e.Tp = Tp;
-        gemm(dt, Hn, d, M, d, W(Lw.pw1_w), (int)h->kpad(d), d, e, h->zero_page, st);
+        consume(e, Lw.pw1_lc, Lw.pw1_ld);
+        gemm(dt, Hn, d, M, d, W(fold ? Lw.pw1_wf : Lw.pw1_w), (int)h->kpad(d), d, e, h->zero_page, st);
         TM(ST_DWCONV);
         if (h->cfg.conv_norm_type == 0) {
           dwconv_norm_swish(dt, ws + wl.G, B, Tp, d, h->K, Wf(Lw.dw_w), Wf(Lw.dw_b), Wf(Lw.bn_mean), Wf(Lw.bn_inv),
@@ -659,16 +737,20 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         TM(ST_PW2);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.pw2_b), 1.0f);
         r.X = X; r.ldx = d;
+        produce(r);
         gemm(dt, ws + wl.S, d, M, d, W(Lw.pw2_w), (int)h->kpad(d), d, r, h->zero_page, st);
       }
       // ---- FFN2 (conformer_modules.py:116-118) ----
-      TM(ST_LN);
-      layernorm(dt, X, M, d, Wf(Lw.ln_w[3]), Wf(Lw.ln_b[3]), nullptr, nullptr, nullptr, Hn, 0, st);
+      if (!fold) {
+        TM(ST_LN);
+        layernorm(dt, X, M, d, Wf(Lw.ln_w[3]), Wf(Lw.ln_b[3]), nullptr, nullptr, nullptr, Hn, 0, st);
+      }
       {
         TM(ST_FFN_UP);
         GemmEpi e = epi_of(EPI_SWISH, Wf(Lw.ff2_b1));
         e.C = ws + wl.U; e.ldc = h->dff;
-        gemm(dt, Hn, d, M, d, W(Lw.ff2_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
+        consume(e, Lw.ff2_lc, Lw.ff2_ld);
+        gemm(dt, Hn, d, M, d, W(fold ? Lw.ff2_w1f : Lw.ff2_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
         TM(ST_FFN_DOWN);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff2_b2), 0.5f);
         r.X = X; r.ldx = d;

@@ -54,7 +54,11 @@ struct Tile {
   static constexpr int STAGE_BYTES = (BM + BN) * BKB;
   static constexpr int EPS = BN;     // fp32 stride of the epilogue image (row writes / 16-B row reads are conflict-free)
   static constexpr int EPI_BYTES = BM / EP * EPS * 4;
-  static constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > EPI_BYTES) ? NSTAGE * STAGE_BYTES : EPI_BYTES;
+  // folded LayerNorm (GemmEpi::ln_in) tables behind the ring / image: per row (mean, rstd), per
+  // column (c, d)
+  static constexpr int RS_OFF = (NSTAGE * STAGE_BYTES > EPI_BYTES) ? NSTAGE * STAGE_BYTES : EPI_BYTES;
+  static constexpr int CD_OFF = RS_OFF + BM * 8;
+  static constexpr int LDS_BYTES = CD_OFF + BN * 8;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
   static_assert(BKB == 64 || BKB == 128, "stage depth");
   static_assert(GEMM_BK_BYTES % BKB == 0, "packed K granule");
@@ -187,7 +191,8 @@ struct ALoadConv {
   }
 };
 
-thread_local int g_splits = 1;   // grid.y of the next split-K launch (gemm_splitk)
+thread_local int g_splits = 1;
+constexpr int LN_PRE = 4;   // folded-LayerNorm granule partials prefetched per row (d <= 512 fully)   // grid.y of the next split-K launch (gemm_splitk)
 
 struct GemmParams {
   const char* W; long ldw_b; int kb; int Mtiles, Ntiles; int M, N;   // kb = packed K bytes per row
@@ -201,10 +206,32 @@ struct GemmParams {
 // Every global load here is unconditional (clamped address, value selected afterwards): a load
 // under a per-thread condition is branched around by hipcc and serialised behind its own
 // vmcnt(0) (cdna_hip_programming.md §5, 'Three .s-level traps' (c)).
-template <typename T, int EPI, class TL>
-CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, long xoff) {
+// Folded LayerNorm (GemmEpi::ln_in): rs[r] = (mean, rstd) of the pass's local row r, cd[j] = (c, d)
+// of the tile's local column j.
+CFM_DEV float ln_fold(float2 s, float v, float2 cd) { return s.y * (v - s.x * cd.x) + cd.y; }
+
+// Sum over the 32 lanes of a half-wave, the same value in every lane: DPP quad permutes and row
+// mirrors (VALU) for 16 lanes, one xor-16 shuffle.
+template <int CTRL> CFM_DEV float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+CFM_DEV float halfwave_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror: lane i <- 7 - i (the other quad of the 8)
+  v += dpp_mov<0x140>(v);   // row_mirror: lane i <- 15 - i (the other 8 of the row)
+  v += __shfl_xor(v, 16, 32);
+  return v;
+}
+
+// FOLD: the LayerNorm fold is active for this launch (GemmEpi::ln_in set: consumer; ln_out / xb
+// set: EPI_RESID producer) - a compile-time flag, so no per-element branches in the unrolled loops.
+template <typename T, int EPI, class TL, bool FOLD>
+CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, long xoff, const float2* rs,
+                      const float2* cd) {
   const GemmEpi& e = p.epi;
   const int tid = threadIdx.x;
+  constexpr bool fold = FOLD;
   if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
     // fp32 output (N % 4 == 0), 4 columns per thread-chunk
     constexpr int CPR = TL::BN / 4;                 // chunks per row
@@ -256,6 +283,32 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
         if (e.wt) store16_wt(e.X, off * 4, make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
                                                       __float_as_uint(o.w)));
         else *(float4*)(e.X + off) = o;
+        if constexpr (EPI == EPI_RESID && FOLD) {
+          {   // compute-type copy of the new rows: the A operand of the LayerNorm-folded GEMM
+            if constexpr (sizeof(T) == 2) {
+              *(uint2*)((T*)e.xb + off) = make_uint2((uint32_t)f2bf(o.x) | ((uint32_t)f2bf(o.y) << 16),
+                                                     (uint32_t)f2bf(o.z) | ((uint32_t)f2bf(o.w) << 16));
+            } else {
+              *(float4*)((T*)e.xb + off) = o;
+            }
+          }
+        }
+      }
+      if constexpr (EPI == EPI_RESID && FOLD) {
+        {
+          // (mean, M2) of this row's 128-column granule: the 32 consecutive threads holding it reduce
+          // by xor shuffles inside their half-wave (CPR % 32 == 0), two passes (mean, then the
+          // squared deviations) - no cancellation
+          static_assert(CPR % 32 == 0, "LayerNorm granule = 32 threads x 4 columns");
+          const bool ok = colok && m < p.M;
+          const int g = (n0 + (cc & ~31) * 4) / LN_GRANULE;
+          const int cnt = min(LN_GRANULE, p.N - g * LN_GRANULE);
+          const float s = halfwave_sum(ok ? (o.x + o.y) + (o.z + o.w) : 0.0f);
+          const float mean = s / (float)max(cnt, 1);
+          const float a0 = o.x - mean, a1 = o.y - mean, a2 = o.z - mean, a3 = o.w - mean;
+          const float q2 = halfwave_sum(ok ? (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3) : 0.0f);
+          if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, q2);
+        }
       }
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
@@ -278,11 +331,14 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       const int m = m0 + r;
       const int t = m % e.Tp;
       const bool masked = t >= lenq[q];
+      float2 st;
+      if constexpr (fold) st = rs[r];
       float o[VE];
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
-        const float a = img[r * TL::EPS + ca + i];
-        const float g = img[r * TL::EPS + cg + i];
+        float a = img[r * TL::EPS + ca + i];
+        float g = img[r * TL::EPS + cg + i];
+        if constexpr (fold) { a = ln_fold(st, a, cd[ca + i]); g = ln_fold(st, g, cd[cg + i]); }
         o[i] = masked ? 0.0f : a * sigmoidf_(g);
       }
       if (m >= p.M || c >= p.N) continue;
@@ -319,10 +375,13 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
+      float2 st;
+      if constexpr (fold) st = rs[r];
       float o[VE];
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
         float v = img[r * TL::EPS + cc * VE + i];
+        if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
         if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
         if constexpr (EPI == EPI_SWISH) v = swishf(v);
         o[i] = v;
@@ -386,13 +445,18 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
             const int h = nv / e.dkp, dd = nv - h * e.dkp;
             float v[G];
             bool full = true;
+            float2 vcd;
+            if constexpr (fold) vcd = cd[cl];
 #pragma unroll
             for (int q = 0; q < G; ++q) {
               const int t = t0 + q;
               const int r = b * Tp + t - m0;
               const bool own = t < Tp && r >= 0 && b * Tp + t <= mlast;
               if (t < Tp && !own) full = false;
-              v[q] = own ? img[r * TL::EPS + cl] : 0.0f;
+              const int rc = min(max(r, 0), TL::BM - 1);
+              float x = img[rc * TL::EPS + cl];
+              if constexpr (fold) x = ln_fold(rs[rc], x, vcd);
+              v[q] = own ? x : 0.0f;
             }
             T* dst = (T*)e.Vt + (((long)b * e.H + h) * e.vt_rows + dd) * e.Tpad + t0;
             if (full) {
@@ -446,6 +510,19 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     wrow[i] = p.W + koff + (long)(n0 + rr) * p.ldw_b + ((lane % TL::SLOTS) ^ TL::swz(rr)) * 16;
   }
   const uint32_t smem_base = lds_addr(smem);
+
+  // folded LayerNorm operands, loaded now and consumed by the epilogue (the loads complete during
+  // the main loop): row tid's first LN_PRE granule partials, column tid's (c, d)
+  float2 ln_pre[LN_PRE];
+  float2 cd_pre = make_float2(0.0f, 0.0f);
+  if (p.epi.ln_in) {
+    const int np = p.epi.ln_parts;
+    const float2* pp = p.epi.ln_in + (long)min(m0 + min(tid, TL::BM - 1), p.M - 1) * np;
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
+    const int nc = n0 + min(tid, TL::BN - 1);
+    cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
+  }
 
   auto stage = [&](int kt, int slot) {
     const long kb0 = (long)kt * TL::BKB;
@@ -573,6 +650,34 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
     for (int j = 0; j < TL::NR; ++j) bcol[j] = p.epi.bias[n0 + wn * (TL::BN / TL::WN) + j * 32 + col];
   }
+  // folded LayerNorm: (mean, rstd) of row tid from its granule partials (Chan et al.'s pairwise
+  // combination of (count, mean, M2)) and (c, d) of column tid, from the values prefetched at the
+  // kernel start; visible after the first pass's barrier
+  float2* rs_tab = (float2*)(smem + TL::RS_OFF);
+  float2* cd_tab = (float2*)(smem + TL::CD_OFF);
+  if (p.epi.ln_in) {
+    const int W = p.epi.ln_width, np = p.epi.ln_parts;
+    const float2* pp = p.epi.ln_in + (long)min(m0 + min(tid, TL::BM - 1), p.M - 1) * np;
+    float sm = 0.0f;
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g)
+      sm += g < np ? (float)min(LN_GRANULE, W - g * LN_GRANULE) * ln_pre[g].x : 0.0f;
+    for (int g = LN_PRE; g < np; ++g) sm += (float)min(LN_GRANULE, W - g * LN_GRANULE) * pp[g].x;
+    const float mean = sm / (float)W;
+    float m2 = 0.0f;
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g) {
+      const float dm = ln_pre[g].x - mean;
+      m2 += g < np ? ln_pre[g].y + (float)min(LN_GRANULE, W - g * LN_GRANULE) * dm * dm : 0.0f;
+    }
+    for (int g = LN_PRE; g < np; ++g) {
+      const float2 pg = pp[g];
+      const float dm = pg.x - mean;
+      m2 += pg.y + (float)min(LN_GRANULE, W - g * LN_GRANULE) * dm * dm;
+    }
+    if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
+    if (tid < TL::BN) cd_tab[tid] = cd_pre;
+  }
   constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
   for (int pass = 0; pass < TL::EP; ++pass) {
@@ -591,7 +696,12 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
         }
     }
     __syncthreads();
-    epilogue<T, EPI, EpiView<TL>>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x);
+    if (p.epi.ln_in || p.epi.ln_out)
+      epilogue<T, EPI, EpiView<TL>, true>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
+                                          rs_tab + pass * EpiView<TL>::BM, cd_tab);
+    else
+      epilogue<T, EPI, EpiView<TL>, false>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
+                                           rs_tab + pass * EpiView<TL>::BM, cd_tab);
   }
 }
 
@@ -683,6 +793,9 @@ int pick_tile(int dtype, int M, int Nw, int epi, bool conv, int K = 0) {
     // the small-M residual tile must be K-grouped the same way: an utterance's output is then
     // bitwise independent of the batch it runs in (tests/test_gpu_encoder.py)
     if (epi == EPI_RESID) return M >= 4096 ? 14 : 16;
+    // the subsampling Linear (K = C * F2 = 10240, N = d): 64 tiles of 256x256 fill a quarter of the
+    // chip; 128x128 in two K-groups (same K order as the small-M 64x128 K-group tile): 154 -> ~100 us
+    if (epi == EPI_SCALE_F32 && K >= 4096) return M >= 4096 ? 12 : 16;
     return 5;
   }
   if (conv || (long)M * Nw >= (long)32 << 20) return 1;

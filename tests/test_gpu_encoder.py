@@ -179,3 +179,25 @@ def test_dropin_enable_pad_mask():
         y2, _ = enc(audio_signal=x, length=ln)
     yr, _ = O.encoder_forward(z["x"], z["lengths"], sd, dict(cfg, use_pad_mask=True))
     check(y2.cpu().numpy(), yr, "fp32")
+
+
+@pytest.mark.parametrize("path", [f for f in ENC_FILES if "large17" in f or "tiny_ctx" in f or "noxscale_ln" in f],
+                         ids=lambda f: os.path.basename(f)[4:-4])
+def test_bf16_layernorm_fold_matches_unfolded(path, monkeypatch):
+    """bf16 mode folds norm_self_att / norm_conv / norm_feed_forward2 into the following GEMM
+    (DESIGN.md §4 "LayerNorm fold"); CFM_LN_FOLD=0 keeps the three LayerNorm launches.  Both must
+    meet the bf16 gate against the reference and agree with each other to bf16 rounding."""
+    z = np.load(path)
+    cfg = json.loads(str(z["cfg_json"]))
+    sd = make_state_dict(cfg, int(z["seed"]))
+    x = z["x"]
+    lens = z["lengths"] if "lengths" in z.files else None
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_LN_FOLD", flag)   # read when the handle is created
+        y, yl = run(native(cfg, "bf16"), sd, x, lens)
+        assert (yl == z["y_len"]).all()
+        out[flag] = (y, check(y, z["y"], "bf16"))
+    d = rel_l2(out["1"][0], out["0"][0])
+    print(f"bf16 relL2 vs reference: fold {out['1'][1]:.3e}, unfolded {out['0'][1]:.3e}; fold vs unfolded {d:.3e}")
+    assert d <= 1e-2, f"fold vs unfolded relL2 {d:.3e}"
