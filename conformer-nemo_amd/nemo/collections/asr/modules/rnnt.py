@@ -17,9 +17,16 @@ same `pred` / `enc` / `joint_net` parameter names (state_dicts load unchanged), 
 forward(encoder_outputs=(B, H1, T), decoder_outputs=(B, H2, U)) -> (B, T, U, V + 1).
 
 log_softmax semantics follow rnnt.py:998-1006: None -> logits on a GPU (the native path only runs
-on a GPU), True -> log-probs, False -> logits.  Differences by design: inference only (the joint's
-backward and the fused joint+RNNT-loss+WER path need the RNNT loss, SURVEY §8f2, which is not
-built: `fuse_loss_wer=True`, or a forward that requires grad, raises NotImplementedError).
+on a GPU), True -> log-probs, False -> logits.
+
+`fuse_loss_wer=True` (conformer_transducer_bpe.yaml:164) runs the reference's fused step
+(rnnt.py:824-949): per `fused_batch_size` sub-batch, the native joint on the sub-batch's own
+(T', U') extent, the loss module set by `set_loss` (the native RNN-T loss, losses/rnnt.py) with its
+reduction forced to None, optional WER through `set_wer`; returns (mean loss, wer, wer_num,
+wer_denom).  Difference by design: the joint has no backward (the joint / prediction-net gradients
+are not built; the path is the cfg-4 forward, SURVEY §8 a-ext4), so a joint whose inputs require
+grad (or a training-mode joint with trainable parameters under autograd) raises
+NotImplementedError: the fused loss is the validation / no-grad loss.
 """
 from __future__ import annotations
 
@@ -241,6 +248,43 @@ class RNNTJoint(NeuralModule):
         self.compute = os.environ.get("CFM_COMPUTE", "bf16")
         self._native = {}
         self._native_versions = {}
+        self._loss = None
+        self._wer = None
+
+    # --- fused-step plumbing (rnnt_abstract.py: AbstractRNNTJoint) ----------------------------
+    @property
+    def loss(self):
+        return self._loss
+
+    def set_loss(self, loss):
+        if not self._fuse_loss_wer:
+            raise ValueError("Attempting to set loss module even though `fuse_loss_wer` is not set!")
+        self._loss = loss
+
+    @property
+    def wer(self):
+        return self._wer
+
+    def set_wer(self, wer):
+        if not self._fuse_loss_wer:
+            raise ValueError("Attempting to set WER module even though `fuse_loss_wer` is not set!")
+        self._wer = wer
+
+    @property
+    def fuse_loss_wer(self):
+        return self._fuse_loss_wer
+
+    def set_fuse_loss_wer(self, fuse_loss_wer, loss=None, metric=None):
+        self._fuse_loss_wer = fuse_loss_wer
+        self._loss = loss
+        self._wer = metric
+
+    @property
+    def fused_batch_size(self):
+        return self._fused_batch_size
+
+    def set_fused_batch_size(self, fused_batch_size):
+        self._fused_batch_size = fused_batch_size
 
     @property
     def num_classes_with_blank(self):
@@ -279,9 +323,10 @@ class RNNTJoint(NeuralModule):
         if not enc_bdt.is_cuda:
             raise RuntimeError("RNNTJoint (MI355X-native) expects its inputs on a ROCm GPU")
         if torch.is_grad_enabled() and (enc_bdt.requires_grad or dec_bdu.requires_grad or
-                                        any(p.requires_grad for p in self.parameters())) and self.training:
-            raise NotImplementedError("the native RNN-T joint is inference-only (its backward needs the RNNT loss, "
-                                      "which is not built); use torch.no_grad() or .eval()")
+                                        (self.training and any(p.requires_grad for p in self.parameters()))):
+            raise NotImplementedError("the native RNN-T joint has no backward (joint and prediction-net gradients "
+                                      "are not built); run it under torch.no_grad() or in .eval() with inputs "
+                                      "that do not require grad")
         nat = self._native_for(enc_bdt.device)
         return nat.forward(enc_bdt, dec_bdu, log_softmax=bool(self.log_softmax))
 
@@ -289,12 +334,67 @@ class RNNTJoint(NeuralModule):
     def forward(self, encoder_outputs: torch.Tensor, decoder_outputs: Optional[torch.Tensor],
                 encoder_lengths: Optional[torch.Tensor] = None, transcripts: Optional[torch.Tensor] = None,
                 transcript_lengths: Optional[torch.Tensor] = None, compute_wer: bool = False):
-        if self._fuse_loss_wer:
-            raise NotImplementedError("fuse_loss_wer needs the RNNT loss (SURVEY §8f2), which is not built")
-        if decoder_outputs is None:
-            raise ValueError("decoder_outputs passed is None, and `fuse_loss_wer` is not set. "
-                             "decoder_outputs can only be None for fused step!")
-        return self._run(encoder_outputs, decoder_outputs)
+        if not self._fuse_loss_wer:
+            if decoder_outputs is None:
+                raise ValueError("decoder_outputs passed is None, and `fuse_loss_wer` is not set. "
+                                 "decoder_outputs can only be None for fused step!")
+            return self._run(encoder_outputs, decoder_outputs)
+        return self._fused_step(encoder_outputs, decoder_outputs, encoder_lengths, transcripts, transcript_lengths,
+                                compute_wer)
+
+    def _fused_step(self, enc_bdt, dec_bdu, encoder_lengths, transcripts, transcript_lengths, compute_wer):
+        """rnnt.py:812-949: sub-batches of fused_batch_size, each narrowed to its own max T' / U'."""
+        if self._loss is None or self._wer is None:
+            raise ValueError("`fuse_loss_wer` flag is set, but `loss` and `wer` modules were not provided! ")
+        if self._fused_batch_size is None:
+            raise ValueError("If `fuse_loss_wer` is set, then `fused_batch_size` cannot be None!")
+        if encoder_lengths is None or transcript_lengths is None:
+            raise ValueError("`fuse_loss_wer` is set, therefore encoder and target lengths must be provided as well!")
+        losses, wer_num_l, wer_den_l = [], [], []
+        wer = None
+        B = int(enc_bdt.size(0))
+        for b0 in range(0, B, self._fused_batch_size):
+            n = min(b0 + self._fused_batch_size, B) - b0
+            sub_enc = enc_bdt.narrow(0, b0, n)                     # (b, D, T)
+            sub_tr = transcripts.narrow(0, b0, n)
+            sub_el = encoder_lengths[b0:b0 + n]
+            sub_tl = transcript_lengths[b0:b0 + n]
+            t_max, u_max = int(sub_el.max()), int(sub_tl.max())
+            if dec_bdu is not None:
+                if sub_enc.shape[2] != t_max:
+                    sub_enc = sub_enc.narrow(2, 0, t_max)
+                sub_dec = dec_bdu.narrow(0, b0, n)
+                if sub_dec.shape[2] != u_max + 1:
+                    sub_dec = sub_dec.narrow(2, 0, u_max + 1)
+                sub_joint = self._run(sub_enc, sub_dec)             # (b, T', U'+1, V+1)
+                if sub_tr.shape[1] != u_max:
+                    sub_tr = sub_tr.narrow(1, 0, u_max)
+                red = self._loss.reduction
+                self._loss.reduction = None
+                try:
+                    losses.append(self._loss(log_probs=sub_joint, targets=sub_tr.contiguous(), input_lengths=sub_el,
+                                             target_lengths=sub_tl))
+                finally:
+                    self._loss.reduction = red
+                del sub_joint
+            else:
+                losses = None
+            if compute_wer:
+                orig = getattr(self._wer, "log_prediction", False)
+                self._wer.log_prediction = bool(orig and b0 == 0)
+                self._wer.update(sub_enc.detach(), sub_el, sub_tr.detach(), sub_tl)
+                wer, wn, wd = self._wer.compute()
+                self._wer.reset()
+                wer_num_l.append(wn)
+                wer_den_l.append(wd)
+                self._wer.log_prediction = orig
+        loss = torch.cat(losses, 0).mean() if losses is not None else None
+        if compute_wer:
+            wer_num = torch.tensor([float(x) for x in wer_num_l]).sum().long()
+            wer_denom = torch.tensor([float(x) for x in wer_den_l]).sum().long()
+        else:
+            wer_num = wer_denom = None
+        return loss, wer, wer_num, wer_denom
 
     def input_example(self, max_batch=1, max_dim=8192):
         dev = next(self.parameters()).device
