@@ -331,8 +331,9 @@ TRAIN_METRIC = "training-step audio-frames/sec, Conformer-CTC-Large B=32/GPU T=1
 
 def run_train(args, world, rank, dev, dist, barrier):
     """BASELINE config 3: one step = encoder train-mode forward (dropout 0.1, batch-statistics BatchNorm,
-    SyncBatchNorm across ranks) + ConvASRDecoder + CTCLoss(mean_batch) + backward + ONE flat RCCL
-    gradient all-reduce + AdamW (conformer_ctc_bpe.yaml optim: betas 0.9/0.98, wd 1e-3).
+    SyncBatchNorm across ranks) + ConvASRDecoder + CTCLoss(mean_batch) + backward with the per-layer
+    gradient buckets all-reduced over RCCL while the backward runs (conformer_amd.dist.GradBuckets)
+    + AdamW (conformer_ctc_bpe.yaml optim: betas 0.9/0.98, wd 1e-3).
     Synthetic targets U=60 uniform in [0, V)."""
     from conformer_amd import dist as cdist
     from nemo.collections.asr.losses import CTCLoss
@@ -358,16 +359,15 @@ def run_train(args, world, rank, dev, dist, barrier):
     lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
     targets = torch.randint(0, V, (B, U), device=dev, generator=g)
     tlen = torch.full((B,), U, dtype=torch.int64, device=dev)
-    bucket = [None]
+    if dist:   # grads = views of one flat buffer, each layer all-reduced as soon as its backward is enqueued
+        cdist.enable_gradient_buckets(torch.nn.ModuleList([enc, dec]))
 
     def step():
         opt.zero_grad(set_to_none=True)
         y, yl = enc(audio_signal=x, length=lengths)
         lp = dec(encoder_output=y)
         loss = loss_fn(log_probs=lp, targets=targets, input_lengths=yl, target_lengths=tlen)
-        loss.backward()
-        if dist:
-            bucket[0] = cdist.allreduce_gradients(params, bucket=bucket[0])
+        loss.backward()          # with dist: the bucket all-reduces finish inside the backward
         opt.step()
         return loss
 
@@ -397,7 +397,8 @@ def run_train(args, world, rank, dev, dist, barrier):
                                    f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss "
                                    f"U={U}, AdamW), B={B}/GPU, T={T}",
                        "global_batch": B * world, "seq_len": T,
-                       "parallelism": f"dp{world}" + (" (1 flat RCCL gradient all-reduce per step)" if dist else "")},
+                       "parallelism": f"dp{world}" + (f" (per-layer RCCL gradient buckets overlapped with the "
+                                                      f"backward, {L + 2} all-reduces per step)" if dist else "")},
             "model_flops": {"GFLOP_per_step_per_gpu_(3x_fwd)": round(3 * fwd / 1e9, 1),
                             "TFLOP/s_per_gpu": round(3 * fwd / (ms_step * 1e-3) / 1e12, 1),
                             "frac_of_peak": round(3 * fwd / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},

@@ -1,11 +1,20 @@
 """Data-parallel plumbing of the training step: one process per GPU, torch.distributed
 with the "nccl" backend (RCCL over xGMI on ROCm; "gloo" in the CPU tests).
 
-* `allreduce_gradients` — the step's single gradient exchange: every parameter gradient is packed
-  into ONE flat fp32 bucket, summed with one all-reduce and scaled by 1/world (DDP's averaging,
-  which with CTC `mean_batch` and equal per-rank batches gives the global-batch gradient).
-  One large collective instead of DDP's 25 MB buckets: on xGMI the ring is per-link bandwidth
-  bound, and 461 MB in one call amortises the launch/latency terms best.
+* `GradBuckets` / `enable_gradient_buckets` — the step's gradient exchange (DDP's averaging, which
+  with CTC `mean_batch` and equal per-rank batches gives the global-batch gradient), overlapped
+  with the backward: every trainable parameter's `.grad` is a VIEW of one flat fp32 buffer (no
+  copy-in / copy-out), laid out in the native parameter-table order so that each Conformer layer's
+  gradients are one contiguous bucket (~6.8 MB for Large); the native backward reports each layer
+  as soon as its last gradient kernel is enqueued (`grad_ready`, cfm_train.h) and the bucket's
+  RCCL all-reduce is issued right then, ordered after the library's stream, so it runs while the
+  earlier layers' backward computes.  Buckets are per layer (17 of them, not DDP's 25 MB cap):
+  xGMI rings are per-link bound (7 x ~153 GB/s), a 6.8 MB bucket already runs at bandwidth, and
+  per-layer granularity lets the exchange start one layer's backward after the loss.  At the end
+  of the backward (autograd's queue_callback) the non-encoder gradients (CTC head) go as one last
+  bucket, every bucket is waited for (stream-level, no host sync) and the buffer scaled by 1/world.
+* `allreduce_gradients` — the same exchange without overlap: one flat all-reduce after the
+  backward (the bitwise reference of the bucketed path in the tests).
 * `convert_sync_batchnorm` — the counterpart of torch.nn.SyncBatchNorm.convert_sync_batchnorm,
   which Lightning applies for `sync_batchnorm: true` (conformer_ctc_bpe.yaml:175): the native
   encoder then sums its BatchNorm statistics over the group (see cfm_train.h).
@@ -13,7 +22,7 @@ with the "nccl" backend (RCCL over xGMI on ROCm; "gloo" in the CPU tests).
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional
+from typing import Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -80,3 +89,125 @@ def shard_batch(x: torch.Tensor, rank: int, world: int) -> torch.Tensor:
         raise ValueError(f"global batch {B} does not split evenly over {world} ranks")
     per = B // world
     return x[rank * per:(rank + 1) * per]
+
+
+class GradBuckets:
+    """Per-layer gradient buckets over one flat buffer (see the module docstring).
+
+    table_params: the native parameter-table rows in order (None / buffers / frozen parameters are
+      skipped); a `grad_ready(first, n)` range of rows is one contiguous slice of the buffer.
+    other_params: every other trainable parameter (reduced as the last bucket)."""
+
+    def __init__(self, table_params: Sequence[Optional[torch.Tensor]], other_params: Iterable[torch.nn.Parameter] = (),
+                 group=None, average: bool = True):
+        seen = set()
+        self.rows: List[Optional[Tuple[int, int]]] = []      # table row -> (offset, numel) or None
+        self.members: List[torch.nn.Parameter] = []
+        self.offsets: List[int] = []
+        off = 0
+        for p in table_params:
+            if isinstance(p, torch.nn.Parameter) and p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self.rows.append((off, p.numel()))
+                self.members.append(p)
+                self.offsets.append(off)
+                off += p.numel()
+            else:
+                self.rows.append(None)
+        self.table_end = off
+        for p in other_params:
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self.members.append(p)
+                self.offsets.append(off)
+                off += p.numel()
+        self.numel = off
+        dev = self.members[0].device if self.members else torch.device("cpu")
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.views = [self.flat[o:o + p.numel()].view_as(p) for o, p in zip(self.offsets, self.members)]
+        self.group = group
+        self.average = average
+        self.world = _world(group)
+        self._works = []
+        self._reduced = []           # (start, end) slices already issued this step
+        self.attach()
+
+    # ---- per step -------------------------------------------------------------------------------
+    def attach(self) -> None:
+        """Point every member's .grad at its view and zero the buffer (call before the backward;
+        the encoder's train forward does)."""
+        self.flat.zero_()
+        for p, v in zip(self.members, self.views):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+        self._works, self._reduced = [], []
+
+    def native_outputs(self, params: Sequence[torch.Tensor], want: Sequence[bool]) -> List[Optional[torch.Tensor]]:
+        """Output pointers for cfm_train_backward: table row i writes straight into its view."""
+        out = []
+        for i, (p, w) in enumerate(zip(params, want)):
+            if not w:
+                out.append(None)
+                continue
+            r = self.rows[i] if i < len(self.rows) else None
+            if r is None:
+                raise RuntimeError(f"table row {i} wants a gradient but is not in the gradient buckets")
+            out.append(self.flat[r[0]:r[0] + r[1]])
+        return out
+
+    def _issue(self, start: int, end: int, stream=None) -> None:
+        if end <= start:
+            return
+        self._reduced.append((start, end))
+        if self.world <= 1:
+            return
+        import torch.distributed as dist
+        from .train import on_library_stream
+        with on_library_stream(stream, self.flat.device):
+            self._works.append(dist.all_reduce(self.flat[start:end], group=self.group, async_op=True))
+
+    def on_ready(self, first: int, n: int, stream=None) -> None:
+        """grad_ready(first, n): all-reduce the slice of table rows [first, first + n)."""
+        spans = [self.rows[i] for i in range(first, min(first + n, len(self.rows))) if self.rows[i] is not None]
+        if spans:
+            self._issue(min(o for o, _ in spans), max(o + k for o, k in spans), stream)
+
+    def finish(self) -> None:
+        """End of the backward: reduce whatever no grad_ready covered, wait, average."""
+        covered = sorted(self._reduced)
+        pos, gaps = 0, []
+        for a, b in covered:
+            if a > pos:
+                gaps.append((pos, a))
+            pos = max(pos, b)
+        if pos < self.numel:
+            gaps.append((pos, self.numel))
+        for a, b in gaps:
+            self._issue(a, b)
+        for w in self._works:
+            w.wait()
+        if self.average and self.world > 1:
+            self.flat.mul_(1.0 / self.world)
+        self._works = []
+
+    @property
+    def issued(self) -> List[Tuple[int, int]]:
+        return list(self._reduced)
+
+
+def enable_gradient_buckets(model: torch.nn.Module, group=None, average: bool = True) -> GradBuckets:
+    """Bucketed, overlapped gradient all-reduce for a model holding one native ConformerEncoder:
+    the encoder's parameters in native table order, then every other trainable parameter."""
+    from nemo.collections.asr.modules import ConformerEncoder
+    encs = [m for m in model.modules() if isinstance(m, ConformerEncoder)]
+    if len(encs) != 1:
+        raise ValueError("enable_gradient_buckets expects exactly one ConformerEncoder in the model")
+    enc = encs[0]
+    names = enc.native_param_names()
+    sd = enc.state_dict(keep_vars=True)
+    table = [sd.get(n) for n in names]
+    ids = {id(t) for t in table if t is not None}
+    others = [p for p in model.parameters() if id(p) not in ids]
+    gb = GradBuckets(table, others, group=group, average=average)
+    enc.set_grad_buckets(gb)
+    return gb

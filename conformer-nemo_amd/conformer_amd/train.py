@@ -8,8 +8,11 @@ behaves like the reference module under autograd (EncDecCTCModel.training_step -
 ctc_models.py:485-514): gradients land in each nn.Parameter's `.grad`.
 
 Multi-GPU: SyncBatchNorm statistics are summed across ranks by a host callback that runs a
-torch.distributed (RCCL) all-reduce on a view of the library's workspace; the gradient exchange
-itself is `conformer_amd.dist.allreduce_gradients` (one flat all-reduce per step).
+torch.distributed (RCCL) all-reduce on a view of the library's workspace, ordered after the
+library's stream.  The gradient exchange is `conformer_amd.dist.GradBuckets` (gradients as views
+of one flat buffer, each layer's bucket all-reduced asynchronously as soon as the native backward
+has enqueued it: `grad_ready` in cfm_train.h) or, without buckets, the one flat all-reduce of
+`conformer_amd.dist.allreduce_gradients` after the backward.
 """
 from __future__ import annotations
 
@@ -21,12 +24,14 @@ import torch
 from . import _lib
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+GRAD_READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 
 class CfmTrainOpts(ctypes.Structure):
     _fields_ = [("dropout", ctypes.c_float), ("dropout_emb", ctypes.c_float), ("dropout_att", ctypes.c_float),
                 ("bn_momentum", ctypes.c_float), ("update_running_stats", ctypes.c_int), ("world", ctypes.c_int),
-                ("seed", ctypes.c_uint64), ("allreduce", ALLREDUCE_FN), ("allreduce_user", ctypes.c_void_p)]
+                ("seed", ctypes.c_uint64), ("allreduce", ALLREDUCE_FN), ("allreduce_user", ctypes.c_void_p),
+                ("grad_ready", GRAD_READY_FN), ("grad_ready_user", ctypes.c_void_p)]
 
 
 def _bind(lib) -> None:
@@ -57,9 +62,11 @@ class EncoderTrainer:
         self.device = torch.device("cuda", native.device)
         self.names: List[str] = list(native.param_names().keys())
         self._ws: Optional[torch.Tensor] = None
-        self._cb = None          # keep the ctypes callback alive
+        self._cb = None          # keep the ctypes callbacks alive
+        self._ready_cb = None
         self._group = None
         self.world = 1
+        self.grad_buckets = None   # conformer_amd.dist.GradBuckets (data parallelism), or None
 
     # ---- SyncBatchNorm plumbing ---------------------------------------------------------------
     def set_sync_group(self, group=None, world: Optional[int] = None) -> None:
@@ -80,7 +87,8 @@ class EncoderTrainer:
                 if off < 0 or off % 4 or off + 4 * n > ws.numel():
                     return 1
                 view = ws[off:off + 4 * n].view(torch.float32)
-                dist.all_reduce(view, group=self._group)
+                with on_library_stream(stream, ws.device):   # ordered after the library's kernels
+                    dist.all_reduce(view, group=self._group)
                 return 0
             except Exception:   # noqa: BLE001  (no exception may cross the C boundary)
                 return 1
@@ -102,6 +110,17 @@ class EncoderTrainer:
             o.allreduce = self._cb
         o.allreduce_user = None
         return o
+
+    def _make_ready_callback(self):
+        gb = self.grad_buckets
+
+        def cb(user, first, n, stream):
+            try:
+                gb.on_ready(first, n, stream)
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+        return GRAD_READY_FN(cb)
 
     def _workspace(self, B: int, T: int) -> torch.Tensor:
         n = int(self.lib.cfm_train_workspace_size(self.native.handle, B, T))
@@ -153,17 +172,49 @@ class EncoderTrainer:
     def backward(self, dy_bdt: torch.Tensor, state: Dict, params: Sequence[torch.Tensor],
                  want: Sequence[bool]) -> List[Optional[torch.Tensor]]:
         dy = dy_bdt.detach().to(self.device, torch.float32).contiguous()
-        grads = [torch.empty_like(p) if w else None for p, w in zip(params, want)]
+        gb = self.grad_buckets
+        if gb is not None:
+            # gradients written straight into the bucket views (p.grad); autograd gets None for them
+            out = gb.native_outputs(params, want)
+            grads = [None] * len(params)
+        else:
+            out = grads = [torch.empty_like(p) if w else None for p, w in zip(params, want)]
         ws = self._workspace(state["B"], state["T"])
         o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"], state["dropout_emb"],
                        state["dropout_att"])
+        if gb is not None:
+            self._ready_cb = self._make_ready_callback()
+            o.grad_ready = self._ready_cb
+            # the remaining (non-encoder) gradients are final only when the whole backward is done
+            torch.autograd.Variable._execution_engine.queue_callback(gb.finish)
         tape = state["tape"]
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
-                                               state["B"], state["T"], ctypes.byref(o), self._ptrs(grads),
+                                               state["B"], state["T"], ctypes.byref(o), self._ptrs(out),
                                                tape.data_ptr(), tape.numel(), ws.data_ptr(), ws.numel(), st),
                    "cfm_train_backward")
         return grads
+
+
+class on_library_stream:
+    """Context: make `stream` (a hipStream_t the library passed to a callback) torch's current stream,
+    so a torch.distributed collective issued inside is ordered after the library's enqueued work."""
+
+    def __init__(self, stream, device):
+        self.stream, self.device = stream, device
+        self._ctx = None
+
+    def __enter__(self):
+        if self.stream and getattr(self.device, "type", "cpu") == "cuda":
+            s = torch.cuda.ExternalStream(int(self.stream), device=self.device)
+            self._ctx = torch.cuda.stream(s)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self._ctx is not None:
+            self._ctx.__exit__(*exc)
+        return False
 
 
 class _EncoderTrainFn(torch.autograd.Function):

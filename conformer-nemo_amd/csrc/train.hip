@@ -1523,6 +1523,15 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
 // =============================================================================================
 // backward
 // =============================================================================================
+// parameter-table rows (build_param_list): pre_encode.* first, then one equal block per layer
+constexpr int kPreEncodeRows = 6;
+
+void grad_ready(const Step& S, int first, int n) {
+  const cfm_train_opts* o = S.o;
+  if (!o->grad_ready || n <= 0) return;
+  if (o->grad_ready(o->grad_ready_user, first, n, (void*)S.st) != 0) fail(CFM_ERR_HIP, "grad_ready callback failed");
+}
+
 void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   const Geo& g = S.g;
   cfm_encoder* h = S.h;
@@ -1534,6 +1543,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   float* gB = S.W_<float>(S.wl.gB);
   float* dbr = S.W_<float>(S.wl.dbr);
   float* red = S.W_<float>(S.wl.red);
+  const int layer_rows = g.L > 0 ? ((int)h->params.size() - kPreEncodeRows - (h->has_out_proj ? 2 : 0)) / g.L : 0;
   void* pa = S.W_(S.wl.pa);
   void* pat = S.W_(S.wl.pat);
   void* pbt = S.W_(S.wl.pbt);
@@ -1729,6 +1739,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     }
     ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, gB);   // gB = d x0
     std::swap(gA, gB);
+    grad_ready(S, kPreEncodeRows + l * layer_rows, layer_rows);   // every gradient of layer l is enqueued
   }
 
   // ---- subsampling backward: gA = d(layer-0 input) ----
@@ -1805,6 +1816,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       if (Gp(S.i_c1b)) colred(part_b, nullptr, nullptr, g.C, nch, g.C, 0, 1.0f, Gp(S.i_c1b), 0, red, st);
     }
   }
+  grad_ready(S, 0, kPreEncodeRows);
 }
 
 }  // namespace

@@ -97,6 +97,14 @@ cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int
  */
 typedef int (*cfm_allreduce_fn)(void* user, float* buf, int64_t n, void* stream);
 
+/* Gradient readiness (data parallelism, SURVEY §8e: the gradient all-reduce overlapped with the
+ * backward): when set, cfm_train_backward calls `grad_ready(user, first, n, stream)` on the host
+ * right after it has ENQUEUED the last kernel writing the gradients of parameter-table rows
+ * [first, first + n) - once per Conformer layer, last layer first, then once for the pre_encode
+ * rows.  A collective issued from the callback and ordered after `stream` (e.g. an RCCL all-reduce
+ * on a view of those gradients) then overlaps the rest of the backward.  Return 0 on success. */
+typedef int (*cfm_grad_ready_fn)(void* user, int first_param, int n_params, void* stream);
+
 typedef struct cfm_train_opts {
   float dropout;               /* ConformerEncoder(dropout=): embedding, FFN inner and residual-branch dropout */
   float dropout_emb;           /* dropout_emb on the positional window (multi_head_attention.py:316)        */
@@ -107,6 +115,8 @@ typedef struct cfm_train_opts {
   uint64_t seed;               /* dropout mask seed; use a fresh one per step                                */
   cfm_allreduce_fn allreduce;  /* required when world > 1                                                    */
   void* allreduce_user;
+  cfm_grad_ready_fn grad_ready;  /* optional (NULL): per-layer gradient readiness, backward only              */
+  void* grad_ready_user;
 } cfm_train_opts;
 
 size_t cfm_train_tape_size(const cfm_encoder* h, int B, int T);

@@ -100,3 +100,57 @@ def test_gradient_allreduce_and_syncbn_callback_gloo_ws2():
         assert rc == 0 and rc_bad != 0
         assert view == [3.0, 6.0, 9.0, 12.0]                   # summed, not averaged
         assert shard == list(range(4 * rank, 4 * rank + 4))
+
+
+def _bucket_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
+    from conformer_amd import dist as cdist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(11 + rank)
+        P = [torch.nn.Parameter(torch.zeros(s)) for s in ((4, 3), (7,), (2, 2), (5,))]
+        P[2].requires_grad_(False)                               # frozen: not bucketed
+        head = torch.nn.Parameter(torch.zeros(6))
+        table = [P[0], torch.zeros(3), None, P[1], P[2], P[3]]   # a buffer row, an empty row
+        gb = cdist.GradBuckets(table, [head], average=True)
+        want = [True, False, False, True, False, True]
+        vals = {i: torch.randn(table[i].shape, generator=g) for i in (0, 3, 5)}
+        outs = gb.native_outputs(table, want)                    # what cfm_train_backward writes into
+        for i, v in vals.items():
+            outs[i].copy_(v.reshape(-1))
+        hv = torch.randn(6, generator=g)
+        head.grad += hv                                         # autograd accumulation into the view
+        gb.on_ready(3, 3)                                       # last "layer" first, as the backward does
+        gb.on_ready(0, 3)
+        gb.finish()
+        bucketed = {i: table[i].grad.clone() for i in (0, 3, 5)}
+        bucketed["head"] = head.grad.clone()
+        views_ok = all(table[i].grad.data_ptr() >= gb.flat.data_ptr() for i in (0, 3, 5))
+        # reference: plain .grad tensors, one flat post-backward all-reduce
+        Q = [torch.nn.Parameter(torch.zeros(t.shape)) for t in (P[0], P[1], P[3], head)]
+        for qp, v in zip(Q, (vals[0], vals[3], vals[5], hv)):
+            qp.grad = v.clone()
+        cdist.allreduce_gradients(Q)
+        same = all(torch.equal(bucketed[k], qp.grad) for k, qp in zip((0, 3, 5, "head"), Q))
+        q.put((rank, same, views_ok, gb.issued, P[2].grad is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_overlapped_allreduce_equals_flat_gloo_ws2():
+    """conformer_amd.dist.GradBuckets: grads are views of one flat buffer, buckets are all-reduced
+    as grad_ready reports them (last layer first) and the rest at finish(); the averaged gradients
+    are bitwise those of the flat post-backward all-reduce."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    for rank, same, views_ok, issued, frozen_none in sorted(q.get(timeout=5) for _ in range(world)):
+        assert same and views_ok and frozen_none
+        # P1 | P3 (rows 3..5) = flat[12:24], P0 (rows 0..2) = flat[0:12], then the head at finish
+        assert issued == [(12, 24), (0, 12), (24, 30)]

@@ -29,7 +29,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, case="train_tiny_ctx", rows=None):
+def _worker(rank, world, port, q, case="train_tiny_ctx", rows=None, buckets=False):
     for p in (os.path.join(ROOT, "conformer-nemo_amd"), os.path.join(ROOT, "tests", "golden")):
         sys.path.insert(0, p)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -54,10 +54,30 @@ def _worker(rank, world, port, q, case="train_tiny_ctx", rows=None):
             sh = lambda a: torch.from_numpy(a[rows[rank]])  # noqa: E731
             scale = 1.0
         x, ln, dy = sh(z["x"]).cuda(), sh(z["lengths"]).cuda(), sh(z["dy"]).cuda()
+        bitwise = None
+        if buckets:
+            # per-layer buckets all-reduced during the backward (grad_ready), grads = buffer views;
+            # then the same step through the flat post-backward all-reduce: bitwise identical
+            gb = cdist.enable_gradient_buckets(enc, average=rows is None)
+            buf0 = {n: b.clone() for n, b in enc.named_buffers()}
+            y, _ = enc(audio_signal=x, length=ln)
+            (y * dy).sum().backward()
+            torch.cuda.synchronize()
+            got_b = {n: p.grad.clone() for n, p in enc.named_parameters()}
+            assert all(p.grad.data_ptr() >= gb.flat.data_ptr() for p in enc.parameters())
+            assert len(gb.issued) == enc._native_cfg["n_layers"] + 1 + (1 if gb.table_end < gb.numel else 0)
+            enc.set_grad_buckets(None)
+            for p_ in enc.parameters():
+                p_.grad = None
+            with torch.no_grad():      # the second step starts from the same running statistics
+                for n, b in enc.named_buffers():
+                    b.copy_(buf0[n])
         y, _ = enc(audio_signal=x, length=ln)
         (y * dy).sum().backward()
         cdist.allreduce_gradients(enc.parameters(), average=rows is None)
         torch.cuda.synchronize()
+        if buckets:
+            bitwise = all(torch.equal(got_b[n], p.grad) for n, p in enc.named_parameters())
         worst = 0.0
         floor = 1e-2 * max(float(np.linalg.norm(z[k])) for k in z.files if k.startswith("grad__"))
         params = dict(enc.named_parameters())
@@ -70,26 +90,79 @@ def _worker(rank, world, port, q, case="train_tiny_ctx", rows=None):
         wb = max(float(np.linalg.norm(bufs[k[5:]].cpu().numpy() - z[k]) / np.linalg.norm(z[k]))
                  for k in z.files if k.startswith("buf__"))
         yl = float(np.linalg.norm(y.detach().cpu().numpy() - sh(z["y"]).numpy()) / np.linalg.norm(sh(z["y"]).numpy()))
-        q.put((rank, worst, wb, yl))
+        q.put((rank, worst, wb, yl, bitwise))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,rows", [("train_tiny_ctx", None), ("train_tiny", [[0, 1], [2]])],
-                         ids=["equal_shards", "unequal_shards"])
-def test_dp2_syncbn_gradients_match_global_batch(case, rows):
+@pytest.mark.parametrize("case,rows,buckets", [("train_tiny_ctx", None, False), ("train_tiny", [[0, 1], [2]], False),
+                                               ("train_tiny_ctx", None, True)],
+                         ids=["equal_shards", "unequal_shards", "bucketed_overlapped"])
+def test_dp2_syncbn_gradients_match_global_batch(case, rows, buckets):
     """unequal_shards: rank 0 holds 2 utterances, rank 1 one, so the ranks' BatchNorm
     frame counts differ; SyncBatchNorm must weight by the global count (as torch.nn.SyncBatchNorm
     does), giving the global batch's statistics, outputs and (summed) gradients."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case, rows)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case, rows, buckets)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(150)
         assert p.exitcode == 0
-    for rank, worst, wb, yl in sorted(q.get(timeout=5) for _ in range(world)):
-        print(f"rank {rank}: worst grad {worst:.2e}, running stats {wb:.2e}, |dy| {yl:.2e}")
-        assert worst <= 1e-3 and wb <= 1e-4 and yl <= 1e-4
+    for rank, worst, wb, yl, bitwise in sorted(q.get(timeout=5) for _ in range(world)):
+        print(f"rank {rank}: worst grad {worst:.2e}, running stats {wb:.2e}, |dy| {yl:.2e}, buckets==flat {bitwise}")
+        assert worst <= 1e-3 and yl <= 1e-4
+        assert wb <= 1e-4
+        assert bitwise in (None, True)
+
+
+def test_grad_ready_order_and_bucket_views():
+    """Single process: the native backward reports every layer, last first, then pre_encode, each a
+    contiguous table range; gradients written into the bucket views equal the plain .grad path."""
+    for p in (os.path.join(ROOT, "conformer-nemo_amd"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from conformer_amd import dist as cdist
+    from nemo.collections.asr.modules import ConformerEncoder
+    from recipe import make_state_dict
+    z = np.load(os.path.join(GOLDEN, "train_tiny_ctx.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(**cfg, dropout=0.0, dropout_emb=0.0, dropout_att=0.0)
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
+    enc.set_compute_mode("fp32")
+    enc = enc.cuda().train()
+    x, ln, dy = (torch.from_numpy(z[k]).cuda() for k in ("x", "lengths", "dy"))
+    y, _ = enc(audio_signal=x, length=ln)
+    (y * dy).sum().backward()
+    plain = {n: p.grad.clone() for n, p in enc.named_parameters()}
+    for p in enc.parameters():
+        p.grad = None
+
+    calls = []
+
+    class Recording(cdist.GradBuckets):
+        def on_ready(self, first, n, stream=None):
+            calls.append((first, n, stream))
+            super().on_ready(first, n, stream)
+
+    names = enc.native_param_names()
+    sdv = enc.state_dict(keep_vars=True)
+    gb = Recording([sdv.get(k) for k in names], [], average=True)
+    enc.set_grad_buckets(gb)
+    y, _ = enc(audio_signal=x, length=ln)
+    (y * dy).sum().backward()
+    torch.cuda.synchronize()
+    L = cfg["n_layers"]
+    per = (len(names) - 6) // L
+    assert [(f, n) for f, n, _ in calls] == [(6 + l * per, per) for l in reversed(range(L))] + [(0, 6)]
+    cur = torch.cuda.current_stream().cuda_stream
+    assert all(int(s or 0) == cur for _, _, s in calls)        # the library runs on torch's stream (0 = default)
+    assert all(names[f + i].startswith(f"layers.{L - 1 - j}.") for j, (f, n, _) in enumerate(calls[:-1])
+               for i in range(n))
+    for n_, p in enc.named_parameters():
+        assert torch.equal(p.grad, plain[n_]), n_
+        assert gb.flat.data_ptr() <= p.grad.data_ptr() < gb.flat.data_ptr() + 4 * gb.numel
