@@ -1,6 +1,6 @@
 """ctypes binding of libcfm.so (the C-ABI declared in include/cfm_encoder.h, cfm_ctc.h, cfm_train.h,
 cfm_joint.h, cfm_stream.h, cfm_mel.h,
-cfm_rnnt_loss.h, cfm_augment.h and cfm_rnnt_decode.h).
+cfm_rnnt_loss.h, cfm_augment.h, cfm_rnnt_decode.h and cfm_comm.h).
 
 The library is built in-tree by `conformer-nemo_amd/csrc/Makefile` (or `__graft_entry__.build()`).
 There is deliberately no fallback: if the shared object is missing or fails to load, importing
@@ -53,6 +53,10 @@ AUGMENT_SYMBOLS = ("cfm_spec_mask_rects", "cfm_spec_shot")
 RNNT_DECODE_SYMBOLS = ("cfm_rnnt_decoder_create", "cfm_rnnt_decoder_destroy", "cfm_rnnt_decoder_set_weights",
                        "cfm_rnnt_decoder_predict_workspace_size", "cfm_rnnt_decoder_predict",
                        "cfm_rnnt_greedy_workspace_size", "cfm_rnnt_greedy_decode")
+# every symbol include/cfm_comm.h declares (bound in conformer_amd/comm.py)
+COMM_SYMBOLS = ("cfm_comm_get_unique_id", "cfm_comm_init", "cfm_comm_destroy", "cfm_comm_world", "cfm_allreduce_grads",
+                "cfm_comm_allreduce_cb", "cfm_grad_buckets_create", "cfm_grad_buckets_ready_cb",
+                "cfm_grad_buckets_finish", "cfm_grad_buckets_issued", "cfm_grad_buckets_destroy")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",

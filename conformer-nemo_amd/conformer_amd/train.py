@@ -182,7 +182,15 @@ class EncoderTrainer:
         ws = self._workspace(state["B"], state["T"])
         o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"], state["dropout_emb"],
                        state["dropout_att"])
-        if gb is not None:
+        if gb is not None and getattr(gb, "native_ready", None) is not None:
+            # conformer_amd.comm.NativeGradBuckets: the library's own callback issues the RCCL
+            # all-reduces (cfm_grad_buckets_ready_cb), no Python in the backward
+            fn, user = gb.native_ready
+            self._ready_cb = GRAD_READY_FN(fn.value)
+            o.grad_ready = self._ready_cb
+            o.grad_ready_user = user
+            torch.autograd.Variable._execution_engine.queue_callback(gb.finish)
+        elif gb is not None:
             self._ready_cb = self._make_ready_callback()
             o.grad_ready = self._ready_cb
             # the remaining (non-encoder) gradients are final only when the whole backward is done

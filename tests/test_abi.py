@@ -45,7 +45,9 @@ def test_library_loads_and_exports_header_symbols():
     assert set(aug) == set(_lib.AUGMENT_SYMBOLS)
     dec = _declared_symbols("cfm_rnnt_decode.h")
     assert set(dec) == set(_lib.RNNT_DECODE_SYMBOLS)
-    for name in ctc + train + joint + stream + mel + rl + aug + dec:
+    comm = _declared_symbols("cfm_comm.h")
+    assert set(comm) == set(_lib.COMM_SYMBOLS)
+    for name in ctc + train + joint + stream + mel + rl + aug + dec + comm:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
