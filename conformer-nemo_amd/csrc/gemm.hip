@@ -705,6 +705,173 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 8-phase 256x256 GEMM for long-K contractions (bf16; the conv2 implicit GEMM, K = 9*C):
+// cdna_hip_programming.md §5 "The 256² 8-phase template" re-derived for this library's loaders.
+//   * 8 waves = 2 (M) x 4 (N), wave tile 128 x 64 = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles.
+//   * A K-tile is 64 elements (128 B per row) in two K-halves X0 | X1 (64 B per row each); LDS holds
+//     two K-tiles (parity kt & 1), each [A0 | B0 | A1 | B1] of 256 rows x 64 B (16 KB): 128 KB.
+//   * 4 phases per K-tile; phase q multiplies K-half q >> 1 for the wave's row half q & 1 (16 MFMAs).
+//     Each phase is [R: ds_read the phase's fragments, issue one item of global->LDS loads] barrier
+//     [M: lgkmcnt(0), 16 MFMAs] barrier.  The two wave rows run one barrier apart (group 1 starts
+//     with an extra barrier), so on every SIMD one wave multiplies while the other reads and loads.
+//   * Loads (4 glds per thread = one K-half of A and B): R_1 of K-tile kt loads X1 of kt+1, R_3
+//     loads X0 of kt+2 - each into a region whose last reader finished >= 2 barriers earlier.  Every
+//     wave waits vmcnt(8) (two items younger than the one needed) before the barrier that precedes
+//     wave row 0's R_0 / R_2, so the data is complete for both rows' reads.  Past the last K-tile
+//     the items load the zero page (the counts stay uniform).
+//   * LDS rows are 64 B: the 16-byte slot of a row is XOR-swizzled by f((row >> 2) & 3),
+//     f = {0, 2, 3, 1}: every 16-lane group of a fragment ds_read_b128 hits 16 distinct bank slots.
+//   * Epilogue: the same LDS image + epilogue<> as gemm_kernel, two 128-row passes.
+// ---------------------------------------------------------------------------------------------
+struct T8 {
+  static constexpr int BM = 256, BN = 256, NT = 512, EP = 2, EPS = 256, WM = 2;
+};
+constexpr int G8_HALF = 256 * 64;       // one K-half image of one operand
+constexpr int G8_BUF = 4 * G8_HALF;     // one K-tile: A0 | B0 | A1 | B1
+static_assert(2 * G8_BUF >= T8::BM / T8::EP * T8::EPS * 4, "epilogue image fits the ring");
+CFM_DEV int g8_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+
+template <int EPI, class ALoad>
+__global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;   // wave row = stagger group (waves w and w+4 share a SIMD)
+
+  const int nblocks = p.Mtiles * p.Ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
+  const int m0 = mt * 256, n0 = ntl * 256;
+
+  // staging: instruction i (0, 1) of this wave fills rows (i*8 + wave)*16 .. +15 of a K-half image
+  int rows[2], lo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rows[i] = (i * 8 + wave) * 16 + (lane >> 2);
+    lo[i] = ((lane & 3) ^ g8_swz(rows[i])) * 16;
+  }
+  typename ALoad::State ast;
+  aload.prepare(ast, m0, rows);
+  const char* wrow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) wrow[i] = p.W + (long)(n0 + rows[i]) * p.ldw_b + lo[i];
+  const char* zsrc = aload.zero + lane * 16;
+  const uint32_t sbase = lds_addr(smem);
+  const int nk = p.kb / 128;
+
+  const int tapb = (int)aload.tapb;   // bytes of one 3x3 tap (C * 2); a K-half never straddles two
+  auto issue = [&](int kt, int h) {   // K-half h of K-tile kt, A then B: 4 glds
+    const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const bool live = kt < nk;        // past the end: the zero page (uniform vmcnt counts)
+    const int kb0 = kt * 128 + h * 64;
+    int tap = 0;                      // wave-uniform: count the tap boundaries below kb0 (no division)
+#pragma unroll
+    for (int t = 1; t < 9; ++t) tap += kb0 >= t * tapb ? 1 : 0;
+    const int tr = (tap >= 3 ? 1 : 0) + (tap >= 6 ? 1 : 0), tf = tap - 3 * tr;
+    const long toff = ((long)tr * aload.F1 + tf) * tapb + (kb0 - tap * tapb);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool v = live && ((ast.valid[i] >> tap) & 1u);
+      const char* src = v ? ast.base[i] + toff + lo[i] : zsrc;
+      glds16_asm(src, base + (i * 8 + wave) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int fslot = (fc ^ g8_swz(fr)) * 16;   // rows are 16-aligned + fr
+  uint4 af[4], bfr[4];
+  auto read_frags = [&](int kt, int q) {
+    const char* hb = smem + (kt & 1) * G8_BUF + (q >> 1) * 2 * G8_HALF;
+    const int r0 = wm * 128 + (q & 1) * 64 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const uint4*)(hb + (r0 + i * 16) * 64 + fslot);
+    if ((q & 1) == 0) {
+      const int c0 = wn * 64 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *(const uint4*)(hb + G8_HALF + (c0 + j * 16) * 64 + fslot);
+    }
+  };
+
+  // prologue: X0(0), X1(0), X0(1); X0(0) complete for every wave, then wave row 1 falls one barrier behind
+  issue(0, 0);
+  issue(0, 1);
+  issue(1, 0);
+  wait_vmcnt<8>();
+  wait_lgkm0();
+  raw_barrier();
+  if (wm == 1) raw_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // R_q
+      read_frags(kt, q);
+      if (q == 1) issue(kt + 1, 1);
+      if (q == 3) issue(kt + 2, 0);
+      if (wm == 1 && (q & 1)) wait_vmcnt<8>();   // before the barrier preceding row 0's R_{q+1}
+      raw_barrier();
+      // M_q
+      wait_lgkm0();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[(q & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), acc[(q & 1) * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0 && (q & 1)) wait_vmcnt<8>();
+      raw_barrier();
+    }
+  }
+  if (wm == 0) raw_barrier();   // re-align the barrier counts of the two wave rows
+  wait_vmcnt<0>();
+  wait_lgkm0();
+  raw_barrier();
+
+  if (p.probe & 2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0];
+    if (t == 1234.5f) ((float*)p.epi.C)[threadIdx.x] = t;
+    return;
+  }
+  // ---- epilogue: two passes of 128 rows (pass p = wave row p), image [128][256] fp32 ----
+  float* img = (float*)smem;
+  float bcol[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bcol[j] = p.epi.bias ? p.epi.bias[n0 + wn * 64 + j * 16 + fr] : 0.0f;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            img[(i * 16 + fc * 4 + e) * T8::EPS + wn * 64 + j * 16 + fr] = acc[i][j][e] + bcol[j];
+    }
+    __syncthreads();
+    epilogue<bf16_t, EPI, EpiView<T8>, false>(p, img, m0 + pass * 128, n0, 0, nullptr, nullptr);
+  }
+}
+
 template <typename T, class TL, template <int> class AL, class ALArgs>
 void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   using ALoad = AL<TL::GA>;
@@ -744,6 +911,8 @@ int packed_width(const GemmEpi& epi, int N) {
 }
 
 int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
+// the 8-phase kernel for the conv2 implicit GEMM (CFM_GEMM8=0: the tiled kernel, A/B)
+int g_gemm8 = [] { const char* s = getenv("CFM_GEMM8"); return s ? atoi(s) : 1; }();
 // write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 
@@ -920,6 +1089,15 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   ConvArgs a{(const char*)g.X1, g.T1, g.F1, g.T2, g.F2, (long)g.C * es, M, (const char*)zero_page};
+  if (dtype == DT_BF16 && g_gemm8 && g_tile_override < 0 && p.kb % 128 == 0 && ((long)g.C * es) % 64 == 0) {
+    // the 8-phase 256x256 kernel (long K): N granule 256 (packed weights are zero-padded to it)
+    ALoadConv<2> al;
+    a.fill(al);
+    p.Mtiles = (M + 255) / 256;
+    p.Ntiles = (N + 255) / 256;
+    cfm_launch((gemm8_kernel<EPI_RELU, ALoadConv<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    return;
+  }
   int tile = pick_tile(dtype, M, N, epi.mode, true);
   if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
   else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
