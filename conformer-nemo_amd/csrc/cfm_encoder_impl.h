@@ -50,6 +50,9 @@ struct cfm_encoder {
   // following GEMM (the residual GEMM before each writes the compute-type rows and per-row granule
   // statistics); off in the fp32 parity mode (CFM_LN_FOLD=0/1 overrides for A/B).
   bool ln_fold = false;
+  // bf16 eval forward with T' <= 256: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish as
+  // one launch (gemm_glu_dw); CFM_GLU_DW=0 keeps the two launches (A/B)
+  bool fuse_glu_dw = true;
   std::vector<hipStream_t> sub_streams;
   std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
   void* zero_page = nullptr;

@@ -54,6 +54,8 @@ enum Epilogue {
   EPI_SCALE_F32 = 4,   // X[m,n] (fp32)  = (acc + bias) * alpha
   EPI_GLU_MASK = 5,    // C[m, c] = (a + ba) * sigmoid(g + bg), zero for padded frames (GLU-packed W)
   EPI_QKV = 6,         // packed cols [q | k | v]: C = [q+u | q+v | k] (ldc = 3*H*dkp), v -> Vt[(b*H+h)][d][t]
+  EPI_GLU_DW = 7,      // EPI_GLU_MASK + depthwise conv (k 31) + BatchNorm (running stats) + Swish on an
+                       // utterance-aligned 256-row tile (utt_tp <= 256 frames): C = conv module's S rows
 };
 
 // Dropout masks (training): keep element e iff hash(key, e) >= thr, thr = p * 2^32; kept values are
@@ -102,6 +104,12 @@ struct GemmEpi {
   int ln_width;
   const float* ln_c;   // [Npad] sum_k W'[n][k] (of the packed, rounded W')
   const float* ln_d;   // [Npad] sum_k beta[k] W[n][k] + bias[n]
+  // Utterance-aligned rows (EPI_GLU_DW): GEMM row m is frame t = m % 256 of utterance b = m / 256,
+  // A / output row b * utt_tp + t (t < utt_tp; utt_M real rows); 0 = rows are plain.
+  int utt_tp, utt_M;
+  const float* dw_w;   // EPI_GLU_DW: depthwise weight [31][d], bias [d], BatchNorm mean / 1/sqrt(var+eps) / w / b
+  const float* dw_b;
+  const float *bn_mean, *bn_inv, *bn_w, *bn_b;
 };
 constexpr int LN_GRANULE = 128;
 
@@ -125,6 +133,11 @@ int set_gemm_tile_override(int tile);
 int set_gemm_probe(int probe);
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                const void* zero_page, hipStream_t st);
+// pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish in one launch (bf16, epi.mode = EPI_GLU_DW,
+// epi.utt_tp = T' <= 256, N = d, d % 64 == 0): one 256x128 tile per (utterance, 64 channels).
+bool gemm_glu_dw_supported(int dtype, int Tp, int d, int K);
+void gemm_glu_dw(int dtype, const void* A, long lda, int B, int Tp, int K, const void* Wp, int Kpad, int N,
+                 const GemmEpi& epi, const void* zero_page, hipStream_t st);
 
 void calc_length(const int32_t* len_in, int32_t* len_out, int B, int T, int repeat, hipStream_t st);
 void conv1_subsample(int dtype, const float* x_bft, int B, int F, int T, const float* w9, const float* bias, int C,

@@ -439,6 +439,7 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     if (const char* mb = getenv("CFM_MICROBATCH")) h->microbatches = std::max(1, std::min(8, atoi(mb)));
     h->ln_fold = h->dtype == DT_BF16 && h->d % 4 == 0;
     if (const char* lf = getenv("CFM_LN_FOLD")) h->ln_fold = atoi(lf) != 0 && h->d % 4 == 0;
+    if (const char* gd = getenv("CFM_GLU_DW")) h->fuse_glu_dw = atoi(gd) != 0;
     ensure_streams(h.get(), 8);
     HIP_OK(hipSetDevice(prev));
     *out = h.release();
@@ -718,7 +719,23 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
         TM(ST_LN);
         layernorm(dt, X, M, d, Wf(Lw.ln_w[2]), Wf(Lw.ln_b[2]), nullptr, nullptr, nullptr, Hn, 0, st);
       }
-      {
+      if (h->fuse_glu_dw && h->cfg.conv_norm_type == 0 && gemm_glu_dw_supported(dt, Tp, d, h->K)) {
+        // pointwise_conv1 + GLU + pad mask + depthwise conv + BatchNorm + Swish in one launch: one
+        // 256-row tile per utterance, the GLU output stays in LDS
+        TM(ST_PW1);
+        GemmEpi e = epi_of(EPI_GLU_DW, Wf(Lw.pw1_b));
+        e.C = ws + wl.S; e.ldc = d; e.lens = h->use_pad_mask ? lens : nullptr; e.Tp = Tp;
+        e.utt_tp = Tp; e.utt_M = M;
+        e.dw_w = Wf(Lw.dw_w); e.dw_b = Wf(Lw.dw_b);
+        e.bn_mean = Wf(Lw.bn_mean); e.bn_inv = Wf(Lw.bn_inv); e.bn_w = Wf(Lw.bn_w); e.bn_b = Wf(Lw.bn_b);
+        consume(e, Lw.pw1_lc, Lw.pw1_ld);
+        gemm_glu_dw(dt, Hn, d, B, Tp, d, W(fold ? Lw.pw1_wf : Lw.pw1_w), (int)h->kpad(d), d, e, h->zero_page, st);
+        TM(ST_PW2);
+        GemmEpi r = epi_of(EPI_RESID, Wf(Lw.pw2_b), 1.0f);
+        r.X = X; r.ldx = d;
+        produce(r);
+        gemm(dt, ws + wl.S, d, M, d, W(Lw.pw2_w), (int)h->kpad(d), d, r, h->zero_page, st);
+      } else {
         TM(ST_PW1);
         GemmEpi e = epi_of(EPI_GLU_MASK, Wf(Lw.pw1_b));
         e.C = ws + wl.G; e.ldc = d; e.lens = h->use_pad_mask ? lens : nullptr; e.Tp = Tp;

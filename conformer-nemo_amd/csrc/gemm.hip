@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "cfm_common.h"
+#include "cfm_abi.h"
 #include "cfm_kernels.h"
 
 namespace cfm {
@@ -123,13 +124,20 @@ template <int G>
 struct ALoadDense {
   static constexpr bool kConv = false;
   const char* A; long lda_b; int M; long kbytes; const char* zero;
+  int utt_tp, utt_rows;   // utterance-aligned rows (GemmEpi::utt_tp): m -> (m / utt_rows) * utt_tp + m % utt_rows
   struct State { const char* row_ptr[G]; };
   CFM_DEV void shift_k(long koff) { A += koff; kbytes -= koff; }
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-      const int m = m0 + rows[i];
-      s.row_ptr[i] = (m < M) ? A + (long)m * lda_b : nullptr;
+      int m = m0 + rows[i];
+      bool ok = m < M;
+      if (utt_tp > 0) {
+        const int b = m / utt_rows, t = m - b * utt_rows;
+        m = b * utt_tp + t;
+        ok = t < utt_tp && m < M;
+      }
+      s.row_ptr[i] = ok ? A + (long)m * lda_b : nullptr;
     }
   }
   // kb0: the K-step's first byte (wave-uniform); lo: this lane's byte offset within the step
@@ -206,6 +214,14 @@ struct GemmParams {
 // Every global load here is unconditional (clamped address, value selected afterwards): a load
 // under a per-thread condition is branched around by hipcc and serialised behind its own
 // vmcnt(0) (cdna_hip_programming.md §5, 'Three .s-level traps' (c)).
+// The stored row of GEMM row m (clamped into range): itself, or for utterance-aligned rows
+// (GemmEpi::utt_tp, tile height BM) frame m % BM of utterance m / BM.
+CFM_DEV int real_row(const GemmParams& p, int m, int BM) {
+  if (p.epi.utt_tp <= 0) return min(m, p.M - 1);
+  const int b = m / BM, t = m - b * BM;
+  return min(b * p.epi.utt_tp + min(t, p.epi.utt_tp - 1), p.epi.utt_M - 1);
+}
+
 // Folded LayerNorm (GemmEpi::ln_in): rs[r] = (mean, rstd) of the pass's local row r, cd[j] = (c, d)
 // of the tile's local column j.
 CFM_DEV float ln_fold(float2 s, float v, float2 cd) { return s.y * (v - s.x * cd.x) + cd.y; }
@@ -309,6 +325,79 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           const float q2 = halfwave_sum(ok ? (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3) : 0.0f);
           if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, q2);
         }
+      }
+    }
+  } else if constexpr (EPI == EPI_GLU_DW) {
+    // pointwise_conv1 -> GLU -> pad mask -> depthwise conv (k 31, zero padding) -> BatchNorm
+    // (running statistics) -> Swish (conformer_modules.py:160-176) for one utterance (the tile's
+    // 256 rows are its frames, T' <= 256) and 64 channels (the tile's 128 GLU-packed columns); the
+    // GLU output never leaves LDS (the unfused path writes and re-reads it through HBM).
+    if constexpr (TL::BM == 256 && TL::BN == 128 && TL::NT == 512) {
+      constexpr int VE = 8, CPR = 8, RPP = 64, NP = 4, K = 31, PAD = 15, DT = 16, NX = DT + K - 1;
+      const int cc = tid % CPR, r0 = tid / CPR;
+      const int oc_local = cc * VE;
+      const int ca = (oc_local / 32) * 64 + oc_local % 32, cg = ca + 32;
+      const int b = m0 / 256, Tp = e.utt_tp;
+      const int len = e.lens ? min(e.lens[b], Tp) : Tp;   // frames >= T' are zero padding of the conv
+      float gv[NP][VE];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int r = r0 + q * RPP;
+        float2 st;
+        if constexpr (fold) st = rs[r];
+#pragma unroll
+        for (int i = 0; i < VE; ++i) {
+          float a = img[r * TL::EPS + ca + i];
+          float g = img[r * TL::EPS + cg + i];
+          if constexpr (fold) { a = ln_fold(st, a, cd[ca + i]); g = ln_fold(st, g, cd[cg + i]); }
+          gv[q][i] = r < len ? a * sigmoidf_(g) : 0.0f;
+        }
+      }
+      __syncthreads();                     // every wave has read the accumulator image
+      float* gimg = (float*)img;           // [256 frames][64 channels] fp32
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        float4* d4 = (float4*)(gimg + (r0 + q * RPP) * 64 + oc_local);
+        d4[0] = make_float4(gv[q][0], gv[q][1], gv[q][2], gv[q][3]);
+        d4[1] = make_float4(gv[q][4], gv[q][5], gv[q][6], gv[q][7]);
+      }
+      __syncthreads();
+      const int c = tid & 63;
+      const int ch = n0 / 2 + c;           // output channel
+      const int chc = min(ch, p.N - 1);
+      float wk[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) wk[k] = e.dw_w[(long)k * p.N + chc];
+      const float bi = e.dw_b[chc], mu = e.bn_mean[chc], inv = e.bn_inv[chc], gw = e.bn_w[chc], gb = e.bn_b[chc];
+      // outputs are staged as bf16 [256 frames][64 channels] behind the GLU image, then stored as
+      // 16-byte row runs (2-byte per-lane stores would make the tail store-issue bound)
+      T* simg = (T*)((char*)img + 256 * 64 * 4);
+      // 8 waves x 2 windows of 16 frames = 256 frames; lanes = consecutive channels (conflict-free)
+#pragma unroll 1
+      for (int h = 0; h < 2; ++h) {
+        const int t0 = ((tid >> 6) * 2 + h) * DT;
+        float x[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          const int t = t0 - PAD + i;
+          const float v = gimg[min(max(t, 0), 255) * 64 + c];
+          x[i] = (t >= 0 && t < 256) ? v : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < DT; ++j) {
+          float a = 0.0f;
+#pragma unroll
+          for (int k = 0; k < K; ++k) a = fmaf(wk[k], x[j + k], a);
+          a += bi;
+          st_f<T>(simg + (t0 + j) * 64 + c, swishf((a - mu) * inv * gw + gb));
+        }
+      }
+      __syncthreads();
+      constexpr int VO = 16 / (int)sizeof(T);            // channels per 16-byte run
+      for (int i = tid; i < 256 * 64 / VO; i += TL::NT) {
+        const int t = i / (64 / VO), c8 = (i % (64 / VO)) * VO;
+        if (t < Tp && n0 / 2 + c8 < p.N)
+          *(uint4*)((T*)e.C + ((long)b * Tp + t) * e.ldc + n0 / 2 + c8) = *(const uint4*)(simg + t * 64 + c8);
       }
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
@@ -517,7 +606,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   float2 cd_pre = make_float2(0.0f, 0.0f);
   if (p.epi.ln_in) {
     const int np = p.epi.ln_parts;
-    const float2* pp = p.epi.ln_in + (long)min(m0 + min(tid, TL::BM - 1), p.M - 1) * np;
+    const float2* pp = p.epi.ln_in + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
 #pragma unroll
     for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
     const int nc = n0 + min(tid, TL::BN - 1);
@@ -657,7 +746,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   float2* cd_tab = (float2*)(smem + TL::CD_OFF);
   if (p.epi.ln_in) {
     const int W = p.epi.ln_width, np = p.epi.ln_parts;
-    const float2* pp = p.epi.ln_in + (long)min(m0 + min(tid, TL::BM - 1), p.M - 1) * np;
+    const float2* pp = p.epi.ln_in + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
     float sm = 0.0f;
 #pragma unroll
     for (int g = 0; g < LN_PRE; ++g)
@@ -896,7 +985,10 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
 
 struct DenseArgs {
   const char* A; long lda_b; int M; long kbytes; const char* zero;
-  template <class AL> void fill(AL& al) const { al.A = A; al.lda_b = lda_b; al.M = M; al.kbytes = kbytes; al.zero = zero; }
+  int utt_tp = 0, utt_rows = 0;
+  template <class AL> void fill(AL& al) const {
+    al.A = A; al.lda_b = lda_b; al.M = M; al.kbytes = kbytes; al.zero = zero; al.utt_tp = utt_tp; al.utt_rows = utt_rows;
+  }
 };
 struct ConvArgs {
   const char* X1; int T1, F1, T2, F2; long tapb; int M; const char* zero;
@@ -907,7 +999,7 @@ struct ConvArgs {
 };
 
 int packed_width(const GemmEpi& epi, int N) {
-  return epi.mode == EPI_GLU_MASK ? 64 * ((N + 31) / 32) : N;
+  return (epi.mode == EPI_GLU_MASK || epi.mode == EPI_GLU_DW) ? 64 * ((N + 31) / 32) : N;
 }
 
 int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
@@ -1080,6 +1172,30 @@ void gemm_splitk(int dtype, const void* A, long lda, int M, int K, const void* W
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
   g_splits = 1;
+}
+
+bool gemm_glu_dw_supported(int dtype, int Tp, int d, int K) {
+  return dtype == DT_BF16 && Tp >= 1 && Tp <= 256 && d % 64 == 0 && K == 31;
+}
+
+void gemm_glu_dw(int dtype, const void* A, long lda, int B, int Tp, int K, const void* Wp, int Kpad, int N,
+                 const GemmEpi& epi, const void* zero_page, hipStream_t st) {
+  if (B <= 0) return;
+  if (!gemm_glu_dw_supported(dtype, Tp, N, 31) || epi.mode != EPI_GLU_DW || epi.utt_tp != Tp)
+    fail(CFM_ERR_UNSUPPORTED, "gemm_glu_dw: bf16, T' <= 256, d % 64 == 0 only");
+  using TL = T256x128;
+  GemmParams p = make_params(2, B * TL::BM, Wp, Kpad, N, epi);
+  p.probe = g_gemm_probe;
+  p.epi.utt_M = B * Tp;
+  DenseArgs a{(const char*)A, lda * 2, B * Tp, (long)K * 2, (const char*)zero_page};
+  a.utt_tp = Tp;
+  a.utt_rows = TL::BM;
+  p.Mtiles = B;
+  p.Ntiles = packed_width(epi, N) / TL::BN;
+  ALoadDense<TL::GA> al;
+  a.fill(al);
+  cfm_launch((gemm_kernel<bf16_t, EPI_GLU_DW, TL, ALoadDense<TL::GA>>), dim3(p.Mtiles * p.Ntiles), dim3(TL::NT), 0, st,
+             p, al);
 }
 
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,

@@ -201,3 +201,23 @@ def test_bf16_layernorm_fold_matches_unfolded(path, monkeypatch):
     d = rel_l2(out["1"][0], out["0"][0])
     print(f"bf16 relL2 vs reference: fold {out['1'][1]:.3e}, unfolded {out['0'][1]:.3e}; fold vs unfolded {d:.3e}")
     assert d <= 1e-2, f"fold vs unfolded relL2 {d:.3e}"
+
+
+@pytest.mark.parametrize("path", [f for f in ENC_FILES if "large17" in f or "tiny_ctx" in f or "nopadmask" in f
+                                  or "xl_h8" in f], ids=lambda f: os.path.basename(f)[4:-4])
+def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
+    """bf16, T' <= 256: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish run as one launch
+    (gemm_glu_dw, the GLU output stays in LDS); CFM_GLU_DW=0 keeps the GLU GEMM + dwconv kernel.
+    Both meet the bf16 gate and agree to bf16 rounding (the fused conv reads the unrounded GLU)."""
+    z = np.load(path)
+    cfg = json.loads(str(z["cfg_json"]))
+    sd = make_state_dict(cfg, int(z["seed"]))
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_GLU_DW", flag)
+        y, yl = run(native(cfg, "bf16"), sd, z["x"], z["lengths"])
+        assert (yl == z["y_len"]).all()
+        out[flag] = (y, check(y, z["y"], "bf16"))
+    d = rel_l2(out["1"][0], out["0"][0])
+    print(f"bf16 relL2 vs reference: fused {out['1'][1]:.3e}, unfused {out['0'][1]:.3e}; fused vs unfused {d:.3e}")
+    assert d <= 1e-2, f"fused vs unfused relL2 {d:.3e}"
