@@ -15,7 +15,8 @@ import re
 import sys
 
 RESID_ORDER = ["ffn_down_gemm", "out_proj_gemm", "pw2_gemm", "ffn_down_gemm"]
-EPI_STAGE = {"0": "pos_gemm", "2": "ffn_up_gemm", "4": "subsample_linear", "5": "pw1_glu_gemm", "6": "qkv_gemm"}
+EPI_STAGE = {"0": "pos_gemm", "2": "ffn_up_gemm", "4": "subsample_linear", "5": "pw1_glu_gemm", "6": "qkv_gemm",
+             "7": "pw1_glu_gemm"}   # 7: pointwise_conv1 + GLU + depthwise conv + BN + Swish in one launch
 
 
 def stage_of(name, state):
@@ -33,6 +34,8 @@ def stage_of(name, state):
         return "dwconv_bn_swish"
     if name.startswith("transpose_kernel"):
         return "output"
+    if "gemm8_kernel" in name:          # the 8-phase conv2 implicit GEMM
+        return "conv2_gemm"
     m = re.match(r"(?:void )?(?:cfm::)?(?:\(anonymous namespace\)::)?gemm_kernel<[^,]+, (\d+),", name)
     if m:
         if "ALoadConv" in name:
@@ -72,7 +75,15 @@ def main(argv):
         else:
             launches.append([key, 1, dur])
     starts = [i for i, l in enumerate(launches) if "calc_length" in l[0][0]]
-    sel = launches[starts[-nfw]:]
+    # keep the bf16 forwards (bench.py also times an fp32 parity-mode forward at the end): a forward
+    # is bf16 when its conv1 launch is conv1_kernel<unsigned short>
+    bf16 = []
+    for j, s0 in enumerate(starts):
+        end = starts[j + 1] if j + 1 < len(starts) else len(launches)
+        seg = launches[s0:end]
+        if any("conv1_kernel<unsigned short>" in l[0][0] for l in seg):
+            bf16.append(seg)
+    sel = [l for seg in bf16[-nfw:] for l in seg]
     state = {"resid": 0}
     agg = {}
     for key, n, dur in sel:
