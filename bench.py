@@ -195,11 +195,13 @@ def main():
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the bf16/fp32 relL2 against the reference golden and the fp32-mode throughput line")
     ap.add_argument("--no-breakdown", action="store_true")
-    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "mel", "decode"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "cache_stream", "mel", "decode"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
                          "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
                          "joint: config 4 (Large-17 encoder B=16 T=1600 + RNN-T joint U=100 V=1024); "
                          "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks); "
+                         "cache_stream: the same 64 streams and 160-frame chunks through the cache-aware chunked "
+                         "encoder (SURVEY f3, causal variant, 60 frames of attention history); "
                          "mel: the log-mel preprocessor in front of config 2 (SURVEY f1); "
                          "decode: config-4 transducer inference (encoder + greedy batch RNN-T decoding, SURVEY f2)")
     ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
@@ -227,6 +229,8 @@ def main():
         return run_joint(args, world, rank, dev, dist, barrier)
     if args.mode == "stream":
         return run_stream(args, world, rank, dev, dist, barrier)
+    if args.mode == "cache_stream":
+        return run_cache_stream(args, world, rank, dev, dist, barrier)
     if args.mode == "mel":
         return run_mel(args, world, rank, dev, dist, barrier)
     if args.mode == "decode":
@@ -588,6 +592,47 @@ def run_stream(args, world, rank, dev, dist, barrier):
         "model_flops": {"GFLOP_per_step_per_gpu": round(fl / 1e9, 1),
                         "TFLOP/s_per_gpu": round(fl / (ms_step * 1e-3) / 1e12, 1),
                         "frac_of_peak": round(fl / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
+
+
+CACHE_STREAM_METRIC = "cache-aware streaming audio-frames/sec, Conformer-XL B=64 streams, 160-frame chunks"
+
+
+def run_cache_stream(args, world, rank, dev, dist, barrier):
+    """the same 64 XL streams advancing by 160 new frames (1.6 s) per
+    step, through the cache-aware chunked encoder (include/cfm_cache_stream.h): 40 new encoder frames
+    per stream per step, 60 frames of attention history carried as per-layer key/value rings (the
+    40 + 60 = 100 encoder frames the buffered path sees in its 400-frame buffer), conv / subsampling
+    state carried too.  Causal variant of the encoder (parity unpinned, see the header); `value`
+    counts NEW audio frames like --mode stream, so the two lines compare directly."""
+    from nemo.collections.asr.modules import ConformerEncoder
+    torch.manual_seed(0)
+    d, H, L, B, n, left = 1024, 8, 24, 64, 160, 60
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H).to(dev).eval()
+    enc.set_compute_mode(args.compute)
+    st = enc.cache_aware_streamer(batch_size=B, chunk_size=n // 4, left_context=left, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    chunks = torch.randn(8, B, 80, n, device=dev, generator=g) * 4.0 - 6.0   # synthetic log-mel chunks
+    it = [0]
+
+    def step():
+        y = st.step(chunks[it[0] % 8])
+        it[0] += 1
+        return y
+
+    with torch.inference_mode():
+        elapsed, (y, yl) = timed_loop(step, args.warmup, args.steps, barrier)
+        assert torch.isfinite(y).all().item()
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    emit(rank, dist, {
+        "metric": CACHE_STREAM_METRIC, "value": round(world * B * n * args.steps / t_max, 1),
+        "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.compute, "data": "synthetic",
+        "config": {"workload": f"Conformer-XLarge (d1024, 8 heads, {L} layers) cache-aware streaming: B={B} streams, "
+                               f"{n}-frame chunks ({n // 4} encoder frames), left context {left}, causal variant",
+                   "global_batch": B * world, "seq_len": n, "parallelism": f"dp{world} (replicas, no collective)"},
     })
 
 

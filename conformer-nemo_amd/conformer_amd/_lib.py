@@ -57,6 +57,9 @@ RNNT_DECODE_SYMBOLS = ("cfm_rnnt_decoder_create", "cfm_rnnt_decoder_destroy", "c
 COMM_SYMBOLS = ("cfm_comm_get_unique_id", "cfm_comm_init", "cfm_comm_destroy", "cfm_comm_world", "cfm_allreduce_grads",
                 "cfm_comm_allreduce_cb", "cfm_grad_buckets_create", "cfm_grad_buckets_ready_cb",
                 "cfm_grad_buckets_finish", "cfm_grad_buckets_issued", "cfm_grad_buckets_destroy")
+# every symbol include/cfm_cache_stream.h declares (bound in conformer_amd/cache_stream.py)
+CACHE_STREAM_SYMBOLS = ("cfm_cache_stream_create", "cfm_cache_stream_destroy", "cfm_cache_stream_reset",
+                        "cfm_cache_stream_workspace_size", "cfm_cache_stream_step", "cfm_cache_stream_position")
 # every symbol include/cfm_ctc.h declares
 CTC_SYMBOLS = (
     "cfm_ctc_head_create", "cfm_ctc_head_destroy", "cfm_ctc_head_set_weights", "cfm_ctc_head_workspace_size",

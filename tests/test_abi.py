@@ -47,7 +47,11 @@ def test_library_loads_and_exports_header_symbols():
     assert set(dec) == set(_lib.RNNT_DECODE_SYMBOLS)
     comm = _declared_symbols("cfm_comm.h")
     assert set(comm) == set(_lib.COMM_SYMBOLS)
-    for name in ctc + train + joint + stream + mel + rl + aug + dec + comm:
+    cs = _declared_symbols("cfm_cache_stream.h")
+    assert set(cs) == set(_lib.CACHE_STREAM_SYMBOLS)
+    from conformer_amd import cache_stream
+    assert set(cache_stream.SYMBOLS) == set(cs)
+    for name in ctc + train + joint + stream + mel + rl + aug + dec + comm + cs:
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
