@@ -56,6 +56,8 @@ enum Epilogue {
   EPI_QKV = 6,         // packed cols [q | k | v]: C = [q+u | q+v | k] (ldc = 3*H*dkp), v -> Vt[(b*H+h)][d][t]
   EPI_GLU_DW = 7,      // EPI_GLU_MASK + depthwise conv (k 31) + BatchNorm (running stats) + Swish on an
                        // utterance-aligned 256-row tile (utt_tp <= 256 frames): C = conv module's S rows
+  EPI_SWISH_BWD = 8,   // training: C (compute type) = acc * dropout'(m*ldz + n) * swish'(zin[m][n]), the
+                       // FFN hidden's backward through Swish and its dropout (conformer_modules.py:196-198)
 };
 
 // Dropout masks (training): keep element e iff hash(key, e) >= thr, thr = p * 2^32; kept values are
@@ -110,6 +112,9 @@ struct GemmEpi {
   const float* dw_w;   // EPI_GLU_DW: depthwise weight [31][d], bias [d], BatchNorm mean / 1/sqrt(var+eps) / w / b
   const float* dw_b;
   const float *bn_mean, *bn_inv, *bn_w, *bn_b;
+  // EPI_SWISH_BWD: pre-activation z (compute type, ld ldz; also the dropout mask's row pitch)
+  const void* zin;
+  long ldz;
 };
 constexpr int LN_GRANULE = 128;
 

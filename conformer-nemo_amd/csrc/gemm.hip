@@ -466,6 +466,12 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       const int m = m0 + r;
       float2 st;
       if constexpr (fold) st = rs[r];
+      float zf[VE];
+      if constexpr (EPI == EPI_SWISH_BWD) {
+        // z row chunk of this output chunk (host guarantees N % VE == 0); rows past M read row M-1
+        const T* zp = (const T*)e.zin + (long)min(m, p.M - 1) * e.ldz + min(n, nlim - VE);
+        Vec16<T>::to_f32(*(const uint4*)zp, zf);
+      }
       float o[VE];
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
@@ -473,6 +479,10 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
         if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
         if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
         if constexpr (EPI == EPI_SWISH) v = swishf(v);
+        if constexpr (EPI == EPI_SWISH_BWD) {
+          const float zz = zf[i], sg = sigmoidf_(zz);
+          v *= drop_mul(e.drop, (uint64_t)m * (uint64_t)e.ldz + (uint64_t)(n + i)) * (sg + zz * sg * (1.0f - sg));
+        }
         o[i] = v;
       }
       if (m >= p.M || n >= nlim) continue;
@@ -979,6 +989,7 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
     case EPI_SCALE_F32: cfm_launch((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad>), grid, block, 0, st, p, al); break;
     case EPI_GLU_MASK: cfm_launch((gemm_kernel<T, EPI_GLU_MASK, TL, ALoad>), grid, block, 0, st, p, al); break;
     case EPI_QKV: cfm_launch((gemm_kernel<T, EPI_QKV, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SWISH_BWD: cfm_launch((gemm_kernel<T, EPI_SWISH_BWD, TL, ALoad>), grid, block, 0, st, p, al); break;
     default: break;
   }
 }

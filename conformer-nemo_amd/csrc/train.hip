@@ -1629,19 +1629,50 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gres, 0.5f, n_md,
                  S.drop(site(l, f ? 5 : 1)), dbr);
       const Drop di = S.drop(site(l, f ? 4 : 0));
-      // linear2 (input u = dropout(swish(z)) recomputed from z)
-      linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f],
-                 WT[f ? WT_FF2_W2 : WT_FF1_W2]);
-      const long n = (long)M * g.dff;
-      if (dt == DT_F32)
-        cfm_launch(swish_drop_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z),
-                   (const float*)dU, n, di, dU);
-      else
-        cfm_launch(swish_drop_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z),
-                   (const float*)dU, n, di, dU);
       float* dhn = S.W_<float>(S.wl.dctx);
-      linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f], q.ff_b1[f],
-                 WT[f ? WT_FF2_W1 : WT_FF1_W1]);
+      if (S.kpad(g.dff) == g.dff) {
+        // linear2's dgrad carries the Swish + dropout backward in its epilogue and writes the FFN
+        // hidden's gradient dz in the compute type (no fp32 round trip, no elementwise pass); dz then
+        // feeds linear1's dgrad as its A operand directly and its wgrad through one transpose pack
+        void* dz = S.W_(S.wl.dU);
+        {
+          const int N = d, K = g.dff;
+          const bool want_w = Gp(q.ff_w2[f]) != nullptr, want_b = Gp(q.ff_b2[f]) != nullptr;
+          if (want_w || want_b) S.pack2(dbr, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq);
+          else S.pack(dbr, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
+          GemmEpi e = S.epi(EPI_SWISH_BWD, nullptr);
+          e.C = dz; e.ldc = K; e.zin = S.T_(z); e.ldz = K; e.drop = di;
+          gemm(dt, pa, S.kpad(N), M, N, WT[f ? WT_FF2_W2 : WT_FF1_W2], S.kpad(N), K, e, h->zero_page, st);
+          if (want_w || want_b) {   // [dW2 | db2] = dy^T . [u | 1], u = dropout(swish(z)) recomputed
+            S.pack(S.T_(z), true, K, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, 1, di, want_b ? K : -1);
+            S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(q.ff_w2[f]) : nullptr, want_b ? Gp(q.ff_b2[f]) : nullptr);
+          }
+        }
+        {
+          const int N = g.dff, K = d;
+          S.gemm_f32out(dz, N, M, N, WT[f ? WT_FF2_W1 : WT_FF1_W1], K, nullptr, 1.0f, dhn, d, false);
+          const bool want_w = Gp(q.ff_w1[f]) != nullptr, want_b = Gp(q.ff_b1[f]) != nullptr;
+          if (want_w || want_b) {   // [dW1 | db1] = dz^T . [hn | 1]
+            S.pack(dz, true, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
+            S.pack(hn, true, d, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, 0, Drop{0, 0, 1.0f},
+                   want_b ? K : -1);
+            S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(q.ff_w1[f]) : nullptr, want_b ? Gp(q.ff_b1[f]) : nullptr);
+          }
+        }
+      } else {
+        // linear2 (input u = dropout(swish(z)) recomputed from z)
+        linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f],
+                   WT[f ? WT_FF2_W2 : WT_FF1_W2]);
+        const long n = (long)M * g.dff;
+        if (dt == DT_F32)
+          cfm_launch(swish_drop_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z),
+                     (const float*)dU, n, di, dU);
+        else
+          cfm_launch(swish_drop_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z),
+                     (const float*)dU, n, di, dU);
+        linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f],
+                   q.ff_b1[f], WT[f ? WT_FF2_W1 : WT_FF1_W1]);
+      }
       ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true);
     };
     ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, gB);   // gB = d x3
