@@ -58,6 +58,8 @@ enum Epilogue {
                        // utterance-aligned 256-row tile (utt_tp <= 256 frames): C = conv module's S rows
   EPI_SWISH_BWD = 8,   // training: C (compute type) = acc * dropout'(m*ldz + n) * swish'(zin[m][n]), the
                        // FFN hidden's backward through Swish and its dropout (conformer_modules.py:196-198)
+  EPI_SWISH_Z = 9,     // training: C = z = acc + bias and C2 = dropout(swish(z)) (mask index m*ldc + n), both
+                       // compute type, ld ldc: the FFN hidden and its pre-activation tape in one pass
 };
 
 // Dropout masks (training): keep element e iff hash(key, e) >= thr, thr = p * 2^32; kept values are
@@ -115,6 +117,7 @@ struct GemmEpi {
   // EPI_SWISH_BWD: pre-activation z (compute type, ld ldz; also the dropout mask's row pitch)
   const void* zin;
   long ldz;
+  void* C2;            // EPI_SWISH_Z: second output
 };
 constexpr int LN_GRANULE = 128;
 

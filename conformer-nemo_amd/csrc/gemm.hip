@@ -513,6 +513,16 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       } else {
         for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
       }
+      if constexpr (EPI == EPI_SWISH_Z) {
+        // the FFN hidden u = dropout(swish(z)) next to z itself (z is the backward's tape)
+        float u[VE];
+#pragma unroll
+        for (int i = 0; i < VE; ++i)
+          u[i] = swishf(o[i]) * drop_mul(e.drop, (uint64_t)m * (uint64_t)e.ldc + (uint64_t)(n + i));
+        T* du = (T*)e.C2 + (long)m * e.ldc + n;
+        if (vec) *(uint4*)du = Vec16<T>::from_f32(u);
+        else for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(du + i, u[i]);
+      }
     }
     if constexpr (EPI == EPI_QKV) {
       // V columns -> Vt[(b*H + h)][dd][t] as 16-byte runs of G consecutive frames ("octets" for bf16):
@@ -990,6 +1000,7 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
     case EPI_GLU_MASK: cfm_launch((gemm_kernel<T, EPI_GLU_MASK, TL, ALoad>), grid, block, 0, st, p, al); break;
     case EPI_QKV: cfm_launch((gemm_kernel<T, EPI_QKV, TL, ALoad>), grid, block, 0, st, p, al); break;
     case EPI_SWISH_BWD: cfm_launch((gemm_kernel<T, EPI_SWISH_BWD, TL, ALoad>), grid, block, 0, st, p, al); break;
+    case EPI_SWISH_Z: cfm_launch((gemm_kernel<T, EPI_SWISH_Z, TL, ALoad>), grid, block, 0, st, p, al); break;
     default: break;
   }
 }

@@ -148,7 +148,7 @@ template <typename Tout>
 __global__ __launch_bounds__(256) void tpack2_kernel(const float* __restrict__ src, long src_ld, int rows, int cols,
                                                        Tout* __restrict__ dA, long ldA, int rpA, int cpA,
                                                        Tout* __restrict__ dT, long ldT, int rpT, int cpT,
-                                                       int src_vec, int vecA, int vecT) {
+                                                       int src_vec, int vecA, int vecT, float scale, Drop dr) {
   __shared__ float tile[64][65];   // [src row][src col]
   const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
   const int c4 = threadIdx.x & 15, r = threadIdx.x >> 4;
@@ -167,6 +167,10 @@ __global__ __launch_bounds__(256) void tpack2_kernel(const float* __restrict__ s
         for (int e = 0; e < 4; ++e)
           if (sj + e < cols) v[e] = sp[e];
       }
+    }
+    if (scale != 1.0f || dr.thr) {   // dy = scale * dropout'(g): the residual branch's dropout backward
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= scale * drop_mul(dr, (uint64_t)si * (uint64_t)src_ld + (uint64_t)(sj + e));
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) tile[rr][cc + e] = v[e];
@@ -306,13 +310,6 @@ __global__ __launch_bounds__(256) void perm_pack_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------------------------
 // elementwise forward pieces
 // ---------------------------------------------------------------------------------------------
-// u = dropout(swish(z)) in the compute type (FFN hidden, conformer_modules.py:196-198)
-template <typename T>
-__global__ __launch_bounds__(256) void swish_drop_kernel(const T* __restrict__ z, long n, Drop drop,
-                                                         T* __restrict__ u) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
-    st_f<T>(u + i, swishf(ld_f<T>(z + i)) * drop_mul(drop, (uint64_t)i));
-}
 // xout = xin + alpha * dropout(br) (residual update, conformer_modules.py:101-118); xout may alias xin
 __global__ __launch_bounds__(256) void resid_drop_kernel(const float* xin, const float* __restrict__ br, float alpha,
                                                          long n, Drop drop, float* xout) {
@@ -1185,7 +1182,7 @@ struct Step {
   }
   // pack(dy, .., dA, lA, rA, cA) and pack(dy, transposed, .., dT, lT, rT, cT) in one launch
   void pack2(const float* src, long ld, int rows, int cols, void* dA, long lA, int rA, int cA, void* dT, long lT, int rT,
-             int cT) const {
+             int cT, float scale = 1.0f, Drop dr = Drop{0, 0, 1.0f}) const {
     const int des = g.dt == DT_F32 ? 4 : 2;
     const int gx = (std::max(cA, rT) + 63) / 64, gy = (std::max(rA, cT) + 63) / 64;
     if (gx <= 0 || gy <= 0) return;
@@ -1194,10 +1191,10 @@ struct Step {
     const int vt = (lT % (16 / des) == 0 && ((uintptr_t)dT % 16) == 0) ? 1 : 0;
     if (g.dt == DT_F32)
       cfm_launch(tpack2_kernel<float>, dim3(gx, gy), dim3(256), 0, st, src, ld, rows, cols, (float*)dA, lA, rA, cA,
-                 (float*)dT, lT, rT, cT, sv, va, vt);
+                 (float*)dT, lT, rT, cT, sv, va, vt, scale, dr);
     else
       cfm_launch(tpack2_kernel<bf16_t>, dim3(gx, gy), dim3(256), 0, st, src, ld, rows, cols, (bf16_t*)dA, lA, rA, cA,
-                 (bf16_t*)dT, lT, rT, cT, sv, va, vt);
+                 (bf16_t*)dT, lT, rT, cT, sv, va, vt, scale, dr);
   }
   // packed forward weight W (N, K) fp32 -> [Npad][Kpad]; transposed Wt -> [Kpad256][Npad_kg]
   void packW(const float* w, int N, int K, void* dst) const {
@@ -1416,18 +1413,14 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
     auto ffn = [&](int f, float* xin, void* hn, long z, float* xout) {
       const long w1 = f ? S.wl.w1b : S.wl.w1, b1 = f ? S.wl.b1b : S.wl.b1;
       const long w2 = f ? S.wl.w2b : S.wl.w2, b2 = f ? S.wl.b2b : S.wl.b2;
-      GemmEpi e = S.epi(EPI_STORE, S.W_<float>(b1));
-      e.C = S.T_(z);
-      e.ldc = g.dff;
-      gemm(dt, hn, d, M, d, S.W_(w1), S.kpad(d), g.dff, e, h->zero_page, st);
-      const long n = (long)M * g.dff;
       const Drop di = S.drop(site(l, f ? 4 : 0));
-      if (dt == DT_F32)
-        cfm_launch(swish_drop_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z), n, di,
-                   S.W_<float>(S.wl.u));
-      else
-        cfm_launch(swish_drop_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const bf16_t>(z), n, di,
-                   S.W_<bf16_t>(S.wl.u));
+      // z (the backward's tape) and u = dropout(swish(z)) from one GEMM epilogue
+      GemmEpi e = S.epi(EPI_SWISH_Z, S.W_<float>(b1));
+      e.C = S.T_(z);
+      e.C2 = S.W_(S.wl.u);
+      e.ldc = g.dff;
+      e.drop = di;
+      gemm(dt, hn, d, M, d, S.W_(w1), S.kpad(d), g.dff, e, h->zero_page, st);
       S.gemm_resid_drop(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 0.5f, xin, xout, d,
                         S.drop(site(l, f ? 5 : 1)));
     };
@@ -1554,11 +1547,19 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   // Linear y = x W^T + b backward for a dense fp32 output gradient dy (M, N):
   //   dx (M, K) fp32 (ldx; accumulate or overwrite), dW (N, K) -> G[gw], db -> G[gb]
   //   x is the saved compute-type input (M, K) (ld ldxin), or xfn = 1: dropout(swish(z)) recomputed
+  //   dy may carry a scale and a dropout mask (ysc, ydr: the residual branch's dropout backward),
+  //   applied while packing (or by one elementwise pass into dbr when no transposed pack is needed)
   auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
-                        float* dx, long ldx, bool acc, int gw, int gb, const void* wtp) {
+                        float* dx, long ldx, bool acc, int gw, int gb, const void* wtp, float ysc = 1.0f,
+                        Drop ydr = Drop{0, 0, 1.0f}) {
     const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
-    if (dx && (want_w || want_b))
-      S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq);
+    const bool fused_y = dx && (want_w || want_b);
+    if (!fused_y && (ysc != 1.0f || ydr.thr)) {
+      cfm_launch(scale_drop_kernel, dim3(ew_grid((long)M * N)), dim3(256), 0, st, dy, ysc, (long)M * N, ydr, dbr);
+      dy = dbr;
+    }
+    if (fused_y)
+      S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq, ysc, ydr);
     else if (dx)
       S.pack(dy, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
     if (dx) {
@@ -1626,8 +1627,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     // FFN block backward: residual grad g (d xout) -> += d xin through the branch
     auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, float* gres) {
       float* dU = S.W_<float>(S.wl.dU);
-      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gres, 0.5f, n_md,
-                 S.drop(site(l, f ? 5 : 1)), dbr);
+      const Drop dres = S.drop(site(l, f ? 5 : 1));
       const Drop di = S.drop(site(l, f ? 4 : 0));
       float* dhn = S.W_<float>(S.wl.dctx);
       if (S.kpad(g.dff) == g.dff) {
@@ -1638,8 +1638,13 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         {
           const int N = d, K = g.dff;
           const bool want_w = Gp(q.ff_w2[f]) != nullptr, want_b = Gp(q.ff_b2[f]) != nullptr;
-          if (want_w || want_b) S.pack2(dbr, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq);
-          else S.pack(dbr, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
+          if (want_w || want_b) {
+            S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq, 0.5f, dres);
+          } else {
+            cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gres, 0.5f, n_md, dres,
+                       dbr);
+            S.pack(dbr, false, N, M, N, false, 1.0f, pa, S.kpad(N), M, S.kpad(N));
+          }
           GemmEpi e = S.epi(EPI_SWISH_BWD, nullptr);
           e.C = dz; e.ldc = K; e.zin = S.T_(z); e.ldz = K; e.drop = di;
           gemm(dt, pa, S.kpad(N), M, N, WT[f ? WT_FF2_W2 : WT_FF1_W2], S.kpad(N), K, e, h->zero_page, st);
@@ -1661,8 +1666,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         }
       } else {
         // linear2 (input u = dropout(swish(z)) recomputed from z)
-        linear_bwd(dbr, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f],
-                   WT[f ? WT_FF2_W2 : WT_FF1_W2]);
+        linear_bwd(gres, d, S.prm(q.ff_w2[f]), g.dff, S.T_(z), g.dff, 1, di, dU, g.dff, false, q.ff_w2[f], q.ff_b2[f],
+                   WT[f ? WT_FF2_W2 : WT_FF1_W2], 0.5f, dres);
         const long n = (long)M * g.dff;
         if (dt == DT_F32)
           cfm_launch(swish_drop_bwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.T_<const float>(z),
@@ -1679,11 +1684,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
 
     // ---- convolution module ----
     {
-      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
-                 S.drop(site(l, 3)), dbr);
       float* dS = S.W_<float>(S.wl.dD);
-      linear_bwd(dbr, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b,
-                 WT[WT_PW2]);
+      linear_bwd(gB, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b,
+                 WT[WT_PW2], 1.0f, S.drop(site(l, 3)));
       float* dZ = S.W_<float>(S.wl.dG);
       const float* xhat = S.T_<const float>(t.xhat);
       cfm_launch(bn_swish_bwd_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dS, xhat, S.prm(q.bn_w),
@@ -1721,11 +1724,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
 
     // ---- attention ----
     {
-      cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gB, 1.0f, n_md,
-                 S.drop(site(l, 2)), dbr);
       float* dctx = S.W_<float>(S.wl.dctx);
-      linear_bwd(dbr, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b,
-                 WT[WT_OUT]);
+      linear_bwd(gB, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b,
+                 WT[WT_OUT], 1.0f, S.drop(site(l, 2)));
       float* dqkv = S.W_<float>(S.wl.dqkv);
       float* dP = S.W_<float>(S.wl.dP);
       const int dk = g.dk;
