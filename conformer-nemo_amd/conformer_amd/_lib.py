@@ -12,7 +12,8 @@ import ctypes
 import os
 from typing import Optional
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcfm.so")
+# CFM_LIB_PATH: load another build of the library (same-process A/B timing in tools/)
+LIB_PATH = os.environ.get("CFM_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcfm.so")
 
 CFM_COMPUTE_FP32 = 0
 CFM_COMPUTE_BF16 = 1

@@ -138,6 +138,16 @@ constexpr float RESCALE_THR = 8.0f;   // log2 units: P entries may reach 2^8 bef
 // need it (uniform branch).
 // `rowx` XORs the BD image row (0 or 32): the LDS kernel keeps the two 32-position halves of the
 // window in a 2-slot ring and swaps their roles every key tile.
+// value of lane l ^ 32 combined with this lane's by a half exchange (v_permlane32_swap, no LDS trip)
+CFM_DEV float halves_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+CFM_DEV float halves_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, int j0, int len, int iq, int lane,
                           int rowx = 0) {
   const int col = lane & 31;
@@ -163,7 +173,7 @@ CFM_DEV float tile_scores(f32x16& st, const float* bd_s, const AttnParams& p, in
       mloc = fmaxf(mloc, st[r]);
     }
   }
-  return fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+  return halves_max(mloc);
 }
 
 // Online softmax with deferred rescale: the running max of a row is raised only when the tile max
@@ -200,7 +210,7 @@ CFM_DEV void softmax_tile(f32x16& st, float mloc, float& m_run, float& l_run, f3
     st[r] = __builtin_amdgcn_exp2f(st[r] - m_use);
     psum += st[r];
   }
-  l_run += psum + __shfl_xor(psum, 32, 64);
+  l_run += halves_sum(psum);
 }
 
 template <typename T, int NS, int ND>
