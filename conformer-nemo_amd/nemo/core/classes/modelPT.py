@@ -51,6 +51,22 @@ class NoamAnnealing(torch.optim.lr_scheduler.LambdaLR):
         super().__init__(optimizer, [factor(i) for i in range(len(bases))], last_epoch)
 
 
+def _check_targets(conf: Any, where: str, path: str = "model") -> None:
+    """A `.nemo` config is untrusted input: every `_target_` in it must name one of this package's
+    drop-in modules (save_restore_connector.RESTORABLE_TARGETS) before any of it is instantiated."""
+    from nemo.core.connectors.save_restore_connector import RESTORABLE_TARGETS
+    if isinstance(conf, Mapping):
+        t = conf.get("_target_")
+        if t is not None and t not in RESTORABLE_TARGETS:
+            raise ValueError(f"refusing to instantiate {path}._target_={t!r} from {where}: "
+                             f"not one of this package's drop-in modules")
+        for k, v in conf.items():
+            _check_targets(v, where, f"{path}.{k}")
+    elif isinstance(conf, (list, tuple)):
+        for i, v in enumerate(conf):
+            _check_targets(v, where, f"{path}[{i}]")
+
+
 class ModelPT(NeuralModule):
     def __init__(self, cfg: Any, trainer=None):
         super().__init__()
@@ -83,6 +99,7 @@ class ModelPT(NeuralModule):
         from nemo.core.connectors.save_restore_connector import SaveRestoreConnector
         conf, sd = SaveRestoreConnector().load_config_and_state_dict(
             restore_path, override_config_path=override_config_path, map_location="cpu")
+        _check_targets(conf, restore_path)
         model = cls(Config(conf))
         model.load_state_dict(sd, strict=strict)
         if map_location is not None:

@@ -114,6 +114,32 @@ def test_save_restore_roundtrip(tok_dir, tmp_path):
     assert a.keys() == b.keys() and all(torch.equal(a[k], b[k]) for k in a)
 
 
+def test_restore_refuses_foreign_targets(tok_dir, tmp_path):
+    """A .nemo config is untrusted: a `_target_` outside this package's drop-in modules is refused
+    before anything is instantiated (nothing in the file runs)."""
+    import yaml
+    from nemo.collections.asr.models import EncDecCTCModelBPE
+    from nemo.core.config import load_config
+    from nemo.core.connectors import SaveRestoreConnector
+    m = EncDecCTCModelBPE(load_config(CTC_BPE_SMALL, {"model.tokenizer.dir": tok_dir}).model)
+    marker = tmp_path / "pwned"
+    cfg = m.cfg.to_dict()
+    cfg["encoder"] = {"_target_": "subprocess.getoutput", "cmd": f"touch {marker}"}
+    path = str(tmp_path / "evil.nemo")
+    SaveRestoreConnector._make_nemo_file_from_members(path, {
+        "model_config.yaml": yaml.safe_dump(cfg).encode(), "model_weights.ckpt": _state_bytes(m)})
+    with pytest.raises(ValueError, match="refusing"):
+        EncDecCTCModelBPE.restore_from(path)
+    assert not marker.exists()
+
+
+def _state_bytes(m):
+    import io
+    buf = io.BytesIO()
+    torch.save(m.state_dict(), buf)
+    return buf.getvalue()
+
+
 def test_wer_metrics():
     from nemo.collections.asr.metrics.wer import WER, word_error_rate
     assert word_error_rate(["a b c", "x"], ["a c c", "x y"]) == pytest.approx(2 / 5)
