@@ -190,6 +190,14 @@ void rel_pos_attention_backward(int dtype, const void* qk, long ldqk, const void
                                 hipStream_t st, Drop adrop = Drop{0u, 0u, 1.0f});
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
 
+// Weight gradient on frame-major operands (wgrad_tn.hip, bf16): out[n][k] (fp32, ld ldo) = sum over
+// rows r of A[r][n] * B'[r][k] with B' = B (bfn 0) or dropout(swish(B)) (bfn 1, mask index r*ldb + k),
+// column K of B' all ones when `ones` (bias), zero beyond; S row splits of `chunk` rows (a multiple of
+// 32) write partial tiles at out + s * split_stride.  Columns 0 .. Kout-1 are written.
+bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb);
+void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bool ones, int bfn, Drop bdr, long rows,
+              int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st);
+
 // ---- backward building blocks (backward.hip) ----
 // dst[i][j] = transpose ? src[j][i] : src[i][j] in the compute type for i < rows_pad, j < cols_pad;
 // src is fp32 [rows][cols] (ld src_ld), zero outside it.

@@ -514,11 +514,15 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
         for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(dst + i, o[i]);
       }
       if constexpr (EPI == EPI_SWISH_Z) {
-        // the FFN hidden u = dropout(swish(z)) next to z itself (z is the backward's tape)
+        // the FFN hidden u = dropout(swish(z)) next to z itself (z is the backward's tape); u is formed
+        // from z as stored (compute type), exactly as the backward recomputes it
+        T zt[VE];
+#pragma unroll
+        for (int i = 0; i < VE; ++i) st_f<T>(&zt[i], o[i]);
         float u[VE];
 #pragma unroll
         for (int i = 0; i < VE; ++i)
-          u[i] = swishf(o[i]) * drop_mul(e.drop, (uint64_t)m * (uint64_t)e.ldc + (uint64_t)(n + i));
+          u[i] = swishf(ld_f<T>((const T*)&zt[i])) * drop_mul(e.drop, (uint64_t)m * (uint64_t)e.ldc + (uint64_t)(n + i));
         T* du = (T*)e.C2 + (long)m * e.ldc + n;
         if (vec) *(uint4*)du = Vec16<T>::from_f32(u);
         else for (int i = 0; i < VE && n + i < nlim; ++i) st_f<T>(du + i, u[i]);
@@ -1079,6 +1083,9 @@ int pick_tile(int dtype, int M, int Nw, int epi, bool conv, int K = 0) {
     // the subsampling Linear (K = C * F2 = 10240, N = d): 64 tiles of 256x256 fill a quarter of the
     // chip; 128x128 in two K-groups (same K order as the small-M 64x128 K-group tile): 154 -> ~100 us
     if (epi == EPI_SCALE_F32 && K >= 4096) return M >= 4096 ? 12 : 16;
+    // the training step's fp32-output dgrads (M = B*T' rows, N = d): 128x128 K-group tiles
+    // (tools/train_ab.sh: 38.5-38.8 against 38.9-39.2 ms per step for the 64x128 tile)
+    if (epi == EPI_SCALE_F32 && M >= 4096) return 14;
     return 5;
   }
   if (conv || (long)M * Nw >= (long)32 << 20) return 1;

@@ -921,7 +921,7 @@ struct Alloc {
   long take(long bytes) { const long o = round_up(off, 256); off = o + round_up(std::max(bytes, 1L), 256); return o; }
 };
 
-struct TapeLayer { long x[5], hn[4], z1, z2, qk, vt, P, ctx, pre, g, xhat, mean, rstd, s; };
+struct TapeLayer { long x[5], hn[4], z1, z2, u1, u2, qk, vt, P, ctx, pre, g, xhat, mean, rstd, s; };
 struct Tape { long xin, lens, X1, X2; std::vector<TapeLayer> lay; long xfin, total; };
 
 Tape tape_layout(const cfm_encoder* h, const Geo& g) {
@@ -938,6 +938,10 @@ Tape tape_layout(const cfm_encoder* h, const Geo& g) {
     for (long& v : l.hn) v = a.take(M * d * es);
     l.z1 = a.take(M * g.dff * es);
     l.z2 = a.take(M * g.dff * es);
+    // the FFN hiddens u = dropout(swish(z)) too: the weight gradient of linear2 reads them as they
+    // are instead of recomputing the activation and its mask per output tile
+    l.u1 = a.take(M * g.dff * es);
+    l.u2 = a.take(M * g.dff * es);
     l.qk = a.take(M * 3 * g.H * g.dkp * es);
     l.vt = a.take((long)g.B * g.H * h->vt_rows * g.Tpad * es);
     l.P = a.take((long)g.NP * g.H * g.dkp * es + 64);
@@ -1282,6 +1286,31 @@ struct Step {
     else
       cfm_launch(slab_sum_kernel, dim3(ew_grid(n / 4 + 1)), dim3(256), 0, st, (const float*)part, S, n, out);
   }
+  // [dW | db] = A^T . [B' | 1] straight from frame-major compute-type operands (wgrad_tn.hip): A
+  // (rows x N, lda) is the packed dy, B (rows x K, ldb) the saved input, B' = dropout(swish(B)) when
+  // bfn = 1.  Split-K over the rows into the same [S][N][K+4] partials as wgrad(), at most as many
+  // splits as wgrad() would use (the partial buffer is sized for those).
+  bool wgrad_rm_ok(int N, int K, long lda, long ldb) const { return wgrad_tn_supported(g.dt, N, K, lda, ldb); }
+  void wgrad_rm(const void* A, long lda, int N, const void* B, long ldb, int K, int bfn, Drop bdr, long rows,
+                float* out, float* bias) const {
+    const int Kb = bias ? K + 4 : K;
+    const long tiles = (long)((N + 127) / 128) * ((Kb + 127) / 128);
+    long S = std::min<long>((512 + tiles - 1) / tiles, wgrad_splits(N, Kb, rows));
+    S = std::max<long>(1, std::min<long>(S, rows / 256));
+    const long chunk = round_up((rows + S - 1) / S, 32);
+    S = (rows + chunk - 1) / chunk;
+    if (S == 1 && !bias) {
+      wgrad_tn(A, lda, N, B, ldb, K, false, bfn, bdr, rows, 1, chunk, out, K, K, 0, st);
+      return;
+    }
+    float* part = W_<float>(wl.part);
+    wgrad_tn(A, lda, N, B, ldb, K, bias != nullptr, bfn, bdr, rows, (int)S, chunk, part, Kb, Kb, (long)N * Kb, st);
+    const long n = (long)N * Kb;
+    if (bias)
+      cfm_launch(slab_sum_wb_kernel, dim3(ew_grid(n)), dim3(256), 0, st, (const float*)part, (int)S, N, K, out, bias);
+    else
+      cfm_launch(slab_sum_kernel, dim3(ew_grid(n / 4 + 1)), dim3(256), 0, st, (const float*)part, (int)S, n, out);
+  }
   void sync(float* buf, long n) const {
     if (o->world > 1 && o->allreduce) {
       if (o->allreduce(o->allreduce_user, buf, (int64_t)n, (void*)st) != 0) fail(CFM_ERR_HIP, "allreduce callback failed");
@@ -1410,23 +1439,23 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       S.flush(b);
     }
     // ---- FFN1 / FFN2 (conformer_modules.py:99-101, 116-118, 183-200) ----
-    auto ffn = [&](int f, float* xin, void* hn, long z, float* xout) {
+    auto ffn = [&](int f, float* xin, void* hn, long z, long u, float* xout) {
       const long w1 = f ? S.wl.w1b : S.wl.w1, b1 = f ? S.wl.b1b : S.wl.b1;
       const long w2 = f ? S.wl.w2b : S.wl.w2, b2 = f ? S.wl.b2b : S.wl.b2;
       const Drop di = S.drop(site(l, f ? 4 : 0));
       // z (the backward's tape) and u = dropout(swish(z)) from one GEMM epilogue
       GemmEpi e = S.epi(EPI_SWISH_Z, S.W_<float>(b1));
       e.C = S.T_(z);
-      e.C2 = S.W_(S.wl.u);
+      e.C2 = S.T_(u);
       e.ldc = g.dff;
       e.drop = di;
       gemm(dt, hn, d, M, d, S.W_(w1), S.kpad(d), g.dff, e, h->zero_page, st);
-      S.gemm_resid_drop(S.W_(S.wl.u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 0.5f, xin, xout, d,
+      S.gemm_resid_drop(S.T_(u), g.dff, M, g.dff, S.W_(w2), d, S.W_<float>(b2), 0.5f, xin, xout, d,
                         S.drop(site(l, f ? 5 : 1)));
     };
     layernorm(dt, X[0], M, d, S.prm(q.ln_w[LN_FF1]), S.prm(q.ln_b[LN_FF1]), nullptr, nullptr, nullptr, S.T_(t.hn[0]),
               0, st);
-    ffn(0, X[0], S.T_(t.hn[0]), t.z1, X[1]);
+    ffn(0, X[0], S.T_(t.hn[0]), t.z1, t.u1, X[1]);
 
     // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
     layernorm(dt, X[1], M, d, S.prm(q.ln_w[LN_ATT]), S.prm(q.ln_b[LN_ATT]), nullptr, nullptr, nullptr, S.T_(t.hn[1]),
@@ -1500,7 +1529,7 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
     }
     layernorm(dt, X[3], M, d, S.prm(q.ln_w[LN_FF2]), S.prm(q.ln_b[LN_FF2]), nullptr, nullptr, nullptr, S.T_(t.hn[3]),
               0, st);
-    ffn(1, X[3], S.T_(t.hn[3]), t.z2, X[4]);
+    ffn(1, X[3], S.T_(t.hn[3]), t.z2, t.u2, X[4]);
     // ---- norm_out (conformer_modules.py:120) -> next layer's input (fp32) ----
     float* nxt = l + 1 < g.L ? S.T_<float>(S.tp.lay[l + 1].x[0]) : S.T_<float>(S.tp.xfin);
     layernorm(dt, X[4], M, d, S.prm(q.ln_w[LN_OUT]), S.prm(q.ln_b[LN_OUT]), nxt, nullptr, nullptr, nullptr, 0, st);
@@ -1553,6 +1582,21 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
                         float* dx, long ldx, bool acc, int gw, int gb, const void* wtp, float ysc = 1.0f,
                         Drop ydr = Drop{0, 0, 1.0f}) {
     const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
+    if ((want_w || want_b) && S.wgrad_rm_ok(N, K, S.kpad(N), ldxin)) {
+      // dy packed once (row-major, scale + dropout applied), used by the dgrad GEMM and, as it lies,
+      // by the weight gradient; the saved input is read in place
+      S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, ysc, ydr);
+      if (dx) {
+        const void* W = wtp;
+        if (!W) {
+          S.packWt(w, N, K, wt);
+          W = wt;
+        }
+        S.gemm_f32out(pa, S.kpad(N), M, N, W, K, nullptr, 1.0f, dx, ldx, acc);
+      }
+      S.wgrad_rm(pa, S.kpad(N), N, xin, ldxin, K, xfn, xdr, M, want_w ? Gp(gw) : nullptr, want_b ? Gp(gb) : nullptr);
+      return;
+    }
     const bool fused_y = dx && (want_w || want_b);
     if (!fused_y && (ysc != 1.0f || ydr.thr)) {
       cfm_launch(scale_drop_kernel, dim3(ew_grid((long)M * N)), dim3(256), 0, st, dy, ysc, (long)M * N, ydr, dbr);
@@ -1625,7 +1669,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     ln_bwd(X[4], q.ln_w[LN_OUT], q.ln_b[LN_OUT], gA, gB, false);
 
     // FFN block backward: residual grad g (d xout) -> += d xin through the branch
-    auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, float* gres) {
+    auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, long u, float* gres) {
       float* dU = S.W_<float>(S.wl.dU);
       const Drop dres = S.drop(site(l, f ? 5 : 1));
       const Drop di = S.drop(site(l, f ? 4 : 0));
@@ -1638,7 +1682,10 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         {
           const int N = d, K = g.dff;
           const bool want_w = Gp(q.ff_w2[f]) != nullptr, want_b = Gp(q.ff_b2[f]) != nullptr;
-          if (want_w || want_b) {
+          const bool rm = S.wgrad_rm_ok(N, K, S.kpad(N), K) && S.wgrad_rm_ok(K, N, K, d);
+          if (rm) {
+            S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, 0.5f, dres);
+          } else if (want_w || want_b) {
             S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq, 0.5f, dres);
           } else {
             cfm_launch(scale_drop_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)gres, 0.5f, n_md, dres,
@@ -1648,7 +1695,10 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
           GemmEpi e = S.epi(EPI_SWISH_BWD, nullptr);
           e.C = dz; e.ldc = K; e.zin = S.T_(z); e.ldz = K; e.drop = di;
           gemm(dt, pa, S.kpad(N), M, N, WT[f ? WT_FF2_W2 : WT_FF1_W2], S.kpad(N), K, e, h->zero_page, st);
-          if (want_w || want_b) {   // [dW2 | db2] = dy^T . [u | 1], u = dropout(swish(z)) recomputed
+          if (rm && (want_w || want_b)) {   // [dW2 | db2] = dy^T . [u | 1], u = dropout(swish(z)) recomputed
+            S.wgrad_rm(pa, S.kpad(N), N, S.T_(u), K, K, 0, Drop{0, 0, 1.0f}, M, want_w ? Gp(q.ff_w2[f]) : nullptr,
+                       want_b ? Gp(q.ff_b2[f]) : nullptr);
+          } else if (want_w || want_b) {
             S.pack(S.T_(z), true, K, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, 1, di, want_b ? K : -1);
             S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(q.ff_w2[f]) : nullptr, want_b ? Gp(q.ff_b2[f]) : nullptr);
           }
@@ -1657,7 +1707,10 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
           const int N = g.dff, K = d;
           S.gemm_f32out(dz, N, M, N, WT[f ? WT_FF2_W1 : WT_FF1_W1], K, nullptr, 1.0f, dhn, d, false);
           const bool want_w = Gp(q.ff_w1[f]) != nullptr, want_b = Gp(q.ff_b1[f]) != nullptr;
-          if (want_w || want_b) {   // [dW1 | db1] = dz^T . [hn | 1]
+          if ((want_w || want_b) && S.wgrad_rm_ok(N, K, N, d)) {   // [dW1 | db1] = dz^T . [hn | 1]
+            S.wgrad_rm(dz, N, N, hn, d, K, 0, Drop{0, 0, 1.0f}, M, want_w ? Gp(q.ff_w1[f]) : nullptr,
+                       want_b ? Gp(q.ff_b1[f]) : nullptr);
+          } else if (want_w || want_b) {
             S.pack(dz, true, N, M, N, true, 1.0f, pat, Mq, N, (int)Mq);
             S.pack(hn, true, d, M, K, true, 1.0f, pbt, Mq, S.npad(K + 4), (int)Mq, 0, Drop{0, 0, 1.0f},
                    want_b ? K : -1);
@@ -1680,7 +1733,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       }
       ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true);
     };
-    ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, gB);   // gB = d x3
+    ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, t.u2, gB);   // gB = d x3
 
     // ---- convolution module ----
     {
@@ -1769,7 +1822,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true);   // gB = d x1
       }
     }
-    ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, gB);   // gB = d x0
+    ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, t.u1, gB);   // gB = d x0
     std::swap(gA, gB);
     grad_ready(S, kPreEncodeRows + l * layer_rows, layer_rows);   // every gradient of layer l is enqueued
   }

@@ -1,0 +1,158 @@
+// Weight-gradient GEMM on row-major operands (training, bf16): out[n][k] = sum_r A[r][n] * B'[r][k].
+//
+// The layer gradients dW = dy^T . x reduce over the B*T' frame rows, and both dy and x are stored
+// frame-major ([rows][features], features contiguous).  The MFMA operands want 8 consecutive
+// reduction rows per lane, i.e. a column of those images: each K-step stages 32 frame rows of A and
+// of B into LDS exactly as they lie in HBM (16-byte chunks, XOR-swizzled 256-byte rows) and the
+// fragments are read with ds_read_b64_tr_b16, gfx950's transposing LDS read (4 rows x 16 columns
+// per 16-lane group, delivered column-major).  No transposed copy of any activation is made.
+//
+// B' extends B: column K is all ones when `ones` (the bias gradient sum_r A[r][n] comes out as
+// column K), columns beyond are zero; bfn = 1 recomputes B' = dropout(swish(B)) while staging (the
+// FFN hidden from its pre-activation tape, mask index r * ldb + k as the forward epilogue).
+// Split-K over frame rows: split s writes its partial tile at out + s * split_stride.
+#include <hip/hip_runtime.h>
+
+#include "cfm_common.h"
+#include "cfm_kernels.h"
+
+namespace cfm {
+namespace {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+constexpr int TB = 128;   // output tile (n rows x k columns)
+constexpr int TK = 32;    // frame rows per K-step
+
+// byte offset of 16-byte chunk `ch` (0..15) of image row `row` (256-byte rows)
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// 32x32x16 operand fragment of columns cb .. cb+31, frame rows kb .. kb+15 of an image
+__device__ __forceinline__ uint4 tr_frag(const char* img, int cb, int kb, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int c0 = (cb + 16 * (g & 1)) >> 3;
+  const int r0 = kb + 8 * (g >> 1);
+  const v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(img + img_off(r0 + q, c0 + (p >> 1)) + 8 * (p & 1)));
+  const v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(img + img_off(r0 + 4 + q, c0 + (p >> 1)) + 8 * (p & 1)));
+  const uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  return make_uint4(ua.x, ua.y, ub.x, ub.y);
+}
+
+template <int BFN>
+__global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16_t* __restrict__ A, long lda, int N,
+                                                       const bf16_t* __restrict__ B, long ldb, int K, int ones,
+                                                       Drop bdr, long rows, long chunk, float* __restrict__ out,
+                                                       long ldo, int Kout, long split_stride) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TK * 256];   // [buf][A|B][32 rows][256 B]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int n0 = blockIdx.y * TB, k0 = blockIdx.x * TB;
+  const long r_beg = (long)blockIdx.z * chunk;
+  const long r_end = min(rows, r_beg + chunk);
+  const int nsteps = (int)((r_end - r_beg + TK - 1) / TK);
+
+  // staging: thread tid moves chunks tid and tid + 256 of each 32 x 16-chunk operand tile
+  uint4 ra[2], rb[2];
+  auto load = [&](long r0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j, r = c >> 4, ch = c & 15;
+      const long rr = r0 + r;
+      const bool rok = rr < r_end;
+      const int na = n0 + ch * 8;
+      ra[j] = (rok && na < N) ? *(const uint4*)(A + rr * lda + na) : make_uint4(0, 0, 0, 0);
+      const int kb = k0 + ch * 8;
+      if (rok && kb < K) {
+        uint4 v = *(const uint4*)(B + rr * ldb + kb);
+        if (BFN == 1) {
+          float f[8];
+          Vec16<bf16_t>::to_f32(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = swishf(f[e]) * drop_mul(bdr, (uint64_t)rr * (uint64_t)ldb + (uint64_t)(kb + e));
+          v = Vec16<bf16_t>::from_f32(f);
+        }
+        rb[j] = v;
+      } else {
+        rb[j] = make_uint4((rok && ones && kb == K) ? 0x3f80u : 0u, 0, 0, 0);   // bf16 1.0 in column K
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* ia = smem + buf * (2 * TK * 256);
+    char* ib = ia + TK * 256;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j, r = c >> 4, ch = c & 15;
+      *(uint4*)(ia + img_off(r, ch)) = ra[j];
+      *(uint4*)(ib + img_off(r, ch)) = rb[j];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  if (nsteps > 0) {
+    load(r_beg);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) load(r_beg + (long)(s + 1) * TK);
+    const char* ia = smem + (s & 1) * (2 * TK * 256);
+    const char* ib = ia + TK * 256;
+#pragma unroll
+    for (int ks = 0; ks < TK; ks += 16) {
+      uint4 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(ia, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = tr_frag(ib, wn * 64 + j * 32, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[i], fb[j]);
+    }
+    if (more) store((s + 1) & 1);
+    __syncthreads();
+  }
+  float* o = out + (long)blockIdx.z * split_stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = k0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = n0 + wm * 64 + i * 32 + acc_row(e, lane);
+        if (row < N && col < Kout) o[(long)row * ldo + col] = acc[i][j][e];
+      }
+    }
+}
+
+}  // namespace
+
+bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb) {
+  return dtype == DT_BF16 && N % 8 == 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0;
+}
+
+void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bool ones, int bfn, Drop bdr, long rows,
+              int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st) {
+  if (N <= 0 || Kout <= 0) return;
+  const dim3 grid((unsigned)((Kout + TB - 1) / TB), (unsigned)((N + TB - 1) / TB), (unsigned)S), block(256);
+  if (bfn == 1)
+    cfm_launch(wgrad_tn_kernel<1>, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
+               ones ? 1 : 0, bdr, rows, chunk, out, ldo, Kout, split_stride);
+  else
+    cfm_launch(wgrad_tn_kernel<0>, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
+               ones ? 1 : 0, bdr, rows, chunk, out, ldo, Kout, split_stride);
+}
+
+}  // namespace cfm
