@@ -1791,9 +1791,14 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       // dropout_emb, regenerated from the step's seed; compute type)
       if (Gp(q.pos_w)) {
         const char* pe_slice = pos_win;
-        S.pack(dP, false, d, g.NP, d, true, 1.0f, pat, Mq, d, (int)Mq);
-        S.pack(pe_slice, true, d, g.NP, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
-        S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), nullptr);
+        if (S.wgrad_rm_ok(d, d, S.kpad(d), d)) {
+          S.pack(dP, false, d, g.NP, d, false, 1.0f, pa, S.kpad(d), g.NP, S.kpad(d));
+          S.wgrad_rm(pa, S.kpad(d), d, pe_slice, d, d, 0, Drop{0, 0, 1.0f}, g.NP, Gp(q.pos_w), nullptr);
+        } else {
+          S.pack(dP, false, d, g.NP, d, true, 1.0f, pat, Mq, d, (int)Mq);
+          S.pack(pe_slice, true, d, g.NP, d, true, 1.0f, pbt, Mq, S.npad(d), (int)Mq);
+          S.wgrad(pat, pbt, Mq, d, d, g.NP, Gp(q.pos_w), nullptr);
+        }
       }
       // q/k/v: biases, input gradient through [Wq; Wk; Wv], stacked weight gradient
       S.pack(dqkv, false, 3L * d, M, 3 * d, false, 1.0f, pa, S.kpad(3L * d), M, S.kpad(3L * d));
@@ -1803,10 +1808,14 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         S.gemm_f32out(pa, S.kpad(3L * d), M, 3 * d, wt, d, nullptr, 1.0f, dhn, d, false);
         const int bi3[3] = {q.q_b, q.k_b, q.v_b};
         if (Gp(q.q_w) || Gp(q.k_w) || Gp(q.v_w) || Gp(q.q_b) || Gp(q.k_b) || Gp(q.v_b)) {
-          S.pack(dqkv, false, 3L * d, M, 3 * d, true, 1.0f, pat, Mq, 3 * d, (int)Mq);
-          S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, d);
           float* tmp = S.W_<float>(S.wl.gtmp);   // (3d, d) stacked weight gradient, then the (3d) biases
-          S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, tmp + 3L * d * d);
+          if (S.wgrad_rm_ok(3 * d, d, S.kpad(3L * d), d)) {
+            S.wgrad_rm(pa, S.kpad(3L * d), 3 * d, S.T_(t.hn[1]), d, d, 0, Drop{0, 0, 1.0f}, M, tmp, tmp + 3L * d * d);
+          } else {
+            S.pack(dqkv, false, 3L * d, M, 3 * d, true, 1.0f, pat, Mq, 3 * d, (int)Mq);
+            S.pack(S.T_(t.hn[1]), true, d, M, d, true, 1.0f, pbt, Mq, S.npad(d + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, d);
+            S.wgrad(pat, pbt, Mq, 3 * d, d, M, tmp, tmp + 3L * d * d);
+          }
           CopyList cl{};
           for (int p = 0; p < 3; ++p) {
             cl.src[2 * p] = tmp + (long)p * d * d;
@@ -1836,10 +1845,15 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   S.perm(S.prm(S.i_sw), 1, wt, false, S.kpad(d), S.npad(KS), S.kpad(d));
   S.gemm_f32out(pa, S.kpad(d), M, d, wt, KS, nullptr, 1.0f, dX2, KS, false);
   if (Gp(S.i_sw) || Gp(S.i_sb)) {
-    S.pack(dbr, false, d, M, d, true, 1.0f, pat, Mq, d, (int)Mq);
-    S.pack(S.T_(S.tp.X2), true, KS, M, KS, true, 1.0f, pbt, Mq, S.npad(KS + 4), (int)Mq, 0, Drop{0, 0, 1.0f}, KS);
     float* tmp = S.W_<float>(S.wl.gtmp);   // (d, KS) permuted gradient
-    S.wgrad(pat, pbt, Mq, d, KS, M, tmp, Gp(S.i_sb));
+    if (S.wgrad_rm_ok(d, KS, S.kpad(d), KS)) {
+      S.wgrad_rm(pa, S.kpad(d), d, S.T_(S.tp.X2), KS, KS, 0, Drop{0, 0, 1.0f}, M, tmp, Gp(S.i_sb));
+    } else {
+      S.pack(dbr, false, d, M, d, true, 1.0f, pat, Mq, d, (int)Mq);
+      S.pack(S.T_(S.tp.X2), true, KS, M, KS, true, 1.0f, pbt, Mq, S.npad(KS + 4), (int)Mq, 0, Drop{0, 0, 1.0f},
+             KS);
+      S.wgrad(pat, pbt, Mq, d, KS, M, tmp, Gp(S.i_sb));
+    }
     if (Gp(S.i_sw)) S.perm(tmp, 4, Gp(S.i_sw), true, KS, d, KS);
   }
   // conv2 + ReLU: dY2 = dX2 * [X2 > 0], rows (b, t2, f2) x C

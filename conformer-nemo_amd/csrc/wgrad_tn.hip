@@ -13,6 +13,8 @@
 // Split-K over frame rows: split s writes its partial tile at out + s * split_stride.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "cfm_common.h"
 #include "cfm_kernels.h"
 
@@ -137,6 +139,109 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16_t* __restrict_
     }
 }
 
+// ---- LDS-DMA variant (bfn = 0): NST-stage ring filled by global_load_lds_dwordx4, counted waits ----
+__device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};
+__device__ uint4 g_one16 = {0x3f80u, 0u, 0u, 0u};   // bf16 1.0 then zeros: the bias column's chunk
+
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// at most `ahead` stages of G loads each still in flight
+template <int G, int MAXA> __device__ __forceinline__ void wait_ahead(int ahead) {
+  if constexpr (MAXA <= 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= MAXA) wait_vm<G * MAXA>();
+    else wait_ahead<G, MAXA - 1>(ahead);
+  }
+}
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr int NST = 4;                    // ring stages (prefetch distance NST - 1)
+constexpr int STAGE = 2 * TK * 256;       // A and B images of one K-step (16 KB)
+
+__global__ __launch_bounds__(256) void wgrad_tn_glds_kernel(const bf16_t* __restrict__ A, long lda, int N,
+                                                            const bf16_t* __restrict__ B, long ldb, int K, int ones,
+                                                            long rows, long chunk, float* __restrict__ out, long ldo,
+                                                            int Kout, long split_stride) {
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int n0 = blockIdx.y * TB, k0 = blockIdx.x * TB;
+  const long r_beg = (long)blockIdx.z * chunk;
+  const long r_end = min(rows, r_beg + chunk);
+  const int nsteps = (int)((r_end - r_beg + TK - 1) / TK);
+  const uint32_t sb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)smem;
+  // stage s -> slot s % NST: wave w moves row groups 2w, 2w+1 (4 rows = 1 KB each) of A and of B;
+  // lane l fills physical chunk l % 16 of row 4*rg + l / 16, i.e. loads the logical chunk that the
+  // XOR swizzle puts there (LDS-DMA writes are lane-linear)
+  auto issue = [&](int s) {
+    const uint32_t base = sb + (uint32_t)((s % NST) * STAGE);
+    const long r0 = r_beg + (long)s * TK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rg = 2 * w + i, row = rg * 4 + (lane >> 4), pc = lane & 15;
+      const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const long rr = r0 + row;
+      const bool rok = rr < r_end;
+      const int na = n0 + ch * 8;
+      const void* sa = (rok && na < N) ? (const void*)(A + rr * lda + na) : (const void*)&g_zero16;
+      glds16(sa, base + rg * 1024);
+      const int kb = k0 + ch * 8;
+      const void* sbp = (rok && kb < K) ? (const void*)(B + rr * ldb + kb)
+                                        : (rok && ones && kb == K) ? (const void*)&g_one16 : (const void*)&g_zero16;
+      glds16(sbp, base + TK * 256 + rg * 1024);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  constexpr int D = NST - 1;
+  for (int s = 0; s < D && s < nsteps; ++s) issue(s);
+  for (int s = 0; s < nsteps; ++s) {
+    wait_ahead<4, D - 1>(min(D, nsteps - s) - 1);   // this wave's loads of stage s have landed
+    bar();                                           // everyone's have; slot (s-1) % NST is free
+    if (s + D < nsteps) issue(s + D);
+    const char* ia = smem + (s % NST) * STAGE;
+    const char* ib = ia + TK * 256;
+#pragma unroll
+    for (int ks = 0; ks < TK; ks += 16) {
+      uint4 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(ia, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = tr_frag(ib, wn * 64 + j * 32, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[i], fb[j]);
+    }
+  }
+  float* o = out + (long)blockIdx.z * split_stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = k0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = n0 + wm * 64 + i * 32 + acc_row(e, lane);
+        if (row < N && col < Kout) o[(long)row * ldo + col] = acc[i][j][e];
+      }
+    }
+}
+
 }  // namespace
 
 bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb) {
@@ -147,6 +252,12 @@ void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bo
               int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st) {
   if (N <= 0 || Kout <= 0) return;
   const dim3 grid((unsigned)((Kout + TB - 1) / TB), (unsigned)((N + TB - 1) / TB), (unsigned)S), block(256);
+  static const bool glds = [] { const char* e = getenv("CFM_WGRAD_GLDS"); return !e || atoi(e) != 0; }();
+  if (bfn == 0 && glds) {
+    cfm_launch(wgrad_tn_glds_kernel, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
+               ones ? 1 : 0, rows, chunk, out, ldo, Kout, split_stride);
+    return;
+  }
   if (bfn == 1)
     cfm_launch(wgrad_tn_kernel<1>, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
                ones ? 1 : 0, bdr, rows, chunk, out, ldo, Kout, split_stride);
