@@ -571,8 +571,8 @@ struct BwdGeom {
   long sld, gld, s_bytes, g_bytes, t_bytes, cs_bytes, p_bytes;
   static constexpr int kPosSplit = 16;    // split-K of the position-gradient GEMM (K = B*T')
   BwdGeom(int B, int Tp, int H, int dk) {
-    sld = round_up(Tp, 4);
-    gld = round_up(2L * Tp - 1, 4);
+    sld = round_up(Tp, 8);            // multiples of 8 elements: 16-byte rows for the TN products
+    gld = round_up(2L * Tp - 1, 8);
     const long BH = (long)B * H;
     s_bytes = round_up(BH * Tp * sld * 4, 256);
     g_bytes = round_up(BH * Tp * gld * 4, 256);
@@ -584,6 +584,10 @@ struct BwdGeom {
 };
 
 }  // namespace
+
+// wgrad_tn.hip: batched C = alpha * A^T . B on row-major bf16 operands (false: operands unsuitable)
+bool bgemm_tn(const void* A, long lda, long az1, long az2, const void* B, long ldb, long bz1, long bz2, float* C,
+              long ldc, long cz1, long cz2, int M, int N, int K, int Z, int Z2, int Ktot, float alpha, hipStream_t st);
 
 size_t rel_pos_attention_backward_ws(int B, int Tp, int H, int dk) { return BwdGeom(B, Tp, H, dk).total(); }
 
@@ -685,8 +689,9 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
   }
   if (dvb) col_sums(tmp, (long)H * dk, (int)BT, H * dk, dvb, 0, cs, st);
   cfm_launch(add_rows_kernel, dim3(1024), dim3(256), 0, st, dq, ld_dqkv, (const float*)tmp, (long)H * dk, BT, H * dk);
-  // dk = dS^T . (q+u)c * ln2
-  {
+  // dk = dS^T . (q+u)c * ln2  (bf16: both operands are frame-major -> the TN kernel)
+  if (!(fused && bgemm_tn(dP, g.sld, (long)H * szs, szs, qkc, ldqk, (long)Tp * ldqk, dkp, dk_, ld_dqkv,
+                          (long)Tp * ld_dqkv, dk, Tp, dk, Tp, Z, H, 0, ln2, st))) {
     BgArgs a = A0(dP, 1, g.sld, (long)H * szs, szs);
     setB(a, qkc, ldqk, 1, (long)Tp * ldqk, dkp);
     setC(a, dk_, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
@@ -712,7 +717,10 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     setB(a, qkc + (long)H * dkp * es, ldqk, 1, dkp, (long)kc * ldqk);
     setC(a, part, (long)H * dk, 1, dk, NP * H * dk);
     a.M = (int)NP; a.N = dk; a.K = kc; a.Z2 = S; a.alpha = ln2; a.accumulate = 0; a.Ktot = (int)BT;
-    bgemm(dt, a, opS, OP_CT, H * S, st);
+    if (!(fused && bgemm_tn(G, g.gld, (long)B * szg, (long)kc * g.gld, qkc + (long)H * dkp * es, ldqk, dkp,
+                            (long)kc * ldqk, part, (long)H * dk, dk, NP * H * dk, (int)NP, dk, kc, H * S, S,
+                            (int)BT, ln2, st)))
+      bgemm(dt, a, opS, OP_CT, H * S, st);
     cfm_launch(slab_rows_kernel, dim3(1024), dim3(256), 0, st, (const float*)part, S, NP, H * dk, dpos, ld_dpos);
   }
 }

@@ -169,36 +169,50 @@ __device__ __forceinline__ void bar() {
 constexpr int NST = 4;                    // ring stages (prefetch distance NST - 1)
 constexpr int STAGE = 2 * TK * 256;       // A and B images of one K-step (16 KB)
 
-__global__ __launch_bounds__(256) void wgrad_tn_glds_kernel(const bf16_t* __restrict__ A, long lda, int N,
-                                                            const bf16_t* __restrict__ B, long ldb, int K, int ones,
-                                                            long rows, long chunk, float* __restrict__ out, long ldo,
-                                                            int Kout, long split_stride) {
+// General form (both weight gradients and the attention backward's batched products):
+//   C[z][m][n] (fp32, ld ldc) = alpha * sum_{r < rows_z} A[z][r][m] * B'[z][r][n]
+// with z = blockIdx.z = z1 * Z2 + z2 placing A at A + z1*az1 + z2*az2 (likewise B, C) and rows_z = K,
+// or min(K, Ktot - z2*K) when Ktot > 0 (split-K slices of one reduction).  Columns m < M of A and
+// n < N of B are real (reads past them only feed discarded outputs); B' column N is all ones when
+// `ones`.  Output columns < Nout are written.
+struct TnArgs {
+  const bf16_t* A; long lda, az1, az2;
+  const bf16_t* B; long ldb, bz1, bz2;
+  float* C; long ldc, cz1, cz2;
+  int M, N, Nout, K, Z2, Ktot, ones;
+  float alpha;
+};
+
+__global__ __launch_bounds__(256) void tn_glds_kernel(TnArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int n0 = blockIdx.y * TB, k0 = blockIdx.x * TB;
-  const long r_beg = (long)blockIdx.z * chunk;
-  const long r_end = min(rows, r_beg + chunk);
-  const int nsteps = (int)((r_end - r_beg + TK - 1) / TK);
+  const int m0 = blockIdx.y * TB, c0 = blockIdx.x * TB;
+  const int z = blockIdx.z, z1 = z / p.Z2, z2 = z - z1 * p.Z2;
+  const bf16_t* A = p.A + z1 * p.az1 + z2 * p.az2;
+  const bf16_t* B = p.B + z1 * p.bz1 + z2 * p.bz2;
+  const long rows = p.Ktot > 0 ? min((long)p.K, (long)p.Ktot - (long)z2 * p.K) : (long)p.K;
+  const int nsteps = rows > 0 ? (int)((rows + TK - 1) / TK) : 0;
   const uint32_t sb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)smem;
   // stage s -> slot s % NST: wave w moves row groups 2w, 2w+1 (4 rows = 1 KB each) of A and of B;
   // lane l fills physical chunk l % 16 of row 4*rg + l / 16, i.e. loads the logical chunk that the
   // XOR swizzle puts there (LDS-DMA writes are lane-linear)
   auto issue = [&](int s) {
     const uint32_t base = sb + (uint32_t)((s % NST) * STAGE);
-    const long r0 = r_beg + (long)s * TK;
+    const long r0 = (long)s * TK;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rg = 2 * w + i, row = rg * 4 + (lane >> 4), pc = lane & 15;
       const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
       const long rr = r0 + row;
-      const bool rok = rr < r_end;
-      const int na = n0 + ch * 8;
-      const void* sa = (rok && na < N) ? (const void*)(A + rr * lda + na) : (const void*)&g_zero16;
+      const bool rok = rr < rows;
+      const int na = m0 + ch * 8;
+      const void* sa = (rok && na < p.M) ? (const void*)(A + rr * p.lda + na) : (const void*)&g_zero16;
       glds16(sa, base + rg * 1024);
-      const int kb = k0 + ch * 8;
-      const void* sbp = (rok && kb < K) ? (const void*)(B + rr * ldb + kb)
-                                        : (rok && ones && kb == K) ? (const void*)&g_one16 : (const void*)&g_zero16;
+      const int kb = c0 + ch * 8;
+      const void* sbp = (rok && kb < p.N) ? (const void*)(B + rr * p.ldb + kb)
+                                          : (rok && p.ones && kb == p.N) ? (const void*)&g_one16
+                                                                         : (const void*)&g_zero16;
       glds16(sbp, base + TK * 256 + rg * 1024);
     }
   };
@@ -228,21 +242,37 @@ __global__ __launch_bounds__(256) void wgrad_tn_glds_kernel(const bf16_t* __rest
         for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[i], fb[j]);
     }
   }
-  float* o = out + (long)blockIdx.z * split_stride;
+  float* o = p.C + z1 * p.cz1 + z2 * p.cz2;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int col = k0 + wn * 64 + j * 32 + (lane & 31);
+      const int col = c0 + wn * 64 + j * 32 + (lane & 31);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = n0 + wm * 64 + i * 32 + acc_row(e, lane);
-        if (row < N && col < Kout) o[(long)row * ldo + col] = acc[i][j][e];
+        const int row = m0 + wm * 64 + i * 32 + acc_row(e, lane);
+        if (row < p.M && col < p.Nout) o[(long)row * p.ldc + col] = p.alpha * acc[i][j][e];
       }
     }
 }
 
 }  // namespace
+
+// Batched TN product for attn_bwd.hip (see TnArgs); false when the operands do not qualify
+// (bf16, 16-byte aligned bases, strides multiples of 8 elements).
+bool bgemm_tn(const void* A, long lda, long az1, long az2, const void* B, long ldb, long bz1, long bz2, float* C,
+              long ldc, long cz1, long cz2, int M, int N, int K, int Z, int Z2, int Ktot, float alpha, hipStream_t st) {
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (!al(A) || !al(B) || lda % 8 || ldb % 8 || az1 % 8 || az2 % 8 || bz1 % 8 || bz2 % 8 || N % 8) return false;
+  TnArgs p{};
+  p.A = (const bf16_t*)A; p.lda = lda; p.az1 = az1; p.az2 = az2;
+  p.B = (const bf16_t*)B; p.ldb = ldb; p.bz1 = bz1; p.bz2 = bz2;
+  p.C = C; p.ldc = ldc; p.cz1 = cz1; p.cz2 = cz2;
+  p.M = M; p.N = N; p.Nout = N; p.K = K; p.Z2 = Z2; p.Ktot = Ktot; p.ones = 0; p.alpha = alpha;
+  const dim3 grid((unsigned)((N + TB - 1) / TB), (unsigned)((M + TB - 1) / TB), (unsigned)Z), block(256);
+  cfm_launch(tn_glds_kernel, grid, block, 0, st, p);
+  return true;
+}
 
 bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb) {
   return dtype == DT_BF16 && N % 8 == 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0;
@@ -254,8 +284,13 @@ void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bo
   const dim3 grid((unsigned)((Kout + TB - 1) / TB), (unsigned)((N + TB - 1) / TB), (unsigned)S), block(256);
   static const bool glds = [] { const char* e = getenv("CFM_WGRAD_GLDS"); return !e || atoi(e) != 0; }();
   if (bfn == 0 && glds) {
-    cfm_launch(wgrad_tn_glds_kernel, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
-               ones ? 1 : 0, rows, chunk, out, ldo, Kout, split_stride);
+    TnArgs p{};
+    p.A = (const bf16_t*)A; p.lda = lda; p.az2 = chunk * lda;
+    p.B = (const bf16_t*)B; p.ldb = ldb; p.bz2 = chunk * ldb;
+    p.C = out; p.ldc = ldo; p.cz2 = split_stride;
+    p.M = N; p.N = K; p.Nout = Kout; p.K = (int)chunk; p.Z2 = S; p.Ktot = (int)rows; p.ones = ones ? 1 : 0;
+    p.alpha = 1.0f;
+    cfm_launch(tn_glds_kernel, grid, block, 0, st, p);
     return;
   }
   if (bfn == 1)
