@@ -698,8 +698,15 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
     a.M = Tp; a.N = dk; a.K = Tp; a.Z2 = H; a.alpha = ln2; a.accumulate = 0;
     bgemm(dt, a, opS, OP_CT, Z, st);
   }
-  // dv = P^T . dctx
-  {
+  // dv = P^T . dctx (bf16: dctx rounded to bf16 in the tmp region, then the TN kernel)
+  bool dv_done = false;
+  if (fused && ld_dctx == (long)H * dk && dk % 8 == 0) {
+    bf16_t* dctx16 = (bf16_t*)tmp;   // tmp (d(q+v)) was consumed by add_rows above
+    convert_f32(DT_BF16, dctx, dctx16, BT * H * dk, st);
+    dv_done = bgemm_tn(S, g.sld, (long)H * szs, szs, dctx16, (long)H * dk, (long)Tp * H * dk, dk, dv, ld_dqkv,
+                       (long)Tp * ld_dqkv, dk, Tp, dk, Tp, Z, H, 0, 1.0f, st);
+  }
+  if (!dv_done) {
     BgArgs a = A0(S, 1, g.sld, (long)H * szs, szs);
     setB(a, dctx, ld_dctx, 1, (long)Tp * ld_dctx, dk);
     setC(a, dv, ld_dqkv, 1, (long)Tp * ld_dqkv, dk);
