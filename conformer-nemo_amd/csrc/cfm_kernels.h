@@ -192,9 +192,13 @@ void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st)
 
 // Weight gradient on frame-major operands (wgrad_tn.hip, bf16): out[n][k] (fp32, ld ldo) = sum over
 // rows r of A[r][n] * B'[r][k] with B' = B (bfn 0) or dropout(swish(B)) (bfn 1, mask index r*ldb + k),
-// column K of B' all ones when `ones` (bias), zero beyond; S row splits of `chunk` rows (a multiple of
+// the bias sum_r A[r][n] at column K when `ones`; S row splits of `chunk` rows (a multiple of
 // 32) write partial tiles at out + s * split_stride.  Columns 0 .. Kout-1 are written.
 bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb);
+// output tiles of one row split (bias in-kernel for bfn 0: no extra column tile) and the block count
+// the row splits aim for (two 128x128 blocks or one larger block per CU)
+int wgrad_tn_tiles(int N, int K, bool ones, int bfn);
+int wgrad_tn_blocks(int bfn);
 void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bool ones, int bfn, Drop bdr, long rows,
               int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st);
 

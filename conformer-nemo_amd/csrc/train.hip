@@ -990,6 +990,18 @@ int wgrad_splits(int N, int K, long rows) {
   return (int)std::max<long>(1, std::min<long>(s, 16));
 }
 
+// Row splits of a frame-major weight gradient (wgrad_tn): enough (tile, split) blocks for the target
+// block count (CFM_TN_BLOCKS overrides it for A/B runs), at least 64 frame rows per split, at most 16
+long tn_splits(int N, int K, bool bias, int bfn, long rows) {
+  static const long env_target = [] { const char* e = getenv("CFM_TN_BLOCKS"); return e ? atol(e) : 0L; }();
+  const long tiles = wgrad_tn_tiles(N, K, bias, bfn);
+  const long target = env_target > 0 ? env_target : wgrad_tn_blocks(bfn);
+  long S = (target + tiles - 1) / tiles;
+  S = std::max<long>(1, std::min<long>({S, rows / 64, 16L}));
+  const long chunk = round_up((rows + S - 1) / S, 32);
+  return (rows + chunk - 1) / chunk;
+}
+
 enum { WT_FF1_W2 = 0, WT_FF1_W1, WT_FF2_W2, WT_FF2_W1, WT_PW2, WT_PW1, WT_OUT };
 struct Ws {
   // forward
@@ -1060,6 +1072,11 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   auto upd = [&](long N, long K, long rows) { part = std::max(part, (long)wgrad_splits((int)N, (int)K, rows) * N * K); };
   upd(dff, d + 4, M); upd(d, dff + 4, M); upd(3 * d, d + 4, M); upd(d, d + 4, M); upd(2 * d, d + 4, M);
   upd(d, d, g.NP); upd(d, (long)g.F2 * g.C + 4, M); upd(g.C, 9L * g.C + 4, g.M2);
+  auto upd_tn = [&](long N, long K, bool bias, long rows) {   // Ws::wgrad_rm (both staging forms)
+    for (int bfn = 0; bfn < 2; ++bfn) part = std::max(part, tn_splits((int)N, (int)K, bias, bfn, rows) * N * (bias ? K + 4 : K));
+  };
+  upd_tn(dff, d, true, M); upd_tn(d, dff, true, M); upd_tn(3 * d, d, true, M); upd_tn(d, d, true, M);
+  upd_tn(2 * d, d, true, M); upd_tn(d, d, false, g.NP); upd_tn(d, (long)g.F2 * g.C, true, M);
   w.part = a.take(part * 4);
   w.dqkv = a.take(M * 3 * d * 4);
   w.dctx = a.take(M * d * 4);
@@ -1294,9 +1311,7 @@ struct Step {
   void wgrad_rm(const void* A, long lda, int N, const void* B, long ldb, int K, int bfn, Drop bdr, long rows,
                 float* out, float* bias) const {
     const int Kb = bias ? K + 4 : K;
-    const long tiles = (long)((N + 127) / 128) * ((Kb + 127) / 128);
-    long S = std::min<long>((512 + tiles - 1) / tiles, wgrad_splits(N, Kb, rows));
-    S = std::max<long>(1, std::min<long>(S, rows / 256));
+    long S = tn_splits(N, K, bias != nullptr, bfn, rows);
     const long chunk = round_up((rows + S - 1) / S, 32);
     S = (rows + chunk - 1) / chunk;
     if (S == 1 && !bias) {

@@ -13,6 +13,7 @@
 // Split-K over frame rows: split s writes its partial tile at out + s * split_stride.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "cfm_common.h"
@@ -183,37 +184,51 @@ struct TnArgs {
   float alpha;
 };
 
-__global__ __launch_bounds__(256) void tn_glds_kernel(TnArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+// Output tile (128*MI) x (128*NI) on 4*MI*NI waves of 64 x 64; a stage holds MI A and NI B column
+// images of 32 frame rows x 128 columns (8 KB each, the 128x128 image layout), so every wave reads
+// its fragments exactly as in the 128x128 kernel.  Larger tiles move fewer L2 -> LDS bytes per MFMA.
+// Bias (p.ones): the block whose column tile is (row tile % column tiles) also sums its A fragments
+// (frame rows of dy for its columns) in VALU beside the MFMAs (waves of the first wave column) and
+// writes sum_r A[r][m] at output column p.N - no appended ones column, so no extra column tile.
+template <int MI, int NI>
+__global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
+  constexpr int TM = TB * MI, TN = TB * NI, NW = 4 * MI * NI, WN = 2 * NI;
+  constexpr int STG = (MI + NI) * TK * 256;          // one stage: MI A images, NI B images
+  constexpr int G = (MI + NI) * 8 / NW;              // 1 KB glds per wave per stage
+  static_assert(G * NW == (MI + NI) * 8, "stage split");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * TB, c0 = blockIdx.x * TB;
+  const int wm = w / WN, wn = w % WN;
+  const int m0 = blockIdx.y * TM, c0 = blockIdx.x * TN;
   const int z = blockIdx.z, z1 = z / p.Z2, z2 = z - z1 * p.Z2;
   const bf16_t* A = p.A + z1 * p.az1 + z2 * p.az2;
   const bf16_t* B = p.B + z1 * p.bz1 + z2 * p.bz2;
   const long rows = p.Ktot > 0 ? min((long)p.K, (long)p.Ktot - (long)z2 * p.K) : (long)p.K;
   const int nsteps = rows > 0 ? (int)((rows + TK - 1) / TK) : 0;
   const uint32_t sb = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)smem;
-  // stage s -> slot s % NST: wave w moves row groups 2w, 2w+1 (4 rows = 1 KB each) of A and of B;
-  // lane l fills physical chunk l % 16 of row 4*rg + l / 16, i.e. loads the logical chunk that the
-  // XOR swizzle puts there (LDS-DMA writes are lane-linear)
+  const bool bias = p.ones && (int)blockIdx.x == (int)(blockIdx.y % gridDim.x) && wn == 0;
+  // stage s -> slot s % NST: glds j of wave w moves 1 KB row group (w*G + j) % 8 (4 rows) of image
+  // (w*G + j) / 8; lane l fills physical chunk l % 16 of row 4*rg + l / 16, i.e. loads the logical
+  // chunk that the XOR swizzle puts there (LDS-DMA writes are lane-linear)
   auto issue = [&](int s) {
-    const uint32_t base = sb + (uint32_t)((s % NST) * STAGE);
+    const uint32_t base = sb + (uint32_t)((s % NST) * STG);
     const long r0 = (long)s * TK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int rg = 2 * w + i, row = rg * 4 + (lane >> 4), pc = lane & 15;
+    for (int j = 0; j < G; ++j) {
+      const int gi = w * G + j, im = gi >> 3, rg = gi & 7;
+      const int row = rg * 4 + (lane >> 4), pc = lane & 15;
       const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
       const long rr = r0 + row;
       const bool rok = rr < rows;
-      const int na = m0 + ch * 8;
-      const void* sa = (rok && na < p.M) ? (const void*)(A + rr * p.lda + na) : (const void*)&g_zero16;
-      glds16(sa, base + rg * 1024);
-      const int kb = c0 + ch * 8;
-      const void* sbp = (rok && kb < p.N) ? (const void*)(B + rr * p.ldb + kb)
-                                          : (rok && p.ones && kb == p.N) ? (const void*)&g_one16
-                                                                         : (const void*)&g_zero16;
-      glds16(sbp, base + TK * 256 + rg * 1024);
+      const void* src;
+      if (im < MI) {
+        const int na = m0 + im * TB + ch * 8;
+        src = (rok && na < p.M) ? (const void*)(A + rr * p.lda + na) : (const void*)&g_zero16;
+      } else {
+        const int kb = c0 + (im - MI) * TB + ch * 8;
+        src = (rok && kb < p.N) ? (const void*)(B + rr * p.ldb + kb) : (const void*)&g_zero16;
+      }
+      glds16(src, base + im * (TK * 256) + rg * 1024);
     }
   };
   f32x16 acc[2][2];
@@ -221,25 +236,36 @@ __global__ __launch_bounds__(256) void tn_glds_kernel(TnArgs p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  float bsum[2] = {0.0f, 0.0f};
+  const int ai = wm >> 1, acol = (wm & 1) * 64, bi = wn >> 1, bcol = (wn & 1) * 64;
   constexpr int D = NST - 1;
   for (int s = 0; s < D && s < nsteps; ++s) issue(s);
   for (int s = 0; s < nsteps; ++s) {
-    wait_ahead<4, D - 1>(min(D, nsteps - s) - 1);   // this wave's loads of stage s have landed
+    wait_ahead<G, D - 1>(min(D, nsteps - s) - 1);   // this wave's loads of stage s have landed
     bar();                                           // everyone's have; slot (s-1) % NST is free
     if (s + D < nsteps) issue(s + D);
-    const char* ia = smem + (s % NST) * STAGE;
-    const char* ib = ia + TK * 256;
+    const char* ia = smem + (s % NST) * STG + ai * (TK * 256);
+    const char* ib = smem + (s % NST) * STG + (MI + bi) * (TK * 256);
 #pragma unroll
     for (int ks = 0; ks < TK; ks += 16) {
       uint4 fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(ia, wm * 64 + i * 32, ks, lane);
+      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(ia, acol + i * 32, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = tr_frag(ib, wn * 64 + j * 32, ks, lane);
+      for (int j = 0; j < 2; ++j) fb[j] = tr_frag(ib, bcol + j * 32, ks, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[i], fb[j]);
+      if (bias) {   // lane l holds 8 frame rows of column (l & 31) of fragment i
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const uint32_t u[4] = {fa[i].x, fa[i].y, fa[i].z, fa[i].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            bsum[i] += __uint_as_float(u[e] << 16) + __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
     }
   }
   float* o = p.C + z1 * p.cz1 + z2 * p.cz2;
@@ -247,13 +273,32 @@ __global__ __launch_bounds__(256) void tn_glds_kernel(TnArgs p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int col = c0 + wn * 64 + j * 32 + (lane & 31);
+      const int col = c0 + bi * TB + bcol + j * 32 + (lane & 31);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * 64 + i * 32 + acc_row(e, lane);
+        const int row = m0 + ai * TB + acol + i * 32 + acc_row(e, lane);
         if (row < p.M && col < p.Nout) o[(long)row * p.ldc + col] = p.alpha * acc[i][j][e];
       }
     }
+  if (bias) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float t = bsum[i] + __shfl_xor(bsum[i], 32);
+      const int row = m0 + ai * TB + acol + i * 32 + lane;
+      if (lane < 32 && row < p.M) o[(long)row * p.ldc + p.N] = p.alpha * t;
+    }
+  }
+}
+
+// weight-gradient tile (CFM_TN_TILE = MI*10 + NI: 11, 21, 12, 22); the batched attention products
+// stay on 128x128
+int tn_tile() {
+  static const int t = [] {
+    const char* e = getenv("CFM_TN_TILE");
+    const int v = e ? atoi(e) : 11;
+    return (v == 11 || v == 21 || v == 12 || v == 22) ? v : 11;
+  }();
+  return t;
 }
 
 }  // namespace
@@ -270,7 +315,7 @@ bool bgemm_tn(const void* A, long lda, long az1, long az2, const void* B, long l
   p.C = C; p.ldc = ldc; p.cz1 = cz1; p.cz2 = cz2;
   p.M = M; p.N = N; p.Nout = N; p.K = K; p.Z2 = Z2; p.Ktot = Ktot; p.ones = 0; p.alpha = alpha;
   const dim3 grid((unsigned)((N + TB - 1) / TB), (unsigned)((M + TB - 1) / TB), (unsigned)Z), block(256);
-  cfm_launch(tn_glds_kernel, grid, block, 0, st, p);
+  cfm_launch((tn_glds_kernel<1, 1>), grid, block, 0, st, p);
   return true;
 }
 
@@ -278,19 +323,37 @@ bool wgrad_tn_supported(int dtype, int N, int K, long lda, long ldb) {
   return dtype == DT_BF16 && N % 8 == 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0;
 }
 
+int wgrad_tn_tiles(int N, int K, bool ones, int bfn) {
+  if (bfn == 0) {
+    const int t = tn_tile(), tm = TB * (t / 10), tn = TB * (t % 10);
+    return ((N + tm - 1) / tm) * ((K + tn - 1) / tn);
+  }
+  const int Kb = ones ? K + 4 : K;
+  return ((N + TB - 1) / TB) * ((Kb + TB - 1) / TB);
+}
+
+int wgrad_tn_blocks(int bfn) { return (bfn == 0 && tn_tile() != 11) ? 256 : 512; }
+
 void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bool ones, int bfn, Drop bdr, long rows,
               int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st) {
   if (N <= 0 || Kout <= 0) return;
   const dim3 grid((unsigned)((Kout + TB - 1) / TB), (unsigned)((N + TB - 1) / TB), (unsigned)S), block(256);
-  static const bool glds = [] { const char* e = getenv("CFM_WGRAD_GLDS"); return !e || atoi(e) != 0; }();
-  if (bfn == 0 && glds) {
+  if (bfn == 0) {
+    // bias (ones): written by the kernel at column K of the ldo-wide output, not as a ones column
     TnArgs p{};
     p.A = (const bf16_t*)A; p.lda = lda; p.az2 = chunk * lda;
     p.B = (const bf16_t*)B; p.ldb = ldb; p.bz2 = chunk * ldb;
     p.C = out; p.ldc = ldo; p.cz2 = split_stride;
-    p.M = N; p.N = K; p.Nout = Kout; p.K = (int)chunk; p.Z2 = S; p.Ktot = (int)rows; p.ones = ones ? 1 : 0;
+    p.M = N; p.N = K; p.Nout = std::min(K, Kout); p.K = (int)chunk; p.Z2 = S; p.Ktot = (int)rows; p.ones = ones ? 1 : 0;
     p.alpha = 1.0f;
-    cfm_launch(tn_glds_kernel, grid, block, 0, st, p);
+    const int t = tn_tile(), mi = t / 10, ni = t % 10;
+    const dim3 g2((unsigned)((K + TB * ni - 1) / (TB * ni)), (unsigned)((N + TB * mi - 1) / (TB * mi)), (unsigned)S);
+    switch (t) {
+      case 21: cfm_launch((tn_glds_kernel<2, 1>), g2, dim3(512), 0, st, p); break;
+      case 12: cfm_launch((tn_glds_kernel<1, 2>), g2, dim3(512), 0, st, p); break;
+      case 22: cfm_launch((tn_glds_kernel<2, 2>), g2, dim3(1024), 0, st, p); break;
+      default: cfm_launch((tn_glds_kernel<1, 1>), g2, dim3(256), 0, st, p); break;
+    }
     return;
   }
   if (bfn == 1)
