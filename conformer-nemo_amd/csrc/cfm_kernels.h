@@ -141,6 +141,17 @@ int set_gemm_tile_override(int tile);
 int set_gemm_probe(int probe);
 void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                const void* zero_page, hipStream_t st);
+// conv2's input gradient for one stride phase (pt, pf) of its input pixels (t1, f1) = (2i + pt, 2j + pf),
+// as an implicit GEMM over the (1 + pt) * (1 + pf) taps reaching the phase: rows (b, i, j), K = taps x C
+// read straight from dY2 (B, T2, F2, C) rows of `ld` elements; epi.mode must be EPI_SCALE_F32.
+struct TConvGeom {
+  const void* dY2;
+  long ld;
+  int B, T2, F2, C, pt, pf, nI, nJ;
+};
+bool gemm_tconv_supported(int dtype, int C);
+void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, const GemmEpi& epi,
+                const void* zero_page, hipStream_t st);
 // pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish in one launch (bf16, epi.mode = EPI_GLU_DW,
 // epi.utt_tp = T' <= 256, N = d, d % 64 == 0): one 256x128 tile per (utterance, 64 channels).
 bool gemm_glu_dw_supported(int dtype, int Tp, int d, int K);

@@ -199,6 +199,49 @@ struct ALoadConv {
   }
 };
 
+// Transposed-conv A operand (conv2's input gradient, one stride phase (pt, pf)): row m = (b, i, j) is
+// conv2 input pixel (t1, f1) = (2i + pt, 2j + pf); its K columns are the taps that reach that pixel,
+// tap = a * nf + c over nt = 1 + pt time taps and nf = 1 + pf frequency taps.  Time tap a = 0 is
+// kt = 1 (pt = 0, source t2 = i) or kt = 0 (pt = 1, source t2 = i + 1); a = 1 is kt = 2 (t2 = i);
+// frequency alike.  Column byte kb = tap * tapb + co * es reads dY2[b][t2][f2][co] (zero off-image).
+// tapb % 128 == 0 (host-checked), so a K-step never straddles two taps.
+template <int G>
+struct ALoadTConv {
+  static constexpr bool kConv = false;
+  const char* dY; long ldb; int T2, F2, nI, nJ, pt, pf; long tapb; int M; const char* zero;
+  struct State { const char* base[G]; uint32_t valid[G]; };
+  CFM_DEV void shift_k(long) {}   // never split
+  CFM_DEV void prepare(State& s, int m0, const int* rows) const {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int m = m0 + rows[i];
+      uint32_t v = 0;
+      const char* base = nullptr;
+      if (m < M) {
+        const int j = m % nJ, bi = m / nJ;
+        const int ii = bi % nI, b = bi / nI;
+        base = dY + ((long)(b * T2 + ii) * F2 + j) * ldb;
+        const int nf = 1 + pf;
+        for (int a = 0; a <= pt; ++a)
+          for (int c = 0; c < nf; ++c) {
+            const int dt = (pt && a == 0) ? 1 : 0, df = (pf && c == 0) ? 1 : 0;
+            if (ii + dt < T2 && j + df < F2) v |= 1u << (a * nf + c);
+          }
+      }
+      s.base[i] = base;
+      s.valid[i] = v;
+    }
+  }
+  CFM_DEV const void* src(const State& s, int i, long kb0, int lo) const {
+    const int k0 = __builtin_amdgcn_readfirstlane((int)kb0);
+    const int tap = __builtin_amdgcn_readfirstlane(k0 / (int)tapb);
+    if (tap >= 4 || !((s.valid[i] >> tap) & 1u)) return zero;
+    const int nf = 1 + pf, a = tap / nf, c = tap - a * nf;
+    const int dt = (pt && a == 0) ? 1 : 0, df = (pf && c == 0) ? 1 : 0;
+    return s.base[i] + ((long)dt * F2 + df) * ldb + (long)(k0 - tap * (int)tapb) + lo;
+  }
+};
+
 thread_local int g_splits = 1;
 constexpr int LN_PRE = 4;   // folded-LayerNorm granule partials prefetched per row (d <= 512 fully)   // grid.y of the next split-K launch (gemm_splitk)
 
@@ -1246,6 +1289,44 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   int tile = pick_tile(dtype, M, N, epi.mode, true);
   if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
   else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
+}
+
+bool gemm_tconv_supported(int dtype, int C) { return C > 0 && ((long)C * dtype_size(dtype)) % 128 == 0; }
+
+// One stride phase of conv2's input gradient (the transposed conv, cfm_kernels.h TConvGeom): fp32
+// rows of the phase-major dY1 image.  bf16 runs on the 256x256 tile (CFM_TCONV_TILE=14: 128x128 K-group).
+void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, const GemmEpi& epi,
+                const void* zero_page, hipStream_t st) {
+  const int M = g.B * g.nI * g.nJ;
+  if (M <= 0) return;
+  if (!gemm_tconv_supported(dtype, g.C) || epi.mode != EPI_SCALE_F32)
+    fail(CFM_ERR_UNSUPPORTED, "gemm_tconv: C * element size % 128 == 0 and an fp32 output only");
+  const int es = dtype_size(dtype);
+  GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
+  auto fill = [&](auto& al) {
+    al.dY = (const char*)g.dY2; al.ldb = g.ld * es; al.T2 = g.T2; al.F2 = g.F2; al.nI = g.nI; al.nJ = g.nJ;
+    al.pt = g.pt; al.pf = g.pf; al.tapb = (long)g.C * es; al.M = M; al.zero = (const char*)zero_page;
+  };
+  auto go = [&](auto kern, auto& al, int bm, int bn, int nt) {
+    fill(al);
+    p.Mtiles = (M + bm - 1) / bm;
+    p.Ntiles = (N + bn - 1) / bn;
+    cfm_launch(kern, dim3(p.Mtiles * p.Ntiles), dim3(nt), 0, st, p, al);
+  };
+  static const int tile = [] { const char* e = getenv("CFM_TCONV_TILE"); return e ? atoi(e) : 11; }();
+  if (dtype == DT_BF16 && tile == 14) {
+    using TL = T128x128k4;
+    ALoadTConv<TL::GA> al;
+    go(gemm_kernel<bf16_t, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+  } else if (dtype == DT_BF16) {
+    using TL = T256x256w;
+    ALoadTConv<TL::GA> al;
+    go(gemm_kernel<bf16_t, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+  } else {
+    using TL = T128x128;
+    ALoadTConv<TL::GA> al;
+    go(gemm_kernel<float, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+  }
 }
 
 }  // namespace cfm

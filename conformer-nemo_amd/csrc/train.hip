@@ -815,10 +815,50 @@ __global__ __launch_bounds__(256) void im2col_t_vec_kernel(const T* __restrict__
   }
 }
 
+// Packed operand of one stride phase (pt, pf) of conv2's input gradient (gemm_tconv):
+//   dst[ci][tap * C + co] = W2[co][ci][kt][kf], tap = a * (1 + pf) + c over the phase's taps, with
+//   kt = pt ? (a == 0 ? 0 : 2) : 1 and kf = pf ? (c == 0 ? 0 : 2) : 1 (zero past the taps / rows).
+template <typename T>
+__global__ __launch_bounds__(256) void tconv_wpack_kernel(const float* __restrict__ w2, int C, int pt, int pf,
+                                                          T* __restrict__ dst, int Kp, int rows_pad) {
+  const long n = (long)rows_pad * Kp;
+  const int nf = 1 + pf, ntap = (1 + pt) * nf;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / Kp), q = (int)(i - (long)r * Kp);
+    float v = 0.0f;
+    if (r < C && q < ntap * C) {
+      const int tap = q / C, co = q - tap * C, a = tap / nf, c = tap - a * nf;
+      const int kt = pt ? (a == 0 ? 0 : 2) : 1, kf = pf ? (c == 0 ? 0 : 2) : 1;
+      v = w2[((long)co * C + r) * 9 + kt * 3 + kf];
+    }
+    st_f<T>(dst + i, v);
+  }
+}
+
+// Phase-major dY1 image written by the four gemm_tconv launches: phase ph = 2*pt + pf holds the
+// pixels (2i + pt, 2j + pf) as rows ((b * nI[pt] + i) * nJ[pf] + j), phases stacked in ph order.
+struct PhaseRows {
+  long base[4];
+  int nI[2], nJ[2];
+  __host__ __device__ PhaseRows(int B, int T1, int F1) {
+    nI[0] = (T1 + 1) / 2; nI[1] = T1 / 2;
+    nJ[0] = (F1 + 1) / 2; nJ[1] = F1 / 2;
+    long o = 0;
+    for (int ph = 0; ph < 4; ++ph) {
+      base[ph] = o;
+      o += (long)B * nI[ph >> 1] * nJ[ph & 1];
+    }
+  }
+};
+
 // conv1 weight gradient, stage 1: partial[chunk][c][tap] = sum over the chunk's (b, t1) rows and all
-// f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T))
+// f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T)).
+// PH: dY1 is the unmasked phase-major image (PhaseRows) and conv1's ReLU mask [X1 > 0] is applied
+// here; otherwise dY1 is (B, T1, F1, C), already masked.
+template <typename TX, bool PH>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int F, int T, int T1, int F1,
-                                                          int C, const float* __restrict__ dy1, int B, int R,
+                                                          int C, const float* __restrict__ dy1,
+                                                          const TX* __restrict__ x1, int B, int R,
                                                           float* __restrict__ partial, float* __restrict__ partial_b) {
   __shared__ float xs[3][264];
   const int chunk = blockIdx.x;
@@ -837,8 +877,22 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
     __syncthreads();
     if (c < C) {
       const float* g = dy1 + ((long)bt * F1) * C + c;
+      long prow[2] = {0, 0};
+      if constexpr (PH) {
+        const PhaseRows pr(B, T1, F1);
+        const int pt = t1 & 1;
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf)
+          prow[pf] = pr.base[2 * pt + pf] + ((long)b * pr.nI[pt] + (t1 >> 1)) * pr.nJ[pf];
+      }
       for (int f1 = 0; f1 < F1; ++f1) {
-        const float gv = g[(long)f1 * C];
+        float gv;
+        if constexpr (PH) {
+          gv = dy1[(prow[f1 & 1] + (f1 >> 1)) * C + c];
+          if (!(ld_f<TX>(x1 + ((long)bt * F1 + f1) * C + c) > 0.0f)) gv = 0.0f;
+        } else {
+          gv = g[(long)f1 * C];
+        }
         accb += gv;
 #pragma unroll
         for (int kt = 0; kt < 3; ++kt)
@@ -1063,7 +1117,8 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   const long KT = np(std::max({dff, d, (long)g.F2 * g.C}) + 4);
   w.pbt = a.take(KT * g.Mq * es);                                      // x^T [Kpad][Mp]
   w.wt = a.take(std::max({np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(3 * d), np(d) * kp(2 * d),
-                          np((long)g.F2 * g.C) * kp(d), np(9L * g.C) * kp(g.C)}) * es);
+                          np((long)g.F2 * g.C) * kp(d), np(9L * g.C) * kp(g.C),
+                          np(g.C) * (kp(g.C) + 2 * kp(2L * g.C) + kp(4L * g.C))}) * es);   // + tconv phases
   // a layer's transposed weights for its dgrad GEMMs, packed in one launch (WT_* order)
   const long wtl_sz[7] = {np(dff) * kp(d), np(d) * kp(dff), np(dff) * kp(d), np(d) * kp(dff), np(d) * kp(d),
                           np(d) * kp(2 * d), np(d) * kp(d)};
@@ -1899,7 +1954,46 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     S.wgrad(pat, S.W_(S.wl.i2c), g.M2p, g.C, 9 * g.C, g.M2, tmp, Gp(S.i_c2b));
     if (Gp(S.i_c2w)) S.perm(tmp, 5, Gp(S.i_c2w), true, 9L * g.C, g.C, 9 * g.C);
   }
-  if (need_c1) {   // dCol = dY2 . W2mat, col2im + conv1 ReLU mask, then conv1's weight/bias gradient
+  static const bool tconv_on = [] { const char* e = getenv("CFM_TCONV"); return e ? atoi(e) != 0 : true; }();
+  if (need_c1 && tconv_on && gemm_tconv_supported(dt, g.C)) {
+    // dY1 = conv2's transposed conv as four stride-phase implicit GEMMs straight from dY2 (no dCol
+    // image, no col2im): phase (pt, pf) of the input pixels gathers the (1+pt)(1+pf) taps reaching it.
+    // The phase-major fp32 result is masked by conv1's ReLU inside conv1's weight-gradient kernel.
+    S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
+    float* dy1 = S.W_<float>(S.wl.dy1);
+    const PhaseRows pr(g.B, g.T1, g.F1);
+    char* wp = (char*)wt;
+    for (int ph = 0; ph < 4; ++ph) {
+      const int pt = ph >> 1, pf = ph & 1, ntap = (1 + pt) * (1 + pf);
+      const int Kp = S.kpad((long)ntap * g.C), rp = S.npad(g.C);
+      const long n = (long)rp * Kp;
+      if (dt == DT_F32)
+        cfm_launch(tconv_wpack_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, S.prm(S.i_c2w), g.C, pt, pf,
+                   (float*)wp, Kp, rp);
+      else
+        cfm_launch(tconv_wpack_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.prm(S.i_c2w), g.C, pt, pf,
+                   (bf16_t*)wp, Kp, rp);
+      GemmEpi e = S.epi(EPI_SCALE_F32, nullptr);
+      e.X = dy1 + pr.base[ph] * g.C;
+      e.ldx = g.C;
+      const TConvGeom tg{pa, S.kpad(g.C), g.B, g.T2, g.F2, g.C, pt, pf, pr.nI[pt], pr.nJ[pf]};
+      gemm_tconv(dt, tg, wp, Kp, g.C, e, h->zero_page, st);
+      wp += n * es;
+    }
+    const int rows = g.B * g.T1, R = 8, nch = (rows + R - 1) / R;
+    float* part = S.W_<float>(S.wl.c1part);
+    float* part_b = part + (long)nch * 9 * g.C;
+    if (dt == DT_F32)
+      cfm_launch((conv1_wgrad_kernel<float, true>), dim3(nch, (g.C + 255) / 256), dim3(256), 0, st,
+                 S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const float*)dy1,
+                 S.T_<const float>(S.tp.X1), g.B, R, part, part_b);
+    else
+      cfm_launch((conv1_wgrad_kernel<bf16_t, true>), dim3(nch, (g.C + 255) / 256), dim3(256), 0, st,
+                 S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const float*)dy1,
+                 S.T_<const bf16_t>(S.tp.X1), g.B, R, part, part_b);
+    if (Gp(S.i_c1w)) colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
+    if (Gp(S.i_c1b)) colred(part_b, nullptr, nullptr, g.C, nch, g.C, 0, 1.0f, Gp(S.i_c1b), 0, red, st);
+  } else if (need_c1) {   // dCol = dY2 . W2mat, col2im + conv1 ReLU mask, then conv1's weight/bias gradient
     S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
     S.perm(S.prm(S.i_c2w), 3, wt, false, S.kpad(g.C), S.npad(9L * g.C), S.kpad(g.C));
     GemmEpi e = S.epi(EPI_STORE, nullptr);
@@ -1924,8 +2018,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       const int rows = g.B * g.T1, R = 8, nch = (rows + R - 1) / R;
       float* part = S.W_<float>(S.wl.c1part);
       float* part_b = part + (long)nch * 9 * g.C;
-      cfm_launch(conv1_wgrad_kernel, dim3(nch, (g.C + 255) / 256), dim3(256), 0, st, S.T_<const float>(S.tp.xin), g.F,
-                 g.T, g.T1, g.F1, g.C, (const float*)dy1, g.B, R, part, part_b);
+      cfm_launch((conv1_wgrad_kernel<float, false>), dim3(nch, (g.C + 255) / 256), dim3(256), 0, st,
+                 S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const float*)dy1, (const float*)nullptr,
+                 g.B, R, part, part_b);
       if (Gp(S.i_c1w)) colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
       if (Gp(S.i_c1b)) colred(part_b, nullptr, nullptr, g.C, nch, g.C, 0, 1.0f, Gp(S.i_c1b), 0, red, st);
     }
