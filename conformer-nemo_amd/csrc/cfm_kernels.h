@@ -143,7 +143,7 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
                const void* zero_page, hipStream_t st);
 // conv2's input gradient for one stride phase (pt, pf) of its input pixels (t1, f1) = (2i + pt, 2j + pf),
 // as an implicit GEMM over the (1 + pt) * (1 + pf) taps reaching the phase: rows (b, i, j), K = taps x C
-// read straight from dY2 (B, T2, F2, C) rows of `ld` elements; epi.mode must be EPI_SCALE_F32.
+// read straight from dY2 (B, T2, F2, C) rows of `ld` elements; epi.mode must be EPI_STORE.
 struct TConvGeom {
   const void* dY2;
   long ld;

@@ -1293,14 +1293,14 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
 
 bool gemm_tconv_supported(int dtype, int C) { return C > 0 && ((long)C * dtype_size(dtype)) % 128 == 0; }
 
-// One stride phase of conv2's input gradient (the transposed conv, cfm_kernels.h TConvGeom): fp32
-// rows of the phase-major dY1 image.  bf16 runs on the 256x256 tile (CFM_TCONV_TILE=14: 128x128 K-group).
+// One stride phase of conv2's input gradient (the transposed conv, cfm_kernels.h TConvGeom): rows
+// of the phase-major dY1 image in the compute type (EPI_STORE).  bf16 runs on the 256x256 tile (CFM_TCONV_TILE=14: 128x128 K-group).
 void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                 const void* zero_page, hipStream_t st) {
   const int M = g.B * g.nI * g.nJ;
   if (M <= 0) return;
-  if (!gemm_tconv_supported(dtype, g.C) || epi.mode != EPI_SCALE_F32)
-    fail(CFM_ERR_UNSUPPORTED, "gemm_tconv: C * element size % 128 == 0 and an fp32 output only");
+  if (!gemm_tconv_supported(dtype, g.C) || epi.mode != EPI_STORE)
+    fail(CFM_ERR_UNSUPPORTED, "gemm_tconv: C * element size % 128 == 0 and a plain store only");
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   auto fill = [&](auto& al) {
@@ -1317,15 +1317,15 @@ void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, 
   if (dtype == DT_BF16 && tile == 14) {
     using TL = T128x128k4;
     ALoadTConv<TL::GA> al;
-    go(gemm_kernel<bf16_t, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+    go(gemm_kernel<bf16_t, EPI_STORE, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
   } else if (dtype == DT_BF16) {
     using TL = T256x256w;
     ALoadTConv<TL::GA> al;
-    go(gemm_kernel<bf16_t, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+    go(gemm_kernel<bf16_t, EPI_STORE, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
   } else {
     using TL = T128x128;
     ALoadTConv<TL::GA> al;
-    go(gemm_kernel<float, EPI_SCALE_F32, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
+    go(gemm_kernel<float, EPI_STORE, TL, ALoadTConv<TL::GA>>, al, TL::BM, TL::BN, TL::NT);
   }
 }
 

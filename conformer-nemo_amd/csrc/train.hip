@@ -853,11 +853,11 @@ struct PhaseRows {
 
 // conv1 weight gradient, stage 1: partial[chunk][c][tap] = sum over the chunk's (b, t1) rows and all
 // f1 of dY1[b,t1,f1,c] * xpad[b, f = 2*f1 - 1 + kf, t = 2*t1 - 1 + kt]  (x is (B, F, T)).
-// PH: dY1 is the unmasked phase-major image (PhaseRows) and conv1's ReLU mask [X1 > 0] is applied
-// here; otherwise dY1 is (B, T1, F1, C), already masked.
+// PH: dY1 is the unmasked phase-major image (PhaseRows, compute type) and conv1's ReLU mask
+// [X1 > 0] is applied here; otherwise dY1 is (B, T1, F1, C) fp32, already masked.
 template <typename TX, bool PH>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ x, int F, int T, int T1, int F1,
-                                                          int C, const float* __restrict__ dy1,
+                                                          int C, const TX* __restrict__ dy1,
                                                           const TX* __restrict__ x1, int B, int R,
                                                           float* __restrict__ partial, float* __restrict__ partial_b) {
   __shared__ float xs[3][264];
@@ -876,7 +876,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
     }
     __syncthreads();
     if (c < C) {
-      const float* g = dy1 + ((long)bt * F1) * C + c;
+      const TX* g = dy1 + ((long)bt * F1) * C + c;
       long prow[2] = {0, 0};
       if constexpr (PH) {
         const PhaseRows pr(B, T1, F1);
@@ -888,10 +888,10 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
       for (int f1 = 0; f1 < F1; ++f1) {
         float gv;
         if constexpr (PH) {
-          gv = dy1[(prow[f1 & 1] + (f1 >> 1)) * C + c];
+          gv = ld_f<TX>(dy1 + (prow[f1 & 1] + (f1 >> 1)) * C + c);
           if (!(ld_f<TX>(x1 + ((long)bt * F1 + f1) * C + c) > 0.0f)) gv = 0.0f;
         } else {
-          gv = g[(long)f1 * C];
+          gv = ld_f<TX>(g + (long)f1 * C);
         }
         accb += gv;
 #pragma unroll
@@ -1958,9 +1958,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   if (need_c1 && tconv_on && gemm_tconv_supported(dt, g.C)) {
     // dY1 = conv2's transposed conv as four stride-phase implicit GEMMs straight from dY2 (no dCol
     // image, no col2im): phase (pt, pf) of the input pixels gathers the (1+pt)(1+pf) taps reaching it.
-    // The phase-major fp32 result is masked by conv1's ReLU inside conv1's weight-gradient kernel.
+    // The phase-major result (compute type) is masked by conv1's ReLU inside conv1's weight-gradient kernel.
     S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
-    float* dy1 = S.W_<float>(S.wl.dy1);
+    char* dy1 = (char*)S.W_<float>(S.wl.dy1);
     const PhaseRows pr(g.B, g.T1, g.F1);
     char* wp = (char*)wt;
     for (int ph = 0; ph < 4; ++ph) {
@@ -1973,9 +1973,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       else
         cfm_launch(tconv_wpack_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, st, S.prm(S.i_c2w), g.C, pt, pf,
                    (bf16_t*)wp, Kp, rp);
-      GemmEpi e = S.epi(EPI_SCALE_F32, nullptr);
-      e.X = dy1 + pr.base[ph] * g.C;
-      e.ldx = g.C;
+      GemmEpi e = S.epi(EPI_STORE, nullptr);
+      e.C = dy1 + pr.base[ph] * g.C * es;
+      e.ldc = g.C;
       const TConvGeom tg{pa, S.kpad(g.C), g.B, g.T2, g.F2, g.C, pt, pf, pr.nI[pt], pr.nJ[pf]};
       gemm_tconv(dt, tg, wp, Kp, g.C, e, h->zero_page, st);
       wp += n * es;
@@ -1989,7 +1989,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
                  S.T_<const float>(S.tp.X1), g.B, R, part, part_b);
     else
       cfm_launch((conv1_wgrad_kernel<bf16_t, true>), dim3(nch, (g.C + 255) / 256), dim3(256), 0, st,
-                 S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const float*)dy1,
+                 S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const bf16_t*)dy1,
                  S.T_<const bf16_t>(S.tp.X1), g.B, R, part, part_b);
     if (Gp(S.i_c1w)) colred(part, nullptr, nullptr, 9L * g.C, nch, 9 * g.C, 0, 1.0f, Gp(S.i_c1w), 0, red, st);
     if (Gp(S.i_c1b)) colred(part_b, nullptr, nullptr, g.C, nch, g.C, 0, 1.0f, Gp(S.i_c1b), 0, red, st);
