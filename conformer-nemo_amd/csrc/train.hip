@@ -433,6 +433,36 @@ __global__ __launch_bounds__(256) void slab_sum_wb_kernel(const float* __restric
   }
 }
 
+// slab_sum_wb_kernel for K % 4 == 0 and a 16-byte aligned w: one float4 of a row per thread step
+// (32-bit index math; the bias column K opens the row's last float4)
+__global__ __launch_bounds__(256) void slab_sum_wb4_kernel(const float* __restrict__ part, int S, int N, int K,
+                                                           float* __restrict__ w, float* __restrict__ b) {
+  const int q4 = (K + 4) >> 2;
+  const int n4 = N * q4;
+  const long n = (long)N * (K + 4);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+    const int r = i / q4, k = 4 * (i - r * q4);
+    float4 a = ((const float4*)part)[i];
+    for (int s2 = 1; s2 < S; ++s2) {
+      const float4 c = ((const float4*)(part + (long)s2 * n))[i];
+      a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+    }
+    if (k < K) {
+      if (w) *(float4*)(w + (long)r * K + k) = a;
+    } else if (b) {
+      b[r] = a.x;
+    }
+  }
+}
+void slab_sum_wb(const float* part, int S, int N, int K, float* w, float* b, hipStream_t st) {
+  if (K % 4 == 0 && ((uintptr_t)w & 15) == 0 && (long)N * (K + 4) / 4 < (1L << 30)) {
+    const long n4 = (long)N * (K + 4) / 4;
+    cfm_launch(slab_sum_wb4_kernel, dim3(ew_grid(n4)), dim3(256), 0, st, part, S, N, K, w, b);
+  } else {
+    cfm_launch(slab_sum_wb_kernel, dim3(ew_grid((long)N * (K + 4))), dim3(256), 0, st, part, S, N, K, w, b);
+  }
+}
+
 size_t colred_ws(long M, long N) { return (size_t)((M + kRedRows - 1) / kRedRows) * N * 4; }
 void colred(const float* src, const float* y, const float* mean, long ld, int M, int N, int f, float alpha, float* out,
             int accumulate, float* ws, hipStream_t st) {
@@ -908,6 +938,71 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
   }
 }
 
+// conv1_wgrad_kernel<TX, true> for C % 8 == 0: a thread owns 8 consecutive channels (16-byte loads of
+// the phase-major dY1 and of the X1 mask, 9 x 8 accumulators), a 64-thread block 512 channels of R
+// (b, t1) rows.  Same per-channel summation order as the scalar kernel (bitwise equal partials).
+template <typename TX>
+__global__ __launch_bounds__(64) void conv1_wgrad_ph8_kernel(const float* __restrict__ x, int F, int T, int T1,
+                                                             int F1, int C, const TX* __restrict__ dy1,
+                                                             const TX* __restrict__ x1, int B, int R,
+                                                             float* __restrict__ partial, float* __restrict__ partial_b) {
+  __shared__ float xs[3][264];
+  const int chunk = blockIdx.x;
+  const int c0 = (blockIdx.y * 64 + threadIdx.x) * 8;
+  float acc[9][8], accb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    accb[e] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k][e] = 0.0f;
+  }
+  const PhaseRows pr(B, T1, F1);
+  const int r0 = chunk * R, r1 = min(B * T1, r0 + R);
+  for (int bt = r0; bt < r1; ++bt) {
+    const int b = bt / T1, t1 = bt - b * T1;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * (F + 2); i += 64) {
+      const int kt = i / (F + 2), fp = i - kt * (F + 2), f = fp - 1, t = 2 * t1 - 1 + kt;
+      xs[kt][fp] = (f >= 0 && f < F && t >= 0 && t < T) ? x[((long)b * F + f) * T + t] : 0.0f;
+    }
+    __syncthreads();
+    if (c0 < C) {
+      const int pt = t1 & 1;
+      long prow[2];
+#pragma unroll
+      for (int pf = 0; pf < 2; ++pf)
+        prow[pf] = pr.base[2 * pt + pf] + ((long)b * pr.nI[pt] + (t1 >> 1)) * pr.nJ[pf];
+      for (int f1 = 0; f1 < F1; ++f1) {
+        float gv[8], mv[8];
+        ld8<TX>(dy1 + (prow[f1 & 1] + (f1 >> 1)) * C + c0, gv);
+        ld8<TX>(x1 + ((long)bt * F1 + f1) * C + c0, mv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (!(mv[e] > 0.0f)) gv[e] = 0.0f;
+          accb[e] += gv[e];
+        }
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int kf = 0; kf < 3; ++kf) {
+            const float xv = xs[kt][2 * f1 + kf];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[kt * 3 + kf][e] = fmaf(gv[e], xv, acc[kt * 3 + kf][e]);
+          }
+      }
+    }
+  }
+  if (c0 < C) {
+    float* pp = partial + ((long)chunk * C + c0) * 9;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) pp[e * 9 + k] = acc[k][e];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) partial_b[(long)chunk * C + c0 + e] = accb[e];
+  }
+}
+
 // (B, T', d) fp32 rows <-> (B, d, T') fp32
 __global__ __launch_bounds__(256) void btd_transpose_kernel(const float* __restrict__ src, int Tp, int d, int to_bdt,
                                                             float* __restrict__ dst) {
@@ -1354,7 +1449,7 @@ struct Step {
     else gemm_splitk(g.dt, At, ldm, N, (int)rows, Bt, ldm, Kb, S, chunk, e, (long)N * Kb, h->zero_page, st);
     const long n = (long)N * Kb;
     if (bias)
-      cfm_launch(slab_sum_wb_kernel, dim3(ew_grid(n)), dim3(256), 0, st, (const float*)part, S, N, K, out, bias);
+      slab_sum_wb(part, S, N, K, out, bias, st);
     else
       cfm_launch(slab_sum_kernel, dim3(ew_grid(n / 4 + 1)), dim3(256), 0, st, (const float*)part, S, n, out);
   }
@@ -1377,7 +1472,7 @@ struct Step {
     wgrad_tn(A, lda, N, B, ldb, K, bias != nullptr, bfn, bdr, rows, (int)S, chunk, part, Kb, Kb, (long)N * Kb, st);
     const long n = (long)N * Kb;
     if (bias)
-      cfm_launch(slab_sum_wb_kernel, dim3(ew_grid(n)), dim3(256), 0, st, (const float*)part, (int)S, N, K, out, bias);
+      slab_sum_wb(part, (int)S, N, K, out, bias, st);
     else
       cfm_launch(slab_sum_kernel, dim3(ew_grid(n / 4 + 1)), dim3(256), 0, st, (const float*)part, (int)S, n, out);
   }
@@ -1983,7 +2078,14 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     const int rows = g.B * g.T1, R = 8, nch = (rows + R - 1) / R;
     float* part = S.W_<float>(S.wl.c1part);
     float* part_b = part + (long)nch * 9 * g.C;
-    if (dt == DT_F32)
+    const dim3 grid8(nch, (g.C / 8 + 63) / 64);
+    if (g.C % 8 == 0 && dt == DT_F32)
+      cfm_launch(conv1_wgrad_ph8_kernel<float>, grid8, dim3(64), 0, st, S.T_<const float>(S.tp.xin), g.F, g.T, g.T1,
+                 g.F1, g.C, (const float*)dy1, S.T_<const float>(S.tp.X1), g.B, R, part, part_b);
+    else if (g.C % 8 == 0)
+      cfm_launch(conv1_wgrad_ph8_kernel<bf16_t>, grid8, dim3(64), 0, st, S.T_<const float>(S.tp.xin), g.F, g.T, g.T1,
+                 g.F1, g.C, (const bf16_t*)dy1, S.T_<const bf16_t>(S.tp.X1), g.B, R, part, part_b);
+    else if (dt == DT_F32)
       cfm_launch((conv1_wgrad_kernel<float, true>), dim3(nch, (g.C + 255) / 256), dim3(256), 0, st,
                  S.T_<const float>(S.tp.xin), g.F, g.T, g.T1, g.F1, g.C, (const float*)dy1,
                  S.T_<const float>(S.tp.X1), g.B, R, part, part_b);
