@@ -409,6 +409,54 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
 #pragma unroll
     for (int s = 0; s < NS; ++s) mfma_slab<bf16_t>(sc[c], aqu[s], *(const uint4*)(kp + 16 * s));
   }
+  // dctx fragments (fp32 -> bf16) and the dP tiles are independent of the softmax: issue them first
+  uint4 adc[NS];
+  {
+    const float* dr = dctx + rowq * ld_dctx + h * dkp + kh;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float4 x0 = *(const float4*)(dr + 16 * s), x1 = *(const float4*)(dr + 16 * s + 4);
+      const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      adc[s] = Vec16<bf16_t>::from_f32(f);
+    }
+  }
+  // V rows of the block's keys [0, 64 nw) into LDS (row pitch dkp + 8 elements; zeros past Tpad),
+  // transposed from the V^T image: a job reads 8 keys of channels 2q and 2q + 1 (two 16-byte loads)
+  // and writes 8 dwords (one channel pair of one key each); consecutive lanes take consecutive
+  // channel pairs, so each ds_write_b32 covers consecutive dwords of one key row.  The dP fragments
+  // are then one 16-byte LDS read per slab instead of eight 2-byte global gathers.  The image lives
+  // in the (not yet written) BD space.
+  const int vpitch = dkp + 8;
+  bf16_t* Vs = (bf16_t*)bd_all;
+  {
+    const int npair = dkp / 2, nkc = 8 * nw;   // channel pairs, 8-key chunks of the 64 nw keys
+    const bf16_t* vt = Vt + (long)bh * vt_rows * Tpad;
+    for (int job = threadIdx.x; job < npair * nkc; job += blockDim.x) {
+      const int q = job % npair, k0 = 8 * (job / npair);
+      uint4 a = make_uint4(0, 0, 0, 0), c = make_uint4(0, 0, 0, 0);
+      if (k0 + 8 <= Tpad) {
+        a = *(const uint4*)(vt + (long)(2 * q) * Tpad + k0);
+        c = *(const uint4*)(vt + (long)(2 * q + 1) * Tpad + k0);
+      }
+      const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wc[4] = {c.x, c.y, c.z, c.w};
+      uint32_t* dst = (uint32_t*)(Vs + (long)k0 * vpitch) + q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dst[(2 * e) * (vpitch / 2)] = (wa[e] & 0xffffu) | (wc[e] << 16);
+        dst[(2 * e + 1) * (vpitch / 2)] = (wa[e] >> 16) | (wc[e] & 0xffff0000u);
+      }
+    }
+  }
+  __syncthreads();
+  f32x16 dp[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const bf16_t* vr = Vs + (long)(64 * w + 32 * c + l32) * vpitch + kh;
+    dp[c] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mfma_slab<bf16_t>(dp[c], adc[s], *(const uint4*)(vr + 16 * s));
+  }
+  __syncthreads();   // every wave has read its V fragments: the BD images may overwrite them
   // BD for positions rbase .. rbase + 95 (every position a row of this wave's keys can touch)
   float* bw = bd_all + w * 32 * BDP;
   const int rbase = Tp - 1 - (i0 + 31) + 64 * w;
@@ -421,32 +469,6 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
     for (int s = 0; s < NS; ++s) mfma_slab<bf16_t>(a, aqv[s], *(const uint4*)(pp + 16 * s));
 #pragma unroll
     for (int e = 0; e < 16; ++e) bw[acc_row(e, lane) * BDP + 32 * t + l32] = a[e];
-  }
-  // dctx fragments (fp32 -> bf16) and the dP tiles are independent of the softmax: issue them first
-  uint4 adc[NS];
-  {
-    const float* dr = dctx + rowq * ld_dctx + h * dkp + kh;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float4 x0 = *(const float4*)(dr + 16 * s), x1 = *(const float4*)(dr + 16 * s + 4);
-      const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      adc[s] = Vec16<bf16_t>::from_f32(f);
-    }
-  }
-  f32x16 dp[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int j = min(64 * w + 32 * c + l32, Tpad - 1);
-    const bf16_t* vp = Vt + (long)bh * vt_rows * Tpad + j;
-    dp[c] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      uint32_t u[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        u[e] = (uint32_t)vp[(long)(16 * s + kh + 2 * e) * Tpad] | ((uint32_t)vp[(long)(16 * s + kh + 2 * e + 1) * Tpad] << 16);
-      mfma_slab<bf16_t>(dp[c], adc[s], make_uint4(u[0], u[1], u[2], u[3]));
-    }
   }
   __syncthreads();
   // logits (log2 units) with the rel_shift, pad and context-window mask
@@ -616,11 +638,12 @@ void rel_pos_attention_backward(int dt, const void* qk, long ldqk, const void* V
   (void)es;
   // bf16: one fused launch produces P, dS and G (bf16) for the consumer GEMMs below
   const bool fused = dt == DT_BF16 && Tp <= 512 && dk % 16 == 0 && dk <= 128 && dkp == dk && ld_dctx % 4 == 0 &&
+                     Tpad % 8 == 0 && ((uintptr_t)Vt % 16) == 0 &&
                      ((uintptr_t)dctx % 16) == 0 && attn_bwd_fused_enabled();
   const int opS = fused ? OP_CT : OP_F32;    // storage of the P / dS / G images
   if (fused) {
     const int nw = (Tp + 63) / 64, nq = (Tp + 31) / 32;
-    const size_t lds = (size_t)nw * 32 * 97 * sizeof(float);
+    const size_t lds = std::max((size_t)nw * 32 * 97 * sizeof(float), (size_t)nw * 64 * (dkp + 8) * sizeof(bf16_t));
     const dim3 grid((unsigned)(nq * Z)), block(64 * nw);
     const bf16_t* q16 = (const bf16_t*)qk;
     bf16_t *P16 = (bf16_t*)S, *dS16 = (bf16_t*)dP, *G16 = (bf16_t*)BD;
