@@ -141,6 +141,33 @@ __global__ __launch_bounds__(256) void tpack_kernel(const Tin* __restrict__ src,
                         rows_pad, cols_pad, ones_row, src_vec, dst_vec);
 }
 
+// Non-transposed fp32 -> bf16 pack (no LDS tile): dst[i][8q .. 8q+7] = scale * src[i][...],
+// zero outside src; rows of cp elements (cp % 8 == 0), 16-byte aligned rows on both sides.
+__global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, long src_ld, int rows, int cols,
+                                                        float scale, bf16_t* __restrict__ dst, long dst_ld, int rp,
+                                                        int cp) {
+  const int q8 = cp >> 3;
+  const long n = (long)rp * q8;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < n; t += (long)gridDim.x * 256) {
+    const int i = (int)(t / q8), j = 8 * (int)(t - (long)i * q8);
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (i < rows) {
+      const float* sp = src + (long)i * src_ld + j;
+      if (j + 8 <= cols) {
+        const float4 a = *(const float4*)sp, b = *(const float4*)(sp + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (j + e < cols) v[e] = sp[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= scale;
+    }
+    *(uint4*)(dst + (long)i * dst_ld + j) = Vec16<bf16_t>::from_f32(v);
+  }
+}
+
 // Both packs of a dense fp32 output gradient dy (rows x cols) from one read: dA = dy in the compute
 // type ([rpA][ldA], the dgrad GEMM's A operand) and dT = dy^T ([rpT][ldT], the wgrad GEMM's A
 // operand), zero outside dy.  The grid covers the larger of the two extents per dimension.
@@ -1317,6 +1344,9 @@ struct Step {
     } else if (src_ct) {
       cfm_launch(tpack_kernel<bf16_t, bf16_t>, grid, block, 0, st, (const bf16_t*)src, ld, rows, cols, (int)tr,
                  scale, fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row, sv, dv);
+    } else if (!tr && fn == 0 && ones_row < 0 && sv == 2 && dv == 1 && cp % 8 == 0) {
+      cfm_launch(pack_rows_kernel, dim3(ew_grid((long)rp * cp / 8)), block, 0, st, (const float*)src, ld, rows,
+                 cols, scale, (bf16_t*)dst, dld, rp, cp);
     } else {
       cfm_launch(tpack_kernel<float, bf16_t>, grid, block, 0, st, (const float*)src, ld, rows, cols, (int)tr, scale,
                  fn, dr, (bf16_t*)dst, dld, rp, cp, ones_row, sv, dv);
