@@ -841,34 +841,54 @@ __global__ __launch_bounds__(256) void col2im_relu_vec_kernel(const T* __restric
 template <typename T>
 __global__ __launch_bounds__(256) void im2col_t_vec_kernel(const T* __restrict__ x1, int T1, int F1, int T2, int F2,
                                                            int C, int M2, T* __restrict__ dst, long ld, int rows_pad) {
+  // one block: 64 pixels x kRT consecutive 64-row tiles; the next row tile's loads are in flight
+  // while the current one is stored
+  constexpr int kRT = 4;
   __shared__ float tile[64][65];   // [row r - r0][pixel m - m0]
-  const int r0 = blockIdx.y * 64, m0 = blockIdx.x * 64;
+  const int m0 = blockIdx.x * 64;
+  float v[2][8];
+  auto load = [&](int r0) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {   // load: pixel m = m0 + (idx >> 3), rows r0 + 8 (idx & 7) .. +7
-    const int idx = q * 256 + threadIdx.x;
-    const int ml = idx >> 3, rl = 8 * (idx & 7);
-    const int m = m0 + ml, r = r0 + rl;
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (m < M2 && r < 9 * C) {
-      const int tap = r / C, ci = r - tap * C, kt = tap / 3, kf = tap - kt * 3;
-      const int f2 = m % F2, bt = m / F2, t2 = bt % T2, b = bt / T2;
-      const int ti = 2 * t2 - 1 + kt, fi = 2 * f2 - 1 + kf;
-      if (ti >= 0 && ti < T1 && fi >= 0 && fi < F1) ld8<T>(x1 + (((long)b * T1 + ti) * F1 + fi) * C + ci, v);
+    for (int q = 0; q < 2; ++q) {   // pixel m = m0 + (idx >> 3), rows r0 + 8 (idx & 7) .. +7
+      const int idx = q * 256 + threadIdx.x;
+      const int ml = idx >> 3, rl = 8 * (idx & 7);
+      const int m = m0 + ml, r = r0 + rl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[q][e] = 0.0f;
+      if (m < M2 && r < 9 * C) {
+        const int tap = r / C, ci = r - tap * C, kt = tap / 3, kf = tap - kt * 3;
+        const int f2 = m % F2, bt = m / F2, t2 = bt % T2, b = bt / T2;
+        const int ti = 2 * t2 - 1 + kt, fi = 2 * f2 - 1 + kf;
+        if (ti >= 0 && ti < T1 && fi >= 0 && fi < F1) ld8<T>(x1 + (((long)b * T1 + ti) * F1 + fi) * C + ci, v[q]);
+      }
     }
+  };
+  const int rt0 = blockIdx.y * kRT;
+  load(rt0 * 64);
+  for (int rt = rt0; rt < rt0 + kRT; ++rt) {
+    const int r0 = rt * 64;
+    if (r0 >= rows_pad) break;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) tile[rl + e][ml] = v[e];
-  }
-  __syncthreads();
+    for (int q = 0; q < 2; ++q) {
+      const int idx = q * 256 + threadIdx.x;
+      const int ml = idx >> 3, rl = 8 * (idx & 7);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {   // store: row r0 + (idx >> 3), pixels m0 + 8 (idx & 7) .. +7
-    const int idx = q * 256 + threadIdx.x;
-    const int rl = idx >> 3, ml = 8 * (idx & 7);
-    const int r = r0 + rl, m = m0 + ml;
-    if (r >= rows_pad || m >= ld) continue;
-    float v[8];
+      for (int e = 0; e < 8; ++e) tile[rl + e][ml] = v[q][e];
+    }
+    __syncthreads();
+    if (rt + 1 < rt0 + kRT && (rt + 1) * 64 < rows_pad) load(r0 + 64);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = r == 9 * C ? (m + e < M2 ? 1.0f : 0.0f) : tile[rl][ml + e];
-    st8<T>(dst + (long)r * ld + m, v);
+    for (int q = 0; q < 2; ++q) {   // store: row r0 + (idx >> 3), pixels m0 + 8 (idx & 7) .. +7
+      const int idx = q * 256 + threadIdx.x;
+      const int rl = idx >> 3, ml = 8 * (idx & 7);
+      const int r = r0 + rl, m = m0 + ml;
+      if (r >= rows_pad || m >= ld) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = r == 9 * C ? (m + e < M2 ? 1.0f : 0.0f) : tile[rl][ml + e];
+      st8<T>(dst + (long)r * ld + m, o);
+    }
+    __syncthreads();
   }
 }
 
@@ -2061,7 +2081,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   if (Gp(S.i_c2w) || Gp(S.i_c2b)) {   // [dW2 | db2] = dY2^T . [im2col(X1) | 1]
     S.pack(dX2, false, g.C, (int)g.M2, g.C, true, 1.0f, pat, g.M2p, g.C, (int)g.M2p);
     const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C + 4) + 31) / 32));
-    const dim3 grid64((unsigned)((g.M2p + 63) / 64), (unsigned)((S.npad(9L * g.C + 4) + 63) / 64));
+    const dim3 grid64((unsigned)((g.M2p + 63) / 64), (unsigned)((S.npad(9L * g.C + 4) + 255) / 256));   // 4 row tiles / block
     const bool vec = g.C % 8 == 0 && g.M2p % 8 == 0;
     if (vec && dt == DT_F32)
       cfm_launch(im2col_t_vec_kernel<float>, grid64, dim3(256), 0, st, S.T_<const float>(S.tp.X1), g.T1, g.F1, g.T2,
