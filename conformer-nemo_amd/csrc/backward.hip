@@ -396,7 +396,7 @@ cfm_status cfm_op_glu_backward(const float* pre, const float* dy, const int32_t*
 }
 
 size_t cfm_op_dwconv_backward_ws_size(int B, int Tp, int d, int K) {
-  const long nt = (Tp + 31) / 32;
+  const long nt = (Tp + 15) / 16;   // weight-gradient partials of 16-frame blocks (the finest split)
   return (size_t)round_up((long)B * nt * K * d * 4, 256) +
          std::max(col_sums_ws((int)(B * nt), K * d), col_sums_ws(B * Tp, d)) + 256;
 }
@@ -408,14 +408,27 @@ cfm_status cfm_op_dwconv_backward(const float* x, const float* w, const float* d
     if (K != 31) fail(CFM_ERR_UNSUPPORTED, "depthwise backward is built for kernel size 31");
     if (!ws || ws_bytes < cfm_op_dwconv_backward_ws_size(B, Tp, d, K)) fail(CFM_ERR_WORKSPACE, "workspace too small");
     hipStream_t st = (hipStream_t)stream;
-    constexpr int DT = 32;
-    const int nt = (Tp + DT - 1) / DT;
-    const dim3 grid(nt, (d + 255) / 256, B), block(256);
-    if (dx) cfm_launch(dwconv_bwd_x_kernel<31, DT>, grid, block, 0, st, dy, w, Tp, d, dx);
+    // frames per block of the input-gradient (CFM_DW_DT) and weight-gradient (CFM_DW_DTW) kernels:
+    // 16 (more blocks in flight for these latency-bound kernels: train 32.46-32.53 against 32.60-32.66
+    // ms/step for 32, 33.06-33.13 against 32.57-32.67 for 64); 32 / 64 selectable for A/B runs
+    static const int dtx = [] { const char* e = getenv("CFM_DW_DT"); return e ? atoi(e) : 16; }();
+    static const int dtw = [] { const char* e = getenv("CFM_DW_DTW"); return e ? atoi(e) : 16; }();
+    const int nt16 = (Tp + 15) / 16;
+    auto grid_of = [&](int dt_) { return dim3((Tp + dt_ - 1) / dt_, (d + 255) / 256, B); };
+    const dim3 block(256);
+    if (dx) {
+      if (dtx == 64) cfm_launch(dwconv_bwd_x_kernel<31, 64>, grid_of(64), block, 0, st, dy, w, Tp, d, dx);
+      else if (dtx == 16) cfm_launch(dwconv_bwd_x_kernel<31, 16>, grid_of(16), block, 0, st, dy, w, Tp, d, dx);
+      else cfm_launch(dwconv_bwd_x_kernel<31, 32>, grid_of(32), block, 0, st, dy, w, Tp, d, dx);
+    }
+    const int DTW = (dtw == 16 || dtw == 64) ? dtw : 32;
+    const int nt = (Tp + DTW - 1) / DTW;
     float* part = (float*)ws;
-    float* cs = (float*)((char*)ws + round_up((long)B * nt * K * d * 4, 256));
+    float* cs = (float*)((char*)ws + round_up((long)B * nt16 * K * d * 4, 256));
     if (dw) {
-      cfm_launch(dwconv_bwd_w_kernel<31, DT>, grid, block, 0, st, x, dy, Tp, d, part);
+      if (DTW == 64) cfm_launch(dwconv_bwd_w_kernel<31, 64>, grid_of(64), block, 0, st, x, dy, Tp, d, part);
+      else if (DTW == 16) cfm_launch(dwconv_bwd_w_kernel<31, 16>, grid_of(16), block, 0, st, x, dy, Tp, d, part);
+      else cfm_launch(dwconv_bwd_w_kernel<31, 32>, grid_of(32), block, 0, st, x, dy, Tp, d, part);
       // dw[c][k] = sum over the B * nt partial blocks of partial[blk][k][c]: column sums of a
       // (B*nt) x (K*d) matrix, then the [k][c] result transposed to the reference (d, 1, K) layout
       col_sums(part, (long)K * d, B * nt, K * d, part + (long)B * nt * K * d - (long)K * d, 0, cs, st);
