@@ -6,9 +6,15 @@ B=32 x T=1000 x 80-mel per GPU, eval mode, through the drop-in
     python bench.py [--gpus N --steps K --warmup W] [--compute bf16|fp32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-Multi-GPU: utterances shard across ranks with no data-path collective (weak scaling, per-GPU
-B=32); the time is the MAX over ranks between barrier+synchronize brackets.  Rank 0 prints ONE
-JSON line.  See DESIGN.md §Measurement for every field.
+`--gpus N` is authoritative: started without a torch.distributed environment (no WORLD_SIZE) and
+N > 1, bench.py starts the N ranks itself (torch.distributed.run children, 127.0.0.1) before any GPU
+call; under a launcher whose WORLD_SIZE differs from N it exits non-zero; the ranks count themselves
+over RCCL and the line reports that count (`ranks_joined`).
+
+Multi-GPU: utterances shard across ranks with no data-path collective in the forward (weak scaling,
+per-GPU B=32); the training leg (`train`, BASELINE config 3) all-reduces its gradients over RCCL.
+Times are the MAX over ranks between barrier+synchronize brackets.  Rank 0 prints ONE JSON line.
+See DESIGN.md §5 for every field.
 """
 import argparse
 import json
@@ -77,11 +83,13 @@ def cpu_baseline(enc, B, T, budget_s):
     """The reference encoder's arithmetic on the host cores: oracle/conformer_torch_cpu.py, a torch-CPU
     restatement of the reference forward (bitwise equal to the imported reference and within 10 % of
     its time in the survey container: profiles/r02_cpu_baseline_check.txt), fp32, eval,
-    torch.no_grad, the timed encoder's weights, batched utterances of T frames; 1 warm-up + min of 3.
-    The batch is cut so that the sample stays near `budget_s` seconds."""
+    torch.no_grad, the timed encoder's weights, the full B x T batch; a small warm-up, then the min of 2.
+    Threads: the CPU share the job is given (OMP_NUM_THREADS, 16 per GPU on the GPU boxes; the box's
+    os.cpu_count() is the whole host, shared with other jobs), else every core of this machine.
+    The batch is cut only if the full batch would exceed `budget_s` seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import conformer_torch_cpu as TC  # CPU baseline leg only
-    threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     sd = {k: v.detach().float().cpu() for k, v in enc.state_dict().items() if v.is_floating_point()}
@@ -93,11 +101,10 @@ def cpu_baseline(enc, B, T, budget_s):
     t0 = time.perf_counter()
     TC.encoder_forward(x, None, sd, cfg)                    # warm-up at a small batch: sizes the sample
     per_utt = (time.perf_counter() - t0) / Bs
-    Bs = int(max(1, min(B, budget_s / 4.0 / max(per_utt, 1e-6))))
+    Bs = int(max(1, min(B, budget_s / 2.0 / max(per_utt, 1e-6))))
     x = torch.randn(Bs, 80, T, generator=g)
-    TC.encoder_forward(x, None, sd, cfg)
     ts = []
-    for _ in range(3):
+    for _ in range(2):
         t0 = time.perf_counter()
         TC.encoder_forward(x, None, sd, cfg)
         ts.append(time.perf_counter() - t0)
@@ -110,9 +117,11 @@ def cpu_baseline(enc, B, T, budget_s):
     except (OSError, StopIteration):
         pass
     return {"value": round(Bs * T / min(ts), 1), "unit": "audio-frames/s", "cores": int(threads), "kind": "port",
-            "cpu_model": cpu_model,
+            "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
+            "threads_note": "OMP_NUM_THREADS = the CPU share the GPU box grants this job (the host's other cores "
+                            "belong to other jobs)" if os.environ.get("OMP_NUM_THREADS") else "all cores",
             "sample": f"oracle/conformer_torch_cpu.py (torch-CPU restatement of the reference, fp32 eval), "
-                      f"Large-17, B={Bs} x T={T} per forward, min of 3 after a warm-up, {total:.1f} s in all"}
+                      f"Large-17, B={Bs} x T={T} per forward, min of 2 after a B=2 warm-up, {total:.1f} s in all"}
 
 
 def parity_and_fp32(dev, B, T, steps=5):
@@ -181,20 +190,76 @@ def job_throughput(t_max, world, B, T, steps):
     return world * B * T * steps / t_max
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a torch.distributed environment: start N ranks, one per GPU,
+    as children of this process (torch.distributed.run, 127.0.0.1 rendezvous) BEFORE anything here touches
+    the GPU, and return their exit status.  Rank 0 prints the one JSON line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(gpus, world):
+    """--gpus N and the launcher's WORLD_SIZE must agree (a mismatch would time the wrong job)."""
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: refusing to report a "
+                         f"{world}-rank job as {gpus} GPUs")
+
+
+def ranks_joined(dev, dist):
+    """Number of ranks that joined the process group, counted by an all-reduce over it (RCCL on GPUs)."""
+    if not dist:
+        return 1
+    t = torch.ones(1, dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t)
+    return int(t.item())
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the launcher and rendezvous only, on CPU (gloo): every rank joins, rank 0 prints the
+    rank count.  Lets tests check `--gpus N` without a GPU."""
+    dist = world > 1
+    if dist:
+        torch.distributed.init_process_group("gloo")
+    n = ranks_joined(torch.device("cpu"), dist)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_joined": n, "gpus_arg": args.gpus, "dry_run": True}), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; without a torch.distributed environment bench.py starts N ranks itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/rendezvous check on CPU (gloo): no GPU, prints the ranks that joined")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--compute", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1000)
     ap.add_argument("--layers", type=int, default=17)
-    ap.add_argument("--cpu-budget", type=float, default=16.0,
+    ap.add_argument("--cpu-budget", type=float, default=40.0,
                     help="seconds of CPU-baseline timing (torch-CPU restatement of the reference; 0 = skip)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the bf16/fp32 relL2 against the reference golden and the fp32-mode throughput line")
     ap.add_argument("--no-breakdown", action="store_true")
+    ap.add_argument("--no-train", action="store_true",
+                    help="forward mode: skip the config-3 training-step leg reported under 'train'")
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "cache_stream", "mel", "decode"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
                          "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
@@ -207,9 +272,15 @@ def main():
     ap.add_argument("--vocab", type=int, default=256, help="train mode: CTC vocabulary (without blank)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # nothing has touched the GPU yet: the ranks are children, this process only waits for them
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args.gpus, world)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dist = world > 1
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -217,6 +288,9 @@ def main():
         import torch.distributed as tdist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         tdist.init_process_group("nccl", device_id=dev)
+        joined = ranks_joined(dev, dist)
+        if joined != args.gpus:
+            raise SystemExit(f"bench.py: {joined} ranks joined the RCCL group, --gpus {args.gpus}")
 
     def barrier():
         if dist:
@@ -257,6 +331,9 @@ def main():
     t_max = max_over_ranks(elapsed, dev, dist)
     value = job_throughput(t_max, world, B, T, args.steps)
     ms_step = 1000.0 * t_max / args.steps
+    # BASELINE config 3 (training step, DP over the same ranks, RCCL gradient buckets): every rank runs it
+    train = None if args.no_train else train_leg(args, world, rank, dev, dist, barrier, args.train_steps,
+                                                   args.train_warmup)
 
     if rank == 0:
         import conformer_amd
@@ -321,6 +398,8 @@ def main():
                             "TFLOP/s_per_gpu": round(total_flop / (ms_step * 1e-3) / 1e12, 1),
                             "frac_of_peak": round(total_flop / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
             "cpu_baseline": cpu,
+            "ranks_joined": world,
+            "train": train,
             "parity": parity,
             "fp32_parity_mode": fp32_line,
             "breakdown": breakdown,
@@ -333,12 +412,13 @@ def main():
 TRAIN_METRIC = "training-step audio-frames/sec, Conformer-CTC-Large B=32/GPU T=1000 (BASELINE config 3)"
 
 
-def run_train(args, world, rank, dev, dist, barrier):
+def train_leg(args, world, rank, dev, dist, barrier, steps, warmup):
     """BASELINE config 3: one step = encoder train-mode forward (dropout 0.1, batch-statistics BatchNorm,
     SyncBatchNorm across ranks) + ConvASRDecoder + CTCLoss(mean_batch) + backward with the per-layer
     gradient buckets all-reduced over RCCL while the backward runs (conformer_amd.dist.GradBuckets)
     + AdamW (conformer_ctc_bpe.yaml optim: betas 0.9/0.98, wd 1e-3).
-    Synthetic targets U=60 uniform in [0, V)."""
+    Synthetic targets U=60 uniform in [0, V).  Every rank runs it (the gradient exchange is
+    collective); returns the max-over-ranks timing and, on rank 0, the FLOP accounting."""
     from conformer_amd import dist as cdist
     from nemo.collections.asr.losses import CTCLoss
     from nemo.collections.asr.modules import ConformerEncoder, ConvASRDecoder
@@ -375,42 +455,45 @@ def run_train(args, world, rank, dev, dist, barrier):
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        loss = step()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    assert torch.isfinite(loss).item()
+    elapsed, loss = timed_loop(step, warmup, steps, barrier)
+    finite = bool(torch.isfinite(loss).item())
     t_max = max_over_ranks(elapsed, dev, dist)
-    value = job_throughput(t_max, world, B, T, args.steps)
-    ms_step = 1000.0 * t_max / args.steps
-    if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        from conformer_oracle import encoder_flops
-        fwd = encoder_flops(B, T, d, L)
-        n_par = sum(p.numel() for p in params)
-        out = {
-            "metric": TRAIN_METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
-            "config": {"workload": f"Conformer-CTC-Large training step (encoder d512/8 heads/{L} layers, dropout 0.1, "
-                                   f"dropout_att 0.1, "
-                                   f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss "
-                                   f"U={U}, AdamW), B={B}/GPU, T={T}",
-                       "global_batch": B * world, "seq_len": T,
-                       "parallelism": f"dp{world}" + (f" (per-layer RCCL gradient buckets overlapped with the "
-                                                      f"backward, {L + 2} all-reduces per step)" if dist else "")},
-            "model_flops": {"GFLOP_per_step_per_gpu_(3x_fwd)": round(3 * fwd / 1e9, 1),
-                            "TFLOP/s_per_gpu": round(3 * fwd / (ms_step * 1e-3) / 1e12, 1),
-                            "frac_of_peak": round(3 * fwd / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
-            "params": n_par, "loss": round(float(loss), 4),
-        }
-        print(json.dumps(out), flush=True)
-    if dist:
-        torch.distributed.destroy_process_group()
+    ms_step = 1000.0 * t_max / steps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops   # FLOP accounting only (after the timed loop)
+    fwd = encoder_flops(B, T, d, L)
+    res = {
+        "ms_per_step": round(ms_step, 4), "value": round(job_throughput(t_max, world, B, T, steps), 1),
+        "unit": "audio-frames/s", "steps": steps, "warmup": warmup,
+        "TFLOP/s_per_gpu": round(3 * fwd / (ms_step * 1e-3) / 1e12, 1),
+        "frac_of_peak": round(3 * fwd / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4),
+        "GFLOP_per_step_per_gpu_(3x_fwd)": round(3 * fwd / 1e9, 1),
+        "loss": round(float(loss), 4), "loss_finite": finite, "params": sum(p.numel() for p in params),
+        "workload": f"Conformer-CTC-Large training step (encoder d512/8 heads/{L} layers, dropout 0.1, dropout_att 0.1, "
+                    f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss U={U}, AdamW), "
+                    f"B={B}/GPU, T={T}",
+        "parallelism": f"dp{world}" + (f" (per-layer RCCL gradient buckets overlapped with the backward, "
+                                       f"{L + 2} all-reduces per step)" if dist else ""),
+    }
+    del enc, dec, opt, params
+    torch.cuda.empty_cache()
+    if not finite:
+        raise SystemExit("bench.py: training loss is not finite")
+    return res
+
+
+def run_train(args, world, rank, dev, dist, barrier):
+    r = train_leg(args, world, rank, dev, dist, barrier, args.steps, args.warmup)
+    emit(rank, dist, {
+        "metric": TRAIN_METRIC, "value": r["value"], "unit": "audio-frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.compute, "data": "synthetic",
+        "config": {"workload": r["workload"], "global_batch": args.batch * world, "seq_len": args.seq,
+                   "parallelism": r["parallelism"]},
+        "model_flops": {"GFLOP_per_step_per_gpu_(3x_fwd)": r["GFLOP_per_step_per_gpu_(3x_fwd)"],
+                        "TFLOP/s_per_gpu": r["TFLOP/s_per_gpu"], "frac_of_peak": r["frac_of_peak"]},
+        "params": r["params"], "loss": r["loss"],
+    })
 
 
 def timed_loop(step, warmup, steps, barrier):
