@@ -468,7 +468,7 @@ def train_leg(args, world, rank, dev, dist, barrier, steps, warmup):
         "TFLOP/s_per_gpu": round(3 * fwd / (ms_step * 1e-3) / 1e12, 1),
         "frac_of_peak": round(3 * fwd / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4),
         "GFLOP_per_step_per_gpu_(3x_fwd)": round(3 * fwd / 1e9, 1),
-        "loss": round(float(loss), 4), "loss_finite": finite, "params": sum(p.numel() for p in params),
+        "loss": round(float(loss.detach()), 4), "loss_finite": finite, "params": sum(p.numel() for p in params),
         "workload": f"Conformer-CTC-Large training step (encoder d512/8 heads/{L} layers, dropout 0.1, dropout_att 0.1, "
                     f"BatchNorm train stats{' + SyncBN' if dist else ''}, CTC head V={V}+1, CTC loss U={U}, AdamW), "
                     f"B={B}/GPU, T={T}",

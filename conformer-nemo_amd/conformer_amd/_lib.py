@@ -96,6 +96,9 @@ class CfmError(RuntimeError):
 _lib: Optional[ctypes.CDLL] = None
 
 
+ABI_VERSION = 2   # include/cfm_encoder.h CFM_ABI_VERSION: the struct layouts these bindings declare
+
+
 def load() -> ctypes.CDLL:
     """Load libcfm.so once.  torch must be imported first so the process shares torch's HIP runtime."""
     global _lib
@@ -179,6 +182,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.cfm_version() != ABI_VERSION:
+        raise CfmError(f"{LIB_PATH}: ABI version {lib.cfm_version()}, these bindings expect {ABI_VERSION} "
+                       f"(include/cfm_encoder.h CFM_ABI_VERSION): rebuild the library")
     _lib = lib
     return lib
 

@@ -114,7 +114,7 @@ class NativeGradBuckets(GradBuckets):
     def issued_count(self) -> int:
         return int(self.comm.lib.cfm_grad_buckets_issued(self.handle))
 
-    def finish(self) -> None:
+    def _finish_impl(self) -> None:
         _lib.check(self.comm.lib.cfm_grad_buckets_finish(self.handle, _stream()), "cfm_grad_buckets_finish")
 
     def __del__(self):

@@ -130,20 +130,48 @@ class GradBuckets:
         self.world = _world(group)
         self._works = []
         self._reduced = []           # (start, end) slices already issued this step
-        self.attach()
+        self._fresh, self._pending, self._finish_queued, self._scratch, self._direct = True, 0, False, None, True
+        for p, v in zip(self.members, self.views):
+            p.grad = v
 
     # ---- per step -------------------------------------------------------------------------------
+    # Gradient accumulation (several backward() calls per optimizer step, or an encoder run twice in
+    # one graph): a fresh step (some member's .grad is None, e.g. after zero_grad(set_to_none=True))
+    # zeroes the buffer and the first native backward writes straight into it, with the per-layer
+    # all-reduces overlapped.  Any later native backward of the same step writes into a scratch buffer
+    # that is then added into the views, and its exchange is one all-reduce of the whole buffer at the
+    # end of the backward.  All-reducing the accumulated sum is exact: the part already reduced is equal
+    # on every rank, so sum_r(avg(g1) + g2_r) / W = avg(g1) + avg(g2).
     def attach(self) -> None:
-        """Point every member's .grad at its view and zero the buffer (call before the backward;
-        the encoder's train forward does)."""
-        self.flat.zero_()
+        """Point every member's .grad at its view; zero the buffer when a new step starts (a member's
+        .grad is None or not the view).  Called by every train-mode encoder forward."""
+        fresh = any(p.grad is None or p.grad.data_ptr() != v.data_ptr() for p, v in zip(self.members, self.views))
+        if fresh:
+            self.flat.zero_()
+            self._fresh = True
+            self._pending = 0
         for p, v in zip(self.members, self.views):
             if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                 p.grad = v
-        self._works, self._reduced = [], []
+        self._pending = getattr(self, "_pending", 0) + 1
+
+    @property
+    def overlap(self) -> bool:
+        """The next native backward may write into the views directly and all-reduce layer by layer:
+        it is the first of a fresh step and the step runs the encoder once."""
+        return getattr(self, "_fresh", True) and getattr(self, "_pending", 1) <= 1
 
     def native_outputs(self, params: Sequence[torch.Tensor], want: Sequence[bool]) -> List[Optional[torch.Tensor]]:
-        """Output pointers for cfm_train_backward: table row i writes straight into its view."""
+        """Output pointers for cfm_train_backward: table row i writes straight into its view (first
+        backward of a fresh step) or into the accumulation scratch (see `accumulate_scratch`)."""
+        direct = getattr(self, "_fresh", True)
+        if direct:
+            base = self.flat
+        else:
+            if getattr(self, "_scratch", None) is None or self._scratch.numel() < self.table_end:
+                self._scratch = torch.empty(max(self.table_end, 1), dtype=torch.float32, device=self.flat.device)
+            self._scratch.zero_()
+            base = self._scratch
         out = []
         for i, (p, w) in enumerate(zip(params, want)):
             if not w:
@@ -152,8 +180,22 @@ class GradBuckets:
             r = self.rows[i] if i < len(self.rows) else None
             if r is None:
                 raise RuntimeError(f"table row {i} wants a gradient but is not in the gradient buckets")
-            out.append(self.flat[r[0]:r[0] + r[1]])
+            out.append(base[r[0]:r[0] + r[1]])
+        self._direct = direct
         return out
+
+    def after_backward(self) -> None:
+        """After cfm_train_backward was enqueued: fold a scratch-written gradient into the views."""
+        if not getattr(self, "_direct", True):
+            self.flat[:self.table_end].add_(self._scratch[:self.table_end])
+        self._fresh = False
+
+    def queue_finish(self) -> None:
+        """Run `finish` once at the end of the current autograd backward pass."""
+        if getattr(self, "_finish_queued", False):
+            return
+        self._finish_queued = True
+        torch.autograd.Variable._execution_engine.queue_callback(self.finish)
 
     def _issue(self, start: int, end: int, stream=None) -> None:
         if end <= start:
@@ -174,6 +216,14 @@ class GradBuckets:
 
     def finish(self) -> None:
         """End of the backward: reduce whatever no grad_ready covered, wait, average."""
+        try:
+            self._finish_impl()
+        finally:
+            self._finish_queued = False
+            self._pending = 0
+            self._issued_last, self._reduced = self._reduced, []
+
+    def _finish_impl(self) -> None:
         covered = sorted(self._reduced)
         pos, gaps = 0, []
         for a, b in covered:
@@ -192,7 +242,8 @@ class GradBuckets:
 
     @property
     def issued(self) -> List[Tuple[int, int]]:
-        return list(self._reduced)
+        """Slices issued so far in this backward, or after `finish` those of the last one."""
+        return list(self._reduced or getattr(self, "_issued_last", []))
 
 
 def enable_gradient_buckets(model: torch.nn.Module, group=None, average: bool = True) -> GradBuckets:

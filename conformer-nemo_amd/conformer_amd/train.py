@@ -182,25 +182,28 @@ class EncoderTrainer:
         ws = self._workspace(state["B"], state["T"])
         o = self._opts(state["dropout"], state["seed"], False, state["bn_momentum"], state["dropout_emb"],
                        state["dropout_att"])
-        if gb is not None and getattr(gb, "native_ready", None) is not None:
-            # conformer_amd.comm.NativeGradBuckets: the library's own callback issues the RCCL
-            # all-reduces (cfm_grad_buckets_ready_cb), no Python in the backward
-            fn, user = gb.native_ready
-            self._ready_cb = GRAD_READY_FN(fn.value)
-            o.grad_ready = self._ready_cb
-            o.grad_ready_user = user
-            torch.autograd.Variable._execution_engine.queue_callback(gb.finish)
-        elif gb is not None:
-            self._ready_cb = self._make_ready_callback()
-            o.grad_ready = self._ready_cb
-            # the remaining (non-encoder) gradients are final only when the whole backward is done
-            torch.autograd.Variable._execution_engine.queue_callback(gb.finish)
+        if gb is not None:
+            if gb.overlap and getattr(gb, "native_ready", None) is not None:
+                # conformer_amd.comm.NativeGradBuckets: the library's own callback issues the RCCL
+                # all-reduces (cfm_grad_buckets_ready_cb), no Python in the backward
+                fn, user = gb.native_ready
+                self._ready_cb = GRAD_READY_FN(fn.value)
+                o.grad_ready = self._ready_cb
+                o.grad_ready_user = user
+            elif gb.overlap:
+                self._ready_cb = self._make_ready_callback()
+                o.grad_ready = self._ready_cb
+            # the remaining (non-encoder, or accumulated) gradients are final only when the whole
+            # backward is done
+            gb.queue_finish()
         tape = state["tape"]
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
                                                state["B"], state["T"], ctypes.byref(o), self._ptrs(out),
                                                tape.data_ptr(), tape.numel(), ws.data_ptr(), ws.numel(), st),
                    "cfm_train_backward")
+        if gb is not None:
+            gb.after_backward()
         return grads
 
 

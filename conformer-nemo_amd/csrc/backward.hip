@@ -6,6 +6,7 @@
 // Reference semantics: torch.nn.LayerNorm (conformer_modules.py:66-70 via the layer, eps 1e-5,
 // biased variance), nn.Linear (y = x W^T + b), Swish (activations.py:20, x * sigmoid(x)).
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "../../include/cfm_train.h"
@@ -344,6 +345,21 @@ void swish_backward(const float* z, const float* du, float* dz, long n, hipStrea
 using namespace cfm;
 
 namespace {
+// CFM_DW_DT / CFM_DW_DTW (A/B measurements): frames per block of the depthwise-conv backward kernels,
+// 16 (default), 32 or 64; anything else is refused rather than silently replaced
+int dw_frames_env(const char* name) {
+  const char* e = getenv(name);
+  if (!e) return 16;
+  const int v = atoi(e);
+  if (v != 16 && v != 32 && v != 64) {
+    fprintf(stderr, "libcfm: %s=%s is not 16, 32 or 64\n", name, e);
+    fail(CFM_ERR_INVALID_ARG, "CFM_DW_DT / CFM_DW_DTW must be 16, 32 or 64");
+  }
+  return v;
+}
+}  // namespace
+
+namespace {
 
 struct LinBwdWs {
   long a1, wt, a2, b2, cs, total;
@@ -411,8 +427,8 @@ cfm_status cfm_op_dwconv_backward(const float* x, const float* w, const float* d
     // frames per block of the input-gradient (CFM_DW_DT) and weight-gradient (CFM_DW_DTW) kernels:
     // 16 (more blocks in flight for these latency-bound kernels: train 32.46-32.53 against 32.60-32.66
     // ms/step for 32, 33.06-33.13 against 32.57-32.67 for 64); 32 / 64 selectable for A/B runs
-    static const int dtx = [] { const char* e = getenv("CFM_DW_DT"); return e ? atoi(e) : 16; }();
-    static const int dtw = [] { const char* e = getenv("CFM_DW_DTW"); return e ? atoi(e) : 16; }();
+    static const int dtx = dw_frames_env("CFM_DW_DT");
+    static const int dtw = dw_frames_env("CFM_DW_DTW");
     const int nt16 = (Tp + 15) / 16;
     auto grid_of = [&](int dt_) { return dim3((Tp + dt_ - 1) / dt_, (d + 255) / 256, B); };
     const dim3 block(256);

@@ -191,6 +191,17 @@ cfm_status cfm_grad_buckets_create(cfm_comm* comm, float* flat, int64_t flat_num
         delete b;
         fail(CFM_ERR_INVALID_ARG, "bucket row outside the gradient buffer");
       }
+    {   // rows must not overlap: an element in two rows would be all-reduced twice
+      std::vector<std::pair<int64_t, int64_t>> r;
+      for (int i = 0; i < n_rows; ++i)
+        if (b->cnt[i] > 0) r.push_back({b->off[i], b->off[i] + b->cnt[i]});
+      std::sort(r.begin(), r.end());
+      for (size_t i = 1; i < r.size(); ++i)
+        if (r[i].first < r[i - 1].second) {
+          delete b;
+          fail(CFM_ERR_INVALID_ARG, "bucket rows overlap in the gradient buffer");
+        }
+    }
     int prev = 0;
     HIP_OK(hipGetDevice(&prev));
     HIP_OK(hipSetDevice(comm->device));
@@ -206,13 +217,19 @@ int cfm_grad_buckets_ready_cb(void* user, int first_param, int n_params, void* s
   auto* b = (cfm_grad_buckets*)user;
   const cfm_status s = guarded([&] {
     if (!b) fail(CFM_ERR_INVALID_ARG, "null bucket handle");
-    int64_t lo = -1, hi = -1;
-    for (int i = std::max(first_param, 0); i < first_param + n_params && i < (int)b->off.size(); ++i) {
-      if (b->cnt[i] <= 0) continue;
-      lo = lo < 0 ? b->off[i] : std::min(lo, b->off[i]);
-      hi = std::max(hi, b->off[i] + b->cnt[i]);
+    // the reported rows' byte ranges, merged into maximal contiguous runs: one all-reduce per run, so
+    // a layout whose rows are not adjacent never pulls in (and double-reduces) another row's slice
+    std::vector<std::pair<int64_t, int64_t>> spans;
+    for (int i = std::max(first_param, 0); i < first_param + n_params && i < (int)b->off.size(); ++i)
+      if (b->cnt[i] > 0) spans.push_back({b->off[i], b->off[i] + b->cnt[i]});
+    std::sort(spans.begin(), spans.end());
+    for (size_t i = 0; i < spans.size();) {
+      int64_t lo = spans[i].first, hi = spans[i].second;
+      size_t j = i + 1;
+      while (j < spans.size() && spans[j].first == hi) hi = spans[j++].second;
+      bucket_issue(b, lo, hi, (hipStream_t)stream);
+      i = j;
     }
-    if (lo >= 0) bucket_issue(b, lo, hi, (hipStream_t)stream);
   });
   return s == CFM_OK ? 0 : 1;
 }

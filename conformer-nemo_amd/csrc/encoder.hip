@@ -390,7 +390,7 @@ GemmEpi epi_of(int mode, const float* bias, float alpha = 1.0f) {
 extern "C" {
 
 const char* cfm_last_error(void) { return g_last_error.c_str(); }
-int cfm_version(void) { return 1; }
+int cfm_version(void) { return CFM_ABI_VERSION; }
 int cfm_encoded_length(int len) { return host_calc_length(len, 2); }
 
 cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int compute_mode, cfm_encoder** out) {

@@ -76,6 +76,12 @@ typedef struct cfm_tensor_view {
 typedef struct cfm_encoder cfm_encoder;
 
 const char* cfm_last_error(void);
+/* ABI revision of every cfm_*.h struct and entry point.  A host checks it against the value it was
+ * built with before passing any struct:
+ *   1  round 1;
+ *   2  cfm_train_opts (cfm_train.h) gained grad_ready / grad_ready_user, and dropout_emb / dropout_att
+ *      became active (an older host's shorter struct would leave the callback pointer unset). */
+#define CFM_ABI_VERSION 2
 int cfm_version(void);
 
 /* calc_length (subsampling.py:272-282) on the host: encoder frames for `len` input frames. */

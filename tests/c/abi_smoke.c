@@ -24,7 +24,7 @@
   } while (0)
 
 int main(void) {
-  CHECK(cfm_version() > 0, "cfm_version");
+  CHECK(cfm_version() == CFM_ABI_VERSION, "cfm_version");
   /* conformer_encoder.py calc_length (subsampling.py:272-282): T = 1000 -> T' = 250, T = 1 -> 1 */
   CHECK(cfm_encoded_length(1000) == 250 && cfm_encoded_length(1) == 1 && cfm_encoded_length(7) == 2,
         "cfm_encoded_length");

@@ -154,3 +154,63 @@ def test_bucketed_overlapped_allreduce_equals_flat_gloo_ws2():
         assert same and views_ok and frozen_none
         # P1 | P3 (rows 3..5) = flat[12:24], P0 (rows 0..2) = flat[0:12], then the head at finish
         assert issued == [(12, 24), (0, 12), (24, 30)]
+
+
+def _accum_worker(rank, world, port, q):
+    """Two micro-batches per optimizer step through GradBuckets (accumulation): the first
+    native backward writes into the views with overlapped per-layer all-reduces, the second writes into
+    the scratch and is added in; the result must equal the flat all-reduce of the summed plain grads."""
+    sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
+    from conformer_amd import dist as cdist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(5 + rank)
+        P = [torch.nn.Parameter(torch.zeros(s)) for s in ((4, 3), (7,), (5,))]
+        head = torch.nn.Parameter(torch.zeros(6))
+        gb = cdist.GradBuckets(P, [head], average=True)
+        want = [True, True, True]
+        micro = [({i: torch.randn(P[i].shape, generator=g) for i in range(3)}, torch.randn(6, generator=g))
+                 for _ in range(2)]
+        for p in P + [head]:
+            p.grad = None                                      # zero_grad(set_to_none=True)
+        overlaps = []
+        for vals, hv in micro:                                 # two forward/backward pairs, one step
+            gb.attach()                                        # what the train forward does
+            overlaps.append(gb.overlap)
+            outs = gb.native_outputs(P, want)                  # what cfm_train_backward writes into
+            for i, v in vals.items():
+                outs[i].copy_(v.reshape(-1))                   # overwrite semantics, as the kernels
+            if gb.overlap:
+                gb.on_ready(0, 3)
+            gb.after_backward()
+            head.grad += hv                                    # autograd accumulation into the view
+            gb.finish()
+        got = [p.grad.clone() for p in P + [head]]
+        Q = [torch.nn.Parameter(torch.zeros(t.shape)) for t in P + [head]]
+        for j, qp in enumerate(Q):
+            qp.grad = sum((micro[k][0][j] if j < 3 else micro[k][1]) for k in range(2)).clone()
+        cdist.allreduce_gradients(Q)
+        close = all(torch.allclose(a, qp.grad, rtol=1e-6, atol=1e-6) for a, qp in zip(got, Q))
+        # a new step (grads set to None) starts from zero again
+        for p in P + [head]:
+            p.grad = None
+        gb.attach()
+        fresh_zero = bool((gb.flat == 0).all()) and gb.overlap
+        q.put((rank, overlaps, close, fresh_zero))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_accumulation_through_buckets_gloo_ws2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    for rank, overlaps, close, fresh_zero in sorted(q.get(timeout=5) for _ in range(world)):
+        assert overlaps == [True, False]
+        assert close and fresh_zero

@@ -166,3 +166,53 @@ def test_grad_ready_order_and_bucket_views():
     for n_, p in enc.named_parameters():
         assert torch.equal(p.grad, plain[n_]), n_
         assert gb.flat.data_ptr() <= p.grad.data_ptr() < gb.flat.data_ptr() + 4 * gb.numel
+
+
+def test_gradient_accumulation_with_buckets_matches_plain():
+    """gradient buckets under accumulation.  Two micro-batches before one
+    optimizer step, and one graph that runs the encoder twice, must give the same .grad with buckets
+    as the plain autograd accumulation path (world 1: no averaging; summation order is the same)."""
+    for p in (os.path.join(ROOT, "conformer-nemo_amd"), os.path.join(ROOT, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from conformer_amd import dist as cdist
+    from nemo.collections.asr.modules import ConformerEncoder
+    from recipe import make_state_dict
+    z = np.load(os.path.join(GOLDEN, "train_tiny_ctx.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(**cfg, dropout=0.0, dropout_emb=0.0, dropout_att=0.0)
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref = enc.state_dict()
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
+    enc.set_compute_mode("fp32")
+    enc = enc.cuda().train()
+    x, ln, dy = (torch.from_numpy(z[k]).cuda() for k in ("x", "lengths", "dy"))
+    x2 = torch.flip(x, dims=[2]).contiguous()
+
+    def micro_batches():
+        for xi in (x, x2):
+            y, _ = enc(audio_signal=xi, length=ln)
+            (y * dy).sum().backward()
+
+    def one_graph():
+        y1, _ = enc(audio_signal=x, length=ln)
+        y2, _ = enc(audio_signal=x2, length=ln)
+        ((y1 * dy).sum() + (y2 * dy).sum()).backward()
+
+    for run in (micro_batches, one_graph):
+        for p in enc.parameters():
+            p.grad = None
+        enc.set_grad_buckets(None)
+        run()
+        plain = {n: p.grad.clone() for n, p in enc.named_parameters()}
+        for p in enc.parameters():
+            p.grad = None
+        gb = cdist.enable_gradient_buckets(torch.nn.ModuleList([enc]))
+        for p in enc.parameters():
+            p.grad = None                  # zero_grad(set_to_none=True) before the step
+        run()
+        torch.cuda.synchronize()
+        for n, p in enc.named_parameters():
+            assert gb.flat.data_ptr() <= p.grad.data_ptr() < gb.flat.data_ptr() + 4 * gb.numel, n
+            torch.testing.assert_close(p.grad, plain[n], rtol=1e-6, atol=1e-7, msg=f"{run.__name__}: {n}")
+        enc.set_grad_buckets(None)
