@@ -26,7 +26,8 @@ EXPORTED_SYMBOLS = (
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
     "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
     "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
-    "cfm_op_rel_attention", "cfm_bench_gemm",
+    "cfm_op_rel_attention", "cfm_bench_gemm", "cfm_encoder_layers_workspace_size", "cfm_encoder_layers_forward",
+    "cfm_op_conv_glu_dwconv_ws_size", "cfm_op_conv_glu_dwconv",
 )
 # every symbol include/cfm_train.h declares
 TRAIN_SYMBOLS = (
@@ -131,6 +132,10 @@ def load() -> ctypes.CDLL:
         "cfm_encoder_forward_timed": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(ci)]),
         "cfm_op_layernorm": (ci, [ci, vp, ci, ci, vp, vp, vp, vp, vp]),
+        "cfm_encoder_layers_workspace_size": (sz, [vp, ci, ci]),
+        "cfm_encoder_layers_forward": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp]),
+        "cfm_op_conv_glu_dwconv_ws_size": (sz, [ci, ci, ci, ci, ci]),
+        "cfm_op_conv_glu_dwconv": (ci, [ci, vp, vp, ci, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_op_linear": (ci, [ci, vp, ci, ci, vp, vp, ci, ci, vp, vp, ctypes.POINTER(sz), vp]),
         "cfm_op_rel_attention_ws_size": (sz, [ci, ci, ci, ci, ci]),
         "cfm_bench_gemm": (ci, [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(ctypes.c_float)]),

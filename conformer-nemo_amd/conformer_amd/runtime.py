@@ -154,6 +154,38 @@ class NativeEncoder:
                    "cfm_encoder_forward")
         return out, out_len
 
+    def layers_forward(self, x_btd: torch.Tensor, lengths: Optional[torch.Tensor] = None,
+                       pos_emb: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The ConformerLayer stack alone (cfm_encoder_layers_forward): x (B, T', d) -> (B, T', d) fp32.
+        lengths: valid frames per utterance (pad / attention masks); pos_emb: (2T'-1, d) relative
+        positions (None = the handle's table)."""
+        if not x_btd.is_cuda or x_btd.dim() != 3 or x_btd.shape[-1] != self.cfg.d_model:
+            raise ValueError(f"x must be a (B, T, {self.cfg.d_model}) tensor on the GPU")
+        x = x_btd.detach().float().contiguous()
+        B, Tp, d = x.shape
+        dev = x.device
+        len_ptr = None
+        if lengths is not None:
+            lengths = lengths.to(device=dev, dtype=torch.int32).contiguous()
+            len_ptr = lengths.data_ptr()
+        pe_ptr = None
+        if pos_emb is not None:
+            pos_emb = pos_emb.detach().to(device=dev, dtype=torch.float32).reshape(-1, d).contiguous()
+            if pos_emb.shape[0] != 2 * Tp - 1:
+                raise ValueError(f"pos_emb must hold 2T'-1 = {2 * Tp - 1} rows, got {pos_emb.shape[0]}")
+            pe_ptr = pos_emb.data_ptr()
+        elif Tp > self.max_audio_length:
+            torch.cuda.synchronize(self.device)
+            self.set_max_audio_length(Tp)
+        y = torch.empty_like(x)
+        nbytes = int(self.lib.cfm_encoder_layers_workspace_size(self.handle, B, Tp))
+        ws = self._workspace(nbytes)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(self.lib.cfm_encoder_layers_forward(self.handle, x.data_ptr(), len_ptr, B, Tp, pe_ptr, y.data_ptr(),
+                                                       ws.data_ptr(), nbytes, ctypes.c_void_p(stream)),
+                   "cfm_encoder_layers_forward")
+        return y
+
     def forward_timed(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None):
         """Per-stage kernel timing (cfm_encoder_forward_timed: every launch replayed in a burst of 8
         between HIP events).  Returns {stage: (device ms per forward, launches per forward)}.

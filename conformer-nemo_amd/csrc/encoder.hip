@@ -335,23 +335,25 @@ void ensure_streams(cfm_encoder* h, int n) {
 // workspace layout
 // ---------------------------------------------------------------------------------------------
 struct WsLayout {
-  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, LS, total;
+  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, LS, PE, LEN, total;
   int T1, T2, Tp, M, Tpad;
 };
 
-WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
+// front: the subsampling images X1 / X2 (the full forward); layers-only forwards (T1 = T2 = T',
+// no front end) instead hold the caller's positional rows in the compute type (PE).
+WsLayout ws_layout_core(const cfm_encoder* h, int B, int T1, int T2, bool front) {
   WsLayout w;
   const long es = h->es;
-  w.T1 = host_calc_length(T, 1);
-  w.T2 = host_calc_length(T, 2);
+  w.T1 = T1;
+  w.T2 = T2;
   w.Tp = w.T2;
   w.M = B * w.Tp;
   w.Tpad = (int)round_up(std::max(w.Tp, 1), 32);
   long off = 0;
   auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(bytes, 256) + 256; return o; };
   const long M = w.M;
-  w.X1 = take((long)B * w.T1 * h->F1 * h->C * es);
-  w.X2 = take((long)B * w.T2 * h->F2 * h->C * es);
+  w.X1 = front ? take((long)B * w.T1 * h->F1 * h->C * es) : -1;
+  w.X2 = front ? take((long)B * w.T2 * h->F2 * h->C * es) : -1;
   w.X = take(M * h->d * 4);
   w.Hn = take(M * h->d * es);
   w.U = take(M * h->dff * es);
@@ -364,8 +366,14 @@ WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
   w.PN = h->cfg.conv_norm_type == 1 ? take(M * h->d * 4) : -1;
   w.Y = h->has_out_proj ? take(M * h->dout * 4) : -1;
   w.LS = h->ln_fold ? take(M * ((h->d + LN_GRANULE - 1) / LN_GRANULE) * 8) : -1;   // folded-LayerNorm row partials
+  w.PE = front ? -1 : take((long)(2 * w.Tp - 1) * h->d * es);
+  w.LEN = front ? -1 : take((long)B * 4);
   w.total = round_up(off, 256);
   return w;
+}
+
+WsLayout ws_layout(const cfm_encoder* h, int B, int T) {
+  return ws_layout_core(h, B, host_calc_length(T, 1), host_calc_length(T, 2), true);
 }
 
 // (q + u) and (q + v) are stored pre-scaled so that exp2(score) == exp(score_ref / sqrt(dk))
@@ -585,30 +593,25 @@ struct ClockGuard {
 };
 #define TM(id) do { if (tm) tm->mark(id); } while (0)
 
-void pos_gemm(cfm_encoder* h, int Tp, void* dst, hipStream_t st) {
-  // linear_pos of every layer at once on pos_emb = pe[center - T' : center + T' - 1]
-  // (batch-independent, multi_head_attention.py:187 + RelPositionalEncoding.forward :311-313)
+// linear_pos of every layer at once on pos_emb (2T'-1 rows of d, compute type): by default the
+// handle's table window pe[center - T' : center + T' - 1] (batch-independent, multi_head_attention.py:187
+// + RelPositionalEncoding.forward :311-313), or a caller's rows (layers-only forward)
+void pos_gemm(cfm_encoder* h, int Tp, void* dst, hipStream_t st, const void* pe_rows = nullptr) {
   const long ldp = (long)h->L * h->H * h->dkp;
   GemmEpi e = epi_of(EPI_STORE, nullptr);
   e.C = dst;
   e.ldc = ldp;
-  const char* pe_slice = h->pe + (long)(h->max_len - Tp) * h->d * h->es;
+  const char* pe_slice = pe_rows ? (const char*)pe_rows : h->pe + (long)(h->max_len - Tp) * h->d * h->es;
   gemm(h->dtype, pe_slice, h->d, 2 * Tp - 1, h->d, h->wbuf + h->pos_w, (int)h->kpad(h->d), (int)ldp, e, h->zero_page,
        st);
 }
 
-void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
-                 int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream, StageTimer* tm,
-                 const char* P_ext = nullptr) {
-  {
-    if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
-    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
-    if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
-    if (T > h->max_len) fail(CFM_ERR_INVALID_ARG, "T exceeds max_audio_length; call cfm_encoder_set_max_audio_length");
-    const WsLayout wl = ws_layout(h, B, T);
-    if (!workspace || workspace_bytes < (size_t)wl.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
-    hipStream_t st = stream;
-    char* ws = (char*)workspace;
+// The ConformerLayer stack (conformer_modules.py:88-121, 17 x in ConformerEncoder.forward_for_export
+// :262-271) on the residual stream X = ws + wl.X (M = B * T' rows of d fp32, the input of layer 0),
+// positional projections of every layer at Pbuf; X holds the last layer's norm_out on return (Hn its
+// compute-type copy when an out_proj follows).
+void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const int32_t* lens, const char* Pbuf,
+                     hipStream_t st, StageTimer* tm) {
     const int dt = h->dtype, d = h->d, H = h->H, dkp = h->dkp, Tp = wl.Tp, M = wl.M, L = h->L;
     const int es = h->es;
     auto W = [&](long off) { return (const void*)(h->wbuf + off); };
@@ -628,37 +631,8 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
       if (!fold) return;
       e.bias = nullptr; e.ln_in = lns; e.ln_parts = lnp; e.ln_width = d; e.ln_c = Wf(lc); e.ln_d = Wf(ld);
     };
-
-    // lengths (subsampling.py:164-171) -> out_len_b, used as the pad mask from here on
-    TM(ST_LEN);
-    calc_length(len_b, out_len_b, B, T, 2, st);
-    const int32_t* lens = out_len_b;
-
-    // ConvSubsampling (subsampling.py:163-176) + xscale (multi_head_attention.py:305-306)
-    TM(ST_CONV1);
-    conv1_subsample(dt, x_bft, B, h->F, T, Wf(h->conv1_w), Wf(h->conv1_b), h->C, ws + wl.X1, st);
-    {
-      TM(ST_CONV2);
-      ConvGeom g{ws + wl.X1, wl.T1, h->F1, wl.T2, h->F2, h->C};
-      GemmEpi e = epi_of(EPI_RELU, Wf(h->conv2_b));
-      e.C = ws + wl.X2;
-      e.ldc = h->C;
-      gemm_conv(dt, g, B, W(h->conv2_w), (int)h->kpad(9 * h->C), h->C, e, h->zero_page, st);
-    }
-    {
-      TM(ST_SUBOUT);
-      const float xs = h->cfg.xscaling ? (float)std::sqrt((double)d) : 1.0f;
-      GemmEpi e = epi_of(EPI_SCALE_F32, Wf(h->sub_b), xs);
-      e.X = X;
-      e.ldx = d;
-      gemm(dt, ws + wl.X2, (long)h->F2 * h->C, M, h->F2 * h->C, W(h->sub_w), (int)h->kpad(h->F2 * h->C), d, e,
-           h->zero_page, st);
-    }
     const long ldp = (long)L * H * dkp;
-    const char* Pbuf = P_ext ? P_ext : ws + wl.P;
     if (L > 0) {
-      TM(ST_POS);
-      if (!P_ext) pos_gemm(h, Tp, ws + wl.P, st);
       TM(ST_LN);
       layernorm(dt, X, M, d, Wf(h->layers[0].ln_w[0]), Wf(h->layers[0].ln_b[0]), nullptr, nullptr, nullptr, Hn, 0, st);
     }
@@ -781,6 +755,59 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
                 next ? Wf(h->layers[l + 1].ln_b[0]) : nullptr, want_t ? Hn : nullptr, 0, st);
     }
 
+}
+
+void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
+                 int32_t* out_len_b, void* workspace, size_t workspace_bytes, hipStream_t stream, StageTimer* tm,
+                 const char* P_ext = nullptr) {
+  {
+    if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+    if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
+    if (T > h->max_len) fail(CFM_ERR_INVALID_ARG, "T exceeds max_audio_length; call cfm_encoder_set_max_audio_length");
+    const WsLayout wl = ws_layout(h, B, T);
+    if (!workspace || workspace_bytes < (size_t)wl.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = stream;
+    char* ws = (char*)workspace;
+    const int dt = h->dtype, d = h->d, H = h->H, dkp = h->dkp, Tp = wl.Tp, M = wl.M, L = h->L;
+    const int es = h->es;
+    auto W = [&](long off) { return (const void*)(h->wbuf + off); };
+    auto Wf = [&](long off) { return (const float*)(h->wbuf + off); };
+    float* X = (float*)(ws + wl.X);
+    void* Hn = ws + wl.Hn;
+
+    // lengths (subsampling.py:164-171) -> out_len_b, used as the pad mask from here on
+    TM(ST_LEN);
+    calc_length(len_b, out_len_b, B, T, 2, st);
+    const int32_t* lens = out_len_b;
+
+    // ConvSubsampling (subsampling.py:163-176) + xscale (multi_head_attention.py:305-306)
+    TM(ST_CONV1);
+    conv1_subsample(dt, x_bft, B, h->F, T, Wf(h->conv1_w), Wf(h->conv1_b), h->C, ws + wl.X1, st);
+    {
+      TM(ST_CONV2);
+      ConvGeom g{ws + wl.X1, wl.T1, h->F1, wl.T2, h->F2, h->C};
+      GemmEpi e = epi_of(EPI_RELU, Wf(h->conv2_b));
+      e.C = ws + wl.X2;
+      e.ldc = h->C;
+      gemm_conv(dt, g, B, W(h->conv2_w), (int)h->kpad(9 * h->C), h->C, e, h->zero_page, st);
+    }
+    {
+      TM(ST_SUBOUT);
+      const float xs = h->cfg.xscaling ? (float)std::sqrt((double)d) : 1.0f;
+      GemmEpi e = epi_of(EPI_SCALE_F32, Wf(h->sub_b), xs);
+      e.X = X;
+      e.ldx = d;
+      gemm(dt, ws + wl.X2, (long)h->F2 * h->C, M, h->F2 * h->C, W(h->sub_w), (int)h->kpad(h->F2 * h->C), d, e,
+           h->zero_page, st);
+    }
+    const char* Pbuf = P_ext ? P_ext : ws + wl.P;
+    if (L > 0 && !P_ext) {
+      TM(ST_POS);
+      pos_gemm(h, Tp, ws + wl.P, st);
+    }
+    run_layer_stack(h, ws, wl, B, lens, Pbuf, st, tm);
+
     const float* fin = X;
     TM(ST_OUT);
     if (h->has_out_proj) {   // out_proj (conformer_encoder.py:277-278)
@@ -854,6 +881,41 @@ cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t
     if (!h || !x_bft || !y_bdt || !out_len_b) fail(CFM_ERR_INVALID_ARG, "null argument");
     if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
     run_split(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream);
+  });
+}
+
+size_t cfm_encoder_layers_workspace_size(const cfm_encoder* h, int B, int Tp) {
+  if (!h || B <= 0 || Tp <= 0) return 0;
+  return (size_t)ws_layout_core(h, B, Tp, Tp, false).total;
+}
+
+cfm_status cfm_encoder_layers_forward(cfm_encoder* h, const float* x_btd, const int32_t* len_b, int B, int Tp,
+                                      const float* pos_emb, float* y_btd, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
+  return guarded([&] {
+    if (!h || !x_btd || !y_btd) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+    if (B <= 0 || Tp <= 0) fail(CFM_ERR_INVALID_ARG, "B and T' must be positive");
+    if (!pos_emb && Tp > h->max_len) fail(CFM_ERR_INVALID_ARG, "T' exceeds max_audio_length");
+    const WsLayout wl = ws_layout_core(h, B, Tp, Tp, false);
+    if (!workspace || workspace_bytes < (size_t)wl.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    const long rows = (long)B * Tp * h->d;
+    HIP_OK(hipMemcpyAsync(ws + wl.X, x_btd, rows * 4, hipMemcpyDeviceToDevice, st));
+    int32_t* lens = (int32_t*)(ws + wl.LEN);
+    calc_length(len_b, lens, B, Tp, 0, st);   // repeat 0: a copy of len_b (T' where NULL)
+    if (h->L > 0) {
+      const void* pe_rows = nullptr;
+      if (pos_emb) {
+        convert_f32(h->dtype, pos_emb, ws + wl.PE, (long)(2 * Tp - 1) * h->d, st);
+        pe_rows = ws + wl.PE;
+      }
+      pos_gemm(h, Tp, ws + wl.P, st, pe_rows);
+      run_layer_stack(h, ws, wl, B, lens, ws + wl.P, st, nullptr);
+    }
+    HIP_OK(hipMemcpyAsync(y_btd, ws + wl.X, rows * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipGetLastError());
   });
 }
 
@@ -934,6 +996,71 @@ cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w,
     e.C = y;
     e.ldc = N;
     gemm(dt, x, K, M, K, base, (int)Kp, N, e, zero, st);
+    HIP_OK(hipGetLastError());
+  });
+}
+
+// ---- ConformerConvolution's middle (conformer_modules.py:164-176) as a kernel-level op --------
+}  // extern "C"
+namespace {
+// GLU over the channel halves [a | gate] of pointwise_conv1's output (nn.functional.glu, dim=1) and
+// the pad mask (masked_fill, conformer_modules.py:166-167): g[m][c] = a * sigmoid(gate), 0 on padded frames
+template <typename T>
+__global__ void glu_mask_kernel(const T* pre, const int32_t* lens, int B, int Tp, int d, T* g) {
+  const long n = (long)B * Tp * d;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / d;
+    const int c = (int)(i - m * d);
+    const int t = (int)(m % Tp), b = (int)(m / Tp);
+    const bool pad = lens && t >= lens[b];
+    const float a = ld_f<T>(pre + m * 2 * d + c), gt = ld_f<T>(pre + m * 2 * d + d + c);
+    st_f<T>(g + i, pad ? 0.0f : a * sigmoidf_(gt));
+  }
+}
+}  // namespace
+extern "C" {
+
+extern "C" size_t cfm_op_conv_glu_dwconv_ws_size(int dtype, int B, int Tp, int d, int K) {
+  const int es = dtype == CFM_COMPUTE_FP32 ? 4 : 2;
+  const long M = (long)B * Tp;
+  return (size_t)(round_up(M * d * es, 256) + round_up(M * d * 4, 256) + round_up((long)d * (K + 6) * 4, 256) + 256);
+}
+
+extern "C" cfm_status cfm_op_conv_glu_dwconv(int dtype, const void* pre, const int32_t* lens, int B, int Tp, int d,
+                                             int K, const float* dw_w, const float* dw_b, int norm_type,
+                                             const float* norm_w, const float* norm_b, const float* bn_mean,
+                                             const float* bn_var, void* out, void* ws, size_t ws_bytes, void* stream) {
+  return guarded([&] {
+    if (!pre || !dw_w || !dw_b || !norm_w || !norm_b || !out || !ws) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (norm_type == 0 && (!bn_mean || !bn_var)) fail(CFM_ERR_INVALID_ARG, "batch_norm needs running statistics");
+    if (K < 1 || K % 2 == 0 || B <= 0 || Tp <= 0 || d <= 0) fail(CFM_ERR_INVALID_ARG, "shape");
+    if (ws_bytes < cfm_op_conv_glu_dwconv_ws_size(dtype, B, Tp, d, K)) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    const long M = (long)B * Tp;
+    hipStream_t st = (hipStream_t)stream;
+    char* w = (char*)ws;
+    char* G = w;
+    float* PN = (float*)(w + round_up(M * d * es, 256));
+    float* prm = (float*)((char*)PN + round_up(M * d * 4, 256));
+    // depthwise weight (d, 1, K) -> [K][d]; BatchNorm running var -> 1/sqrt(var + eps) (host, as set_weights)
+    std::vector<float> hw((size_t)d * K), hv(d, 1.0f), host((size_t)d * (K + 1));
+    HIP_OK(hipMemcpyAsync(hw.data(), dw_w, hw.size() * 4, hipMemcpyDeviceToHost, st));
+    if (norm_type == 0) HIP_OK(hipMemcpyAsync(hv.data(), bn_var, (size_t)d * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (int k = 0; k < K; ++k)
+      for (int c = 0; c < d; ++c) host[(size_t)k * d + c] = hw[(size_t)c * K + k];
+    for (int c = 0; c < d; ++c) host[(size_t)K * d + c] = 1.0f / std::sqrt(hv[c] + 1e-5f);
+    HIP_OK(hipMemcpyAsync(prm, host.data(), host.size() * 4, hipMemcpyHostToDevice, st));
+    const dim3 g(1024), b(256);
+    if (dt == DT_F32) cfm_launch(glu_mask_kernel<float>, g, b, 0, st, (const float*)pre, lens, B, Tp, d, (float*)G);
+    else cfm_launch(glu_mask_kernel<bf16_t>, g, b, 0, st, (const bf16_t*)pre, lens, B, Tp, d, (bf16_t*)G);
+    if (norm_type == 0) {
+      dwconv_norm_swish(dt, G, B, Tp, d, K, prm, dw_b, bn_mean, prm + (long)K * d, norm_w, norm_b, out, nullptr, st);
+    } else {
+      dwconv_norm_swish(dt, G, B, Tp, d, K, prm, dw_b, nullptr, nullptr, nullptr, nullptr, nullptr, PN, st);
+      layernorm(dt, PN, (int)M, d, norm_w, norm_b, nullptr, nullptr, nullptr, out, 1, st);
+    }
+    HIP_OK(hipStreamSynchronize(st));   // the host staging vector must outlive the copy
     HIP_OK(hipGetLastError());
   });
 }

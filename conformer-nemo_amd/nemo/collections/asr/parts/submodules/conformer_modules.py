@@ -1,9 +1,12 @@
-"""ConformerLayer / ConformerConvolution / ConformerFeedForward parameter containers
-(reference conformer_modules.py:28-200).  Attribute names and shapes are the reference's, so
-state_dicts load unchanged; the arithmetic is the native layer loop of csrc/encoder.hip.
-"""
+"""ConformerLayer / ConformerConvolution / ConformerFeedForward (reference conformer_modules.py:28-200).
+Attribute names and shapes are the reference's, so state_dicts load unchanged.  Inside ConformerEncoder
+the arithmetic is the native layer loop of csrc/encoder.hip; called on their own, the modules run
+natively too (conformer_amd.submodule_ops): ConformerLayer through the same layer stack
+(cfm_encoder_layers_forward), the feed-forward and convolution modules through the kernel-level
+entry points.  Standalone calls are inference-only (eval mode, no autograd)."""
 from __future__ import annotations
 
+import torch
 from torch import nn
 from torch.nn import LayerNorm
 
@@ -41,8 +44,27 @@ class ConformerLayer(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.norm_out = LayerNorm(d_model)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("ConformerLayer runs inside ConformerEncoder's native forward")
+    def forward(self, x, att_mask=None, pos_emb=None, pad_mask=None):
+        """x (B, T, d_model) -> (B, T, d_model) (conformer_modules.py:88-121): macaron FFN, rel-pos MHSA,
+        convolution module, FFN, norm_out, on the native layer stack.  att_mask (B, T, T) / pad_mask (B, T)
+        (True = masked) as ConformerEncoder builds them; pos_emb (1, 2T-1, d_model) from
+        RelPositionalEncoding."""
+        from conformer_amd import submodule_ops as ops
+        ops.check_inference(self, x)
+        if self.self_attention_model != "rel_pos":
+            raise NotImplementedError("the native layer stack implements self_attention_model='rel_pos'")
+        if pos_emb is None:
+            raise ValueError("rel_pos ConformerLayer needs pos_emb (RelPositionalEncoding's output)")
+        B, T, _ = x.shape
+        lengths, ctx = ops.masks_to_lengths(att_mask, pad_mask, B, T, x.device)
+        if not hasattr(self, "_runner"):
+            self._runner = ops.LayerRunner()
+        return self._runner.forward(self, x, lengths, pos_emb, ctx, pad_mask is not None, ops.compute_mode(self))
+
+    def set_compute_mode(self, compute: str):
+        if compute not in ("bf16", "fp32"):
+            raise ValueError("compute must be 'bf16' or 'fp32'")
+        self.compute = compute
 
 
 class ConformerConvolution(nn.Module):
@@ -62,8 +84,21 @@ class ConformerConvolution(nn.Module):
         self.activation = Swish()
         self.pointwise_conv2 = nn.Conv1d(d_model, d_model, kernel_size=1, stride=1, padding=0, bias=True)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("ConformerConvolution runs inside ConformerEncoder's native forward")
+    def forward(self, x, pad_mask=None):
+        """x (B, T, d_model) -> (B, T, d_model) (conformer_modules.py:160-180): pointwise_conv1, GLU, pad mask,
+        depthwise conv, Batch/LayerNorm, Swish, pointwise_conv2.  pad_mask (B, T), True = padded frame."""
+        from conformer_amd import submodule_ops as ops
+        ops.check_inference(self, x)
+        compute = ops.compute_mode(self)
+        B, T, d = x.shape
+        lengths = None
+        if pad_mask is not None:
+            lengths, _ = ops.masks_to_lengths(None, pad_mask, B, T, x.device)
+        x2 = x.detach().reshape(B * T, d).to(ops.COMPUTE_DTYPE[compute]).contiguous()
+        pre = ops.linear(x2, self.pointwise_conv1.weight, self.pointwise_conv1.bias, 0, compute)
+        mid = ops.conv_glu_dwconv(pre, lengths, B, T, d, self, compute)
+        y = ops.linear(mid, self.pointwise_conv2.weight, self.pointwise_conv2.bias, 0, compute)
+        return y.float().reshape(B, T, d)
 
 
 class ConformerFeedForward(nn.Module):
@@ -74,5 +109,15 @@ class ConformerFeedForward(nn.Module):
         self.dropout = nn.Dropout(p=dropout)
         self.linear2 = nn.Linear(d_ff, d_model)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("ConformerFeedForward runs inside ConformerEncoder's native forward")
+    def forward(self, x):
+        """linear1 -> Swish -> linear2 (conformer_modules.py:195-200; dropout is the identity in eval)."""
+        from conformer_amd import submodule_ops as ops
+        ops.check_inference(self, x)
+        if not isinstance(self.activation, (Swish, nn.SiLU)):
+            raise NotImplementedError("the native feed-forward fuses Swish; other activations are not implemented")
+        compute = ops.compute_mode(self)
+        shape = x.shape
+        x2 = x.detach().reshape(-1, shape[-1]).to(ops.COMPUTE_DTYPE[compute]).contiguous()
+        h = ops.linear(x2, self.linear1.weight, self.linear1.bias, 2, compute)
+        y = ops.linear(h, self.linear2.weight, self.linear2.bias, 0, compute)
+        return y.float().reshape(*shape[:-1], y.shape[-1])

@@ -1,8 +1,10 @@
-"""Attention / positional-encoding parameter containers (reference multi_head_attention.py).
+"""Attention / positional-encoding modules (reference multi_head_attention.py).
 
 RelPositionMultiHeadAttention's arithmetic (Transformer-XL scores with rel_shift, masked softmax,
-P.V) is the fused HIP kernel csrc/attention.hip; linear_q/k/v are one packed MFMA GEMM whose
-epilogue writes V pre-transposed, linear_pos of all layers is one GEMM per forward.
+P.V) is the fused HIP kernel csrc/attention.hip; inside the encoder linear_q/k/v are one packed MFMA
+GEMM and linear_pos of all layers is one GEMM per forward.  Called on their own, the attention modules
+run the projections on cfm_op_linear and the core on cfm_op_rel_attention (conformer_amd.submodule_ops);
+MultiHeadAttention is the same core with zero positional scores and biases.  Inference only.
 """
 from __future__ import annotations
 
@@ -25,8 +27,40 @@ class MultiHeadAttention(nn.Module):
         self.linear_out = nn.Linear(n_feat, n_feat)
         self.dropout = nn.Dropout(p=dropout_rate)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("attention runs inside ConformerEncoder's native forward")
+    def forward(self, query, key, value, mask, pos_emb=None):
+        """Scaled dot-product attention (multi_head_attention.py:94-128): (B, T, n_feat) -> (B, T, n_feat)."""
+        return self._native_attention(query, key, value, mask, None)
+
+    def set_compute_mode(self, compute: str):
+        if compute not in ("bf16", "fp32"):
+            raise ValueError("compute must be 'bf16' or 'fp32'")
+        self.compute = compute
+
+    def _native_attention(self, query, key, value, mask, pos_emb):
+        from conformer_amd import submodule_ops as ops
+        ops.check_inference(self, query, key, value)
+        B, T, d = query.shape
+        if key.shape[1] != T or value.shape[1] != T:
+            raise NotImplementedError("the native attention core is self-attention shaped (time1 == time2)")
+        compute = ops.compute_mode(self)
+        dt = ops.COMPUTE_DTYPE[compute]
+        dev = query.device
+        lengths, ctx = ops.masks_to_lengths(mask, None, B, T, dev)
+        proj = lambda x, lin: ops.linear(x.detach().reshape(B * T, d).to(dt).contiguous(), lin.weight, lin.bias, 0,  # noqa: E731
+                                         compute)
+        q, k, v = proj(query, self.linear_q), proj(key, self.linear_k), proj(value, self.linear_v)
+        if pos_emb is None:   # MultiHeadAttention: no positional scores, no biases
+            p = torch.zeros((2 * T - 1, d), dtype=dt, device=dev)
+            u = vb = torch.zeros((self.h, self.d_k), device=dev)
+        else:
+            if pos_emb.shape[0] != 1 or pos_emb.shape[1] != 2 * T - 1:
+                raise ValueError(f"pos_emb must be (1, 2T-1, n_feat) = (1, {2 * T - 1}, {d})")
+            p = ops.linear(pos_emb.detach().reshape(2 * T - 1, d).to(dt).contiguous(), self.linear_pos.weight, None, 0,
+                           compute)
+            u, vb = self.pos_bias_u, self.pos_bias_v
+        ctxv = ops.rel_attention(q, k, v, p, u, vb, lengths, B, T, self.h, self.d_k, ctx, compute)
+        y = ops.linear(ctxv, self.linear_out.weight, self.linear_out.bias, 0, compute)
+        return y.float().reshape(B, T, d)
 
 
 class RelPositionMultiHeadAttention(MultiHeadAttention):
@@ -39,6 +73,11 @@ class RelPositionMultiHeadAttention(MultiHeadAttention):
         else:
             self.pos_bias_u = pos_bias_u
             self.pos_bias_v = pos_bias_v
+
+    def forward(self, query, key, value, mask, pos_emb):
+        """Transformer-XL attention with relative positions (multi_head_attention.py:172-210):
+        (B, T, n_feat) -> (B, T, n_feat); mask (B, T, T) True = masked; pos_emb (1, 2T-1, n_feat)."""
+        return self._native_attention(query, key, value, mask, pos_emb)
 
 
 class PositionalEncoding(nn.Module):

@@ -130,6 +130,18 @@ cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t
  * average is ADDED into stage_ms[stage]; stage_launches[stage] += kernels per forward.
  * Synchronises.  The outputs of this call are NOT the forward's (replayed residual adds) — timing
  * only.  Not graph-capturable; used for the per-kernel roofline in bench.py. */
+/* The ConformerLayer stack alone (ConformerLayer.forward, conformer_modules.py:88-121, applied for
+ * every layer of the handle as ConformerEncoder.forward_for_export :262-271 does): x_btd (B, T', d) fp32
+ * is layer 0's input (after the positional encoding's xscale), y_btd (B, T', d) fp32 the last layer's
+ * norm_out.  len_b (B) int32 valid frames per utterance (the pad and attention masks, as in the
+ * encoder; NULL = all T'); pos_emb (2T'-1, d) fp32 relative positions T'-1 ... -(T'-1) as
+ * RelPositionalEncoding.forward returns them (NULL = the handle's own table).  Stream-ordered;
+ * workspace of cfm_encoder_layers_workspace_size bytes.  The subsampling weights are not used. */
+size_t cfm_encoder_layers_workspace_size(const cfm_encoder* h, int B, int Tp);
+cfm_status cfm_encoder_layers_forward(cfm_encoder* h, const float* x_btd, const int32_t* len_b, int B, int Tp,
+                                      const float* pos_emb, float* y_btd, void* workspace, size_t workspace_bytes,
+                                      void* stream);
+
 int cfm_num_stages(void);
 const char* cfm_stage_name(int i);
 cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,
@@ -153,6 +165,18 @@ size_t cfm_op_rel_attention_ws_size(int dtype, int B, int Tp, int H, int dk);
 cfm_status cfm_op_rel_attention(int dtype, const void* q, const void* k, const void* v, const void* p,
                                 const float* pos_u, const float* pos_v, const int32_t* lens, int B, int Tp, int H,
                                 int dk, int ctx_left, int ctx_right, void* out, void* ws, void* stream);
+
+/* ConformerConvolution between its pointwise convolutions (conformer_modules.py:164-176): pre (B*T', 2d)
+ * compute type = pointwise_conv1's output [a | gate] -> GLU -> pad mask (frames t >= lens[b] zeroed;
+ * lens NULL = no mask) -> depthwise conv (k = K, zero padding (K-1)/2; dw_w (d, 1, K), dw_b (d), fp32) ->
+ * norm_type 0: BatchNorm1d with running statistics (eps 1e-5) | 1: LayerNorm(d) -> Swish -> out (B*T', d)
+ * compute type.  Synchronises the stream (host-side weight relayout).  Scratch of
+ * cfm_op_conv_glu_dwconv_ws_size bytes. */
+size_t cfm_op_conv_glu_dwconv_ws_size(int dtype, int B, int Tp, int d, int K);
+cfm_status cfm_op_conv_glu_dwconv(int dtype, const void* pre, const int32_t* lens, int B, int Tp, int d, int K,
+                                  const float* dw_w, const float* dw_b, int norm_type, const float* norm_w,
+                                  const float* norm_b, const float* bn_mean, const float* bn_var, void* out, void* ws,
+                                  size_t ws_bytes, void* stream);
 
 /* GEMM microbenchmark on synthetic data: average device ms of `iters` launches of the encoder's
  * GEMM (M x N x K, epilogue id as in csrc/cfm_kernels.h, tile -1 = automatic choice).  Allocates. */
