@@ -53,6 +53,10 @@ struct cfm_encoder {
   // bf16 eval forward with T' <= 256: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish as
   // one launch (gemm_glu_dw); CFM_GLU_DW=0 keeps the two launches (A/B)
   bool fuse_glu_dw = true;
+  // conv.0 recomputed inside conv.2 (conv12_fused) - off by default: bitwise equal to the two-kernel path but
+  // 5.60 against 4.96 ms per forward (its 9 fp32 FMAs per X1 value overflow the MFMA ping-pong's VALU slots,
+  // DESIGN.md section 4); env CFM_CONV12=1 turns it on
+  bool fuse_conv12 = false;
   std::vector<hipStream_t> sub_streams;
   std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
   void* zero_page = nullptr;

@@ -150,6 +150,14 @@ struct TConvGeom {
   int B, T2, F2, C, pt, pf, nI, nJ;
 };
 bool gemm_tconv_supported(int dtype, int C);
+// ConvSubsampling's conv.0 + ReLU + conv.2 + ReLU (bf16, C % 128 == 0, C <= 1024): X1 is recomputed
+// inside conv2's implicit GEMM from per-pixel input patches instead of being written and re-read.
+// X2 (B, T2, F2, C) bf16; `patch` scratch of conv12_patch_bytes(B, T1, F1) bytes.
+bool conv12_supported(int dtype, int C);
+size_t conv12_patch_bytes(int B, int T1, int F1, int C);
+void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T2, int F2, const float* w1,
+                  const float* b1, int C, const void* Wp, int Kpad, const float* b2, void* X2, void* patch,
+                  const void* zero_page, hipStream_t st);
 void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                 const void* zero_page, hipStream_t st);
 // pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish in one launch (bf16, epi.mode = EPI_GLU_DW,

@@ -352,7 +352,10 @@ WsLayout ws_layout_core(const cfm_encoder* h, int B, int T1, int T2, bool front)
   long off = 0;
   auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(bytes, 256) + 256; return o; };
   const long M = w.M;
-  w.X1 = front ? take((long)B * w.T1 * h->F1 * h->C * es) : -1;
+  // the fused conv.0 + conv.2 kernel needs no X1 image, only its per-pixel input patches
+  w.X1 = !front ? -1
+       : (h->fuse_conv12 && conv12_supported(h->dtype, h->C)) ? take((long)conv12_patch_bytes(B, w.T1, h->F1, h->C))
+                                          : take((long)B * w.T1 * h->F1 * h->C * es);
   w.X2 = front ? take((long)B * w.T2 * h->F2 * h->C * es) : -1;
   w.X = take(M * h->d * 4);
   w.Hn = take(M * h->d * es);
@@ -448,6 +451,7 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     h->ln_fold = h->dtype == DT_BF16 && h->d % 4 == 0;
     if (const char* lf = getenv("CFM_LN_FOLD")) h->ln_fold = atoi(lf) != 0 && h->d % 4 == 0;
     if (const char* gd = getenv("CFM_GLU_DW")) h->fuse_glu_dw = atoi(gd) != 0;
+    if (const char* cc = getenv("CFM_CONV12")) h->fuse_conv12 = atoi(cc) != 0;
     ensure_streams(h.get(), 8);
     HIP_OK(hipSetDevice(prev));
     *out = h.release();
@@ -782,9 +786,14 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
     const int32_t* lens = out_len_b;
 
     // ConvSubsampling (subsampling.py:163-176) + xscale (multi_head_attention.py:305-306)
-    TM(ST_CONV1);
-    conv1_subsample(dt, x_bft, B, h->F, T, Wf(h->conv1_w), Wf(h->conv1_b), h->C, ws + wl.X1, st);
-    {
+    if (h->fuse_conv12 && conv12_supported(dt, h->C)) {
+      // conv.0 + ReLU recomputed inside conv.2's implicit GEMM: no X1 image
+      TM(ST_CONV2);
+      conv12_fused(x_bft, B, h->F, T, wl.T1, h->F1, wl.T2, h->F2, Wf(h->conv1_w), Wf(h->conv1_b), h->C,
+                   W(h->conv2_w), (int)h->kpad(9 * h->C), Wf(h->conv2_b), ws + wl.X2, ws + wl.X1, h->zero_page, st);
+    } else {
+      TM(ST_CONV1);
+      conv1_subsample(dt, x_bft, B, h->F, T, Wf(h->conv1_w), Wf(h->conv1_b), h->C, ws + wl.X1, st);
       TM(ST_CONV2);
       ConvGeom g{ws + wl.X1, wl.T1, h->F1, wl.T2, h->F2, h->C};
       GemmEpi e = epi_of(EPI_RELU, Wf(h->conv2_b));

@@ -1028,6 +1028,250 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv1 -> conv2 fused (ConvSubsampling conv.0 + ReLU + conv.2 + ReLU, subsampling.py:105-116, 173):
+// the 8-phase implicit GEMM above with its A operand COMPUTED instead of loaded.  A[m][tap*C + c] =
+// X1[b][t1][f1][c] = ReLU(b1[c] + sum_k W1[c][k] * x[b][2f1-1+e][2t1-1+a]), k = 3a + e, at the conv2 input
+// pixel (t1, f1) = (2t2-1+kt, 2f2-1+kf) of output row m = (b, t2, f2) (zero outside the X1 image), so the
+// 655 MB X1 image of the two-kernel path is never written nor re-read.
+//   * A pre-pass (conv12_patch_kernel) writes every conv2-input pixel's 3x3 input patch (36 B + flag) and
+//     conv1's weights as [k][c] rows; a chunk's weights are wave-uniform, so they come in by scalar loads.
+//   * Wave w computes the A chunks of rows (w>>1)*64 + lane for the 16 channels (w & 1)*16 .. +15 of
+//     every K-half (two 8-channel chunks); each lane keeps the 3x3 input patch of its row for the current
+//     conv2 tap in registers, reloaded when the schedule reaches the next tap (x is L1 / L2 resident).
+//   * Schedule (per K-tile kt, R phases): R_0 chunk 1 of half (kt+1, 0), R_1 / R_2 chunks 0 / 1 of half
+//     (kt+1, 1), R_3 chunk 0 of half (kt+2, 0) - the same slots the DMA version fills, so every write
+//     lands >= 2 barriers after the last read of its region and >= 4 phases before its first read.
+//     The B operand (W2) keeps its LDS-DMA loads (2 per thread per K-half).
+//   * The X1 values are computed with conv1_kernel's exact fma order and rounding, so the output is
+//     bitwise the two-kernel path's (tests/test_gpu_encoder.py).
+// ---------------------------------------------------------------------------------------------
+struct Conv12Args {
+  const float4* patch;  // conv12_patch_kernel's (B, T1+2, F1+2) x 12 floats: 3x3 input patch + in-image flag
+  const float* w1t;     // conv.0.weight as [k][c] (k < 9) + conv.0.bias as row 9, fp32
+  const char* zero;     // zero page: B loads past the last K-tile
+  int T1, F1, T2, F2, C;
+};
+
+// Per conv2-input pixel (b, t1, f1), t1 in [-1, T1], f1 in [-1, F1] (conv2's zero-padding ring
+// included): the 3x3 conv1 input patch x[b][2f1-1+e][2t1-1+a] at [3a + e] (zero where conv1 pads),
+// [9] = 1 inside the X1 image, 0 on the ring; 12 floats (3 x 16 B) per pixel.
+__global__ __launch_bounds__(256) void conv12_patch_kernel(const float* __restrict__ x, int B, int F, int T, int T1,
+                                                           int F1, float4* __restrict__ patch, const float* __restrict__ w1,
+                                                           const float* __restrict__ b1, int C, float* __restrict__ w1t) {
+  const int W = F1 + 2, Hh = T1 + 2;
+  const long n = (long)B * Hh * W;
+  if (blockIdx.x == 0)   // conv1 weights as [k][c] rows (+ the bias row): wave-uniform scalar loads in conv12_kernel
+    for (int i = threadIdx.x; i < 10 * C; i += 256) {
+      const int k = i / C, c = i - k * C;
+      w1t[i] = k < 9 ? w1[(long)c * 9 + k] : b1[c];
+    }
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int fi = (int)(i % W);
+    const long r = i / W;
+    const int ti = (int)(r % Hh), b = (int)(r / Hh);
+    const int t1 = ti - 1, f1 = fi - 1;
+    const bool ok = t1 >= 0 && t1 < T1 && f1 >= 0 && f1 < F1;
+    float v[12];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int t = 2 * t1 - 1 + a, f = 2 * f1 - 1 + e;
+        v[3 * a + e] = (ok && t >= 0 && t < T && f >= 0 && f < F) ? x[((long)b * F + f) * T + t] : 0.0f;
+      }
+    v[9] = ok ? 1.0f : 0.0f;
+    v[10] = v[11] = 0.0f;
+    patch[3 * i] = make_float4(v[0], v[1], v[2], v[3]);
+    patch[3 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
+    patch[3 * i + 2] = make_float4(v[8], v[9], v[10], v[11]);
+  }
+}
+constexpr int C12_MAXC = 1024;
+
+__global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int C = ca.C;
+
+  const int nblocks = p.Mtiles * p.Ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
+  const int m0 = mt * 256, n0 = ntl * 256;
+
+
+  // B staging (W2 rows): as gemm8_kernel
+  int rows[2], lo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rows[i] = (i * 8 + wave) * 16 + (lane >> 2);
+    lo[i] = ((lane & 3) ^ g8_swz(rows[i])) * 16;
+  }
+  const char* wrow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) wrow[i] = p.W + (long)(n0 + rows[i]) * p.ldw_b + lo[i];
+  const char* zsrc = ca.zero + lane * 16;
+  const uint32_t sbase = lds_addr(smem);
+  const int nk = p.kb / 128;
+
+  // A computation: this lane's row and its 16-channel group (two 8-channel chunks)
+  const int arow = (wave >> 1) * 64 + lane;
+  const int cgrp = (wave & 1) * 16;
+  const int am = m0 + arow;
+  const bool arow_ok = am < p.M;
+  const int amc = min(am, p.M - 1);
+  const int af2 = amc % ca.F2, bt = amc / ca.F2;
+  const int at2 = bt % ca.T2, ab = bt / ca.T2;
+  // this row's conv2-input pixel (2t2-1, 2f2-1) = padded-grid entry (2t2, 2f2); a tap adds (kt, kf)
+  const float4* prow = ca.patch + 3 * (((long)ab * (ca.T1 + 2) + 2 * at2) * (ca.F1 + 2) + 2 * af2);
+  float pcur[9];
+  int ptap = 0;
+  bool pok = false;
+  auto load_patch = [&](int tap) {
+    const int kt2 = tap / 3, kf2 = tap - 3 * (tap / 3);
+    const float4* q = prow + 3 * (kt2 * (ca.F1 + 2) + kf2);
+    const float4 u0 = q[0], u1 = q[1], u2 = q[2];
+    pcur[0] = u0.x; pcur[1] = u0.y; pcur[2] = u0.z; pcur[3] = u0.w;
+    pcur[4] = u1.x; pcur[5] = u1.y; pcur[6] = u1.z; pcur[7] = u1.w;
+    pcur[8] = u2.x;
+    pok = arow_ok && u2.y != 0.0f;
+  };
+  load_patch(0);
+
+  // K-half (kt, h): K elements [kt*64 + 32h, +32) = tap (kt*64 + 32h) / C, channels c0 .. c0+31
+  auto compute_chunk = [&](int kt, int h, int j) {
+    __builtin_amdgcn_sched_barrier(0);   // keep the chunk's arithmetic inside its R phase
+    const int kel = kt * 64 + 32 * h;
+    const int c0 = kel - ptap * C + cgrp + 8 * j;   // this chunk's first channel (C % 64 == 0: one tap per K-tile)
+    // the chunk's 8 channels are the same for every lane of the wave: weights by scalar loads (SGPRs)
+    typedef const __attribute__((address_space(4))) f32x4 cfloat4;   // constant address space: s_load_dwordx4
+    cfloat4* wk = (cfloat4*)(ca.w1t + __builtin_amdgcn_readfirstlane(c0));   // c0 % 8 == 0: 32-byte aligned
+    const int C4 = C / 4;
+    uint32_t packed[4];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {   // 4 channels at a time
+      float acc4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const f32x4 w = wk[k * C4 + half];
+        acc4[0] = fmaf(w[0], pcur[k], acc4[0]); acc4[1] = fmaf(w[1], pcur[k], acc4[1]);
+        acc4[2] = fmaf(w[2], pcur[k], acc4[2]); acc4[3] = fmaf(w[3], pcur[k], acc4[3]);
+      }
+      const f32x4 bv = wk[9 * C4 + half];
+      const bool live = pok && kt < nk;
+      const float o0 = live ? fmaxf(acc4[0] + bv[0], 0.0f) : 0.0f, o1 = live ? fmaxf(acc4[1] + bv[1], 0.0f) : 0.0f;
+      const float o2 = live ? fmaxf(acc4[2] + bv[2], 0.0f) : 0.0f, o3 = live ? fmaxf(acc4[3] + bv[3], 0.0f) : 0.0f;
+      packed[2 * half] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+      packed[2 * half + 1] = (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16);
+    }
+    // 16-byte slot (cgrp / 8 + j) of row arow in the K-half image, XOR-swizzled as the DMA fills it
+    char* img = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const int slot = (cgrp / 8 + j) ^ g8_swz(arow);
+    *(uint4*)(img + arow * 64 + slot * 16) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto issue_b = [&](int kt, int h) {   // K-half h of K-tile kt of W2: 2 glds
+    const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const bool live = kt < nk;
+    const int kb0 = kt * 128 + h * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int fslot = (fc ^ g8_swz(fr)) * 16;
+  uint4 af[4], bfr[4];
+  auto read_frags = [&](int kt, int q) {
+    const char* hb = smem + (kt & 1) * G8_BUF + (q >> 1) * 2 * G8_HALF;
+    const int r0 = wm * 128 + (q & 1) * 64 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const uint4*)(hb + (r0 + i * 16) * 64 + fslot);
+    if ((q & 1) == 0) {
+      const int c0 = wn * 64 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *(const uint4*)(hb + G8_HALF + (c0 + j * 16) * 64 + fslot);
+    }
+  };
+
+  // prologue: halves (0,0), (0,1), (1,0) of A computed, of B loaded
+  issue_b(0, 0);
+  issue_b(0, 1);
+  issue_b(1, 0);
+  compute_chunk(0, 0, 0); compute_chunk(0, 0, 1);
+  compute_chunk(0, 1, 0); compute_chunk(0, 1, 1);
+  compute_chunk(1, 0, 0);
+  wait_vmcnt<4>();
+  wait_lgkm0();
+  raw_barrier();
+  if (wm == 1) raw_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // R_q
+      read_frags(kt, q);
+      if (q == 0) compute_chunk(kt + 1, 0, 1);
+      if (q == 1) { issue_b(kt + 1, 1); compute_chunk(kt + 1, 1, 0); }
+      if (q == 2) compute_chunk(kt + 1, 1, 1);
+      if (q == 3) {
+        issue_b(kt + 2, 0);
+        if (((kt + 2) * 64) % C == 0) {   // K-tile kt+2 starts the next conv2 tap: its input patch
+          ptap = (kt + 2) * 64 / C;
+          if (ptap < 9) load_patch(ptap);
+        }
+        compute_chunk(kt + 2, 0, 0);
+      }
+      if (wm == 1 && (q & 1)) wait_vmcnt<4>();
+      raw_barrier();
+      // M_q
+      wait_lgkm0();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[(q & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), acc[(q & 1) * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0 && (q & 1)) wait_vmcnt<4>();
+      raw_barrier();
+    }
+  }
+  if (wm == 0) raw_barrier();
+  wait_vmcnt<0>();
+  wait_lgkm0();
+  raw_barrier();
+
+  float* img = (float*)smem;
+  float bcol[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bcol[j] = p.epi.bias ? p.epi.bias[n0 + wn * 64 + j * 16 + fr] : 0.0f;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            img[(i * 16 + fc * 4 + e) * T8::EPS + wn * 64 + j * 16 + fr] = acc[i][j][e] + bcol[j];
+    }
+    __syncthreads();
+    epilogue<bf16_t, EPI_RELU, EpiView<T8>, false>(p, img, m0 + pass * 128, n0, 0, nullptr, nullptr);
+  }
+}
+
 template <typename T, class TL, template <int> class AL, class ALArgs>
 void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   using ALoad = AL<TL::GA>;
@@ -1289,6 +1533,41 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
   int tile = pick_tile(dtype, M, N, epi.mode, true);
   if (dtype == DT_F32) dispatch<float, ALoadConv>(tile, p, a, st);
   else dispatch<bf16_t, ALoadConv>(tile, p, a, st);
+}
+
+bool conv12_supported(int dtype, int C) {
+  return dtype == DT_BF16 && C > 0 && C <= C12_MAXC && C % 128 == 0 && g_tile_override < 0;
+}
+
+size_t conv12_patch_bytes(int B, int T1, int F1, int C) {
+  return (size_t)B * (T1 + 2) * (F1 + 2) * 48 + 256 + (size_t)10 * C * 4;
+}
+
+// conv.0 + ReLU + conv.2 + ReLU: x (B, F, T) fp32 -> X2 (B, T2, F2, C) bf16; `patch` is scratch of
+// conv12_patch_bytes(B, T1, F1) bytes
+void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T2, int F2, const float* w1,
+                  const float* b1, int C, const void* Wp, int Kpad, const float* b2, void* X2, void* patch,
+                  const void* zero_page, hipStream_t st) {
+  const int M = B * T2 * F2;
+  if (M <= 0) return;
+  if (!conv12_supported(DT_BF16, C)) fail(CFM_ERR_UNSUPPORTED, "conv12_fused: bf16, C % 128 == 0, C <= 1024");
+  const long npix = (long)B * (T1 + 2) * (F1 + 2);
+  float* w1t = (float*)((char*)patch + ((npix * 48 + 255) / 256) * 256);
+  cfm_launch(conv12_patch_kernel, dim3((unsigned)std::min<long>((npix + 255) / 256, 4096)), dim3(256), 0, st, x_bft, B,
+             F, T, T1, F1, (float4*)patch, w1, b1, C, w1t);
+  GemmEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.mode = EPI_RELU;
+  e.bias = b2;
+  e.alpha = 1.0f;
+  e.C = X2;
+  e.ldc = C;
+  GemmParams p = make_params(2, M, Wp, Kpad, C, e);
+  p.probe = 0;
+  p.Mtiles = (M + 255) / 256;
+  p.Ntiles = (C + 255) / 256;
+  Conv12Args a{(const float4*)patch, w1t, (const char*)zero_page, T1, F1, T2, F2, C};
+  cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
 }
 
 bool gemm_tconv_supported(int dtype, int C) { return C > 0 && ((long)C * dtype_size(dtype)) % 128 == 0; }

@@ -221,3 +221,26 @@ def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
     d = rel_l2(out["1"][0], out["0"][0])
     print(f"bf16 relL2 vs reference: fused {out['1'][1]:.3e}, unfused {out['0'][1]:.3e}; fused vs unfused {d:.3e}")
     assert d <= 1e-2, f"fused vs unfused relL2 {d:.3e}"
+
+
+@pytest.mark.parametrize("B,T", [(2, 333), (32, 1000)])
+def test_bf16_fused_conv12_matches_two_kernels(B, T, monkeypatch):
+    """ConvSubsampling's conv.0 recomputed inside conv.2's implicit GEMM (conv12_fused, CFM_CONV12=1)
+    against the two-kernel path (the default: conv1_kernel writes X1, the 8-phase GEMM reads it): the X1 values
+    are computed with the same fma order and bf16 rounding and the MFMA order is unchanged, so the
+    encoder output is bitwise identical.  B=32 x T=1000 is the north-star shape; T=333 has ragged
+    image borders (odd T1 / T2) and a padded last M tile."""
+    z = np.load(os.path.join(GOLDEN, "enc_large17.npz"))
+    cfg = dict(json.loads(str(z["cfg_json"])), n_layers=2)
+    sd = {k: v for k, v in make_state_dict(json.loads(str(z["cfg_json"])), int(z["seed"])).items()
+          if not k.startswith("layers.") or k.split(".")[1] in ("0", "1")}
+    g = torch.Generator().manual_seed(B + T)
+    x = torch.randn(B, 80, T, generator=g).numpy()
+    lens = np.array([T - (7 * i) % (T // 2) for i in range(B)], dtype=np.int64)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_CONV12", flag)
+        out[flag] = run(native(cfg, "bf16"), sd, x, lens)
+    assert (out["1"][1] == out["0"][1]).all()
+    assert np.isfinite(out["1"][0]).all()
+    assert np.array_equal(out["1"][0], out["0"][0]), f"max diff {np.abs(out['1'][0] - out['0'][0]).max():.3e}"
