@@ -40,7 +40,8 @@ TRAIN_SYMBOLS = (
 # every symbol include/cfm_joint.h declares
 JOINT_SYMBOLS = (
     "cfm_rnnt_joint_create", "cfm_rnnt_joint_destroy", "cfm_rnnt_joint_set_weights", "cfm_rnnt_joint_workspace_size",
-    "cfm_rnnt_joint_forward",
+    "cfm_rnnt_joint_forward", "cfm_rnnt_joint_forward_train", "cfm_rnnt_joint_backward_workspace_size",
+    "cfm_rnnt_joint_backward",
 )
 # every symbol include/cfm_stream.h declares
 STREAM_SYMBOLS = ("cfm_frame_buffer_step",)
@@ -54,7 +55,9 @@ AUGMENT_SYMBOLS = ("cfm_spec_mask_rects", "cfm_spec_shot")
 # every symbol include/cfm_rnnt_decode.h declares (bound in conformer_amd/rnnt_decode.py)
 RNNT_DECODE_SYMBOLS = ("cfm_rnnt_decoder_create", "cfm_rnnt_decoder_destroy", "cfm_rnnt_decoder_set_weights",
                        "cfm_rnnt_decoder_predict_workspace_size", "cfm_rnnt_decoder_predict",
-                       "cfm_rnnt_greedy_workspace_size", "cfm_rnnt_greedy_decode")
+                       "cfm_rnnt_greedy_workspace_size", "cfm_rnnt_greedy_decode", "cfm_rnnt_decoder_train_tape_size",
+                       "cfm_rnnt_decoder_train_forward", "cfm_rnnt_decoder_backward_workspace_size",
+                       "cfm_rnnt_decoder_backward")
 # every symbol include/cfm_comm.h declares (bound in conformer_amd/comm.py)
 COMM_SYMBOLS = ("cfm_comm_get_unique_id", "cfm_comm_init", "cfm_comm_destroy", "cfm_comm_world", "cfm_allreduce_grads",
                 "cfm_comm_allreduce_cb", "cfm_grad_buckets_create", "cfm_grad_buckets_ready_cb",
@@ -159,6 +162,10 @@ def load() -> ctypes.CDLL:
         "cfm_rnnt_joint_set_weights": (ci, [vp, vp, vp, vp, vp, vp, vp, vp]),
         "cfm_rnnt_joint_workspace_size": (sz, [vp, ci, ci, ci]),
         "cfm_rnnt_joint_forward": (ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, sz, vp]),
+        "cfm_rnnt_joint_forward_train": (ci, [vp, vp, vp, ci, ci, ci, ctypes.c_float, ctypes.c_uint64, vp, vp, sz, vp]),
+        "cfm_rnnt_joint_backward_workspace_size": (sz, [vp, ci, ci, ci]),
+        "cfm_rnnt_joint_backward": (ci, [vp, vp, vp, ci, ci, ci, ctypes.c_float, ctypes.c_uint64, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_frame_buffer_step": (ci, [vp, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, vp, vp]),
         "cfm_mel_create": (ci, [ctypes.POINTER(CfmMelCfg), ci, ctypes.POINTER(vp)]),
         "cfm_mel_destroy": (None, [vp]),

@@ -29,6 +29,11 @@ def _bind(lib) -> None:
             ("cfm_rnnt_decoder_predict_workspace_size", sz, [vp, ci, ci]),
             ("cfm_rnnt_decoder_predict", ci, [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, sz, vp]),
             ("cfm_rnnt_greedy_workspace_size", sz, [vp, ci, ci, ci]),
+            ("cfm_rnnt_decoder_train_tape_size", sz, [vp, ci, ci, ci]),
+            ("cfm_rnnt_decoder_train_forward", ci, [vp, vp, ci, ci, ci, ctypes.c_float, ctypes.c_uint64, vp, vp, sz, vp]),
+            ("cfm_rnnt_decoder_backward_workspace_size", sz, [vp, ci, ci, ci]),
+            ("cfm_rnnt_decoder_backward", ci, [vp, vp, ci, ci, ci, ctypes.c_float, ctypes.c_uint64, vp, vp, pp, pp, vp, pp,
+                                               pp, pp, pp, vp, sz, vp]),
             ("cfm_rnnt_greedy_decode", ci, [vp, vp, vp, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, vp, vp,
                                             vp, vp, vp, vp, vp, sz, vp])):
         fn = getattr(lib, name)
@@ -104,6 +109,52 @@ class NativePredictionNet:
             None if hs is None else hs.data_ptr(), None if cs is None else cs.data_ptr(), g.data_ptr(), h.data_ptr(),
             c.data_ptr(), ws.data_ptr(), ws.numel(), self._stream()), "cfm_rnnt_decoder_predict")
         return g, (h, c)
+
+    # ---- training (cfm_rnnt_decoder_train_forward / _backward) ---------------------------------
+    def train_forward(self, y: torch.Tensor, add_sos: bool, dropout: float, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Teacher-forced g (B, S, H) from the zero state, plus the tape the backward needs."""
+        y = y.to(self.device, torch.int64).contiguous()
+        B, U = y.shape
+        S = U + (1 if add_sos else 0)
+        g = torch.empty((B, S, self.H), dtype=torch.float32, device=self.device)
+        n = int(self.lib.cfm_rnnt_decoder_train_tape_size(self.handle, B, U, 1 if add_sos else 0))
+        tape = torch.empty(n, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.cfm_rnnt_decoder_train_forward(self.handle, y.data_ptr(), B, U, 1 if add_sos else 0,
+                                                           ctypes.c_float(dropout), ctypes.c_uint64(seed), g.data_ptr(),
+                                                           tape.data_ptr(), n, self._stream()),
+                   "cfm_rnnt_decoder_train_forward")
+        return g, tape
+
+    def backward(self, y: torch.Tensor, add_sos: bool, dropout: float, seed: int, tape: torch.Tensor, dg: torch.Tensor,
+                 w_ih: List[torch.Tensor], w_hh: List[torch.Tensor], want: Sequence[bool]):
+        """(d_embed, [dw_ih], [dw_hh], [db_ih], [db_hh]); `want` = (embed, w_ih, w_hh, b_ih, b_hh)."""
+        y = y.to(self.device, torch.int64).contiguous()
+        B, U = y.shape
+        dg = dg.detach().to(self.device, torch.float32).contiguous()
+        f = lambda t: t.detach().to(self.device, torch.float32).contiguous()  # noqa: E731
+        wi, wh = [f(t) for t in w_ih], [f(t) for t in w_hh]
+        z = lambda shape, on: [torch.empty(shape, device=self.device) for _ in range(self.L)] if on else None  # noqa: E731
+        demb = torch.empty((self.V + 1, self.H), device=self.device) if want[0] else None
+        dwi = z((4 * self.H, self.H), want[1])
+        dwh = z((4 * self.H, self.H), want[2])
+        dbi = z((4 * self.H,), want[3] or want[4])
+        dbh = z((4 * self.H,), want[4])
+        n = int(self.lib.cfm_rnnt_decoder_backward_workspace_size(self.handle, B, U, 1 if add_sos else 0))
+        ws = self._workspace(n)
+        keep = []
+
+        def arr(ts):
+            if ts is None:
+                return None
+            p, a = _ptrs(ts)
+            keep.append(a)
+            return p
+        pwi, pwh = arr(wi), arr(wh)
+        _lib.check(self.lib.cfm_rnnt_decoder_backward(
+            self.handle, y.data_ptr(), B, U, 1 if add_sos else 0, ctypes.c_float(dropout), ctypes.c_uint64(seed),
+            tape.data_ptr(), dg.data_ptr(), pwi, pwh, None if demb is None else demb.data_ptr(), arr(dwi), arr(dwh),
+            arr(dbi), arr(dbh), ws.data_ptr(), n, self._stream()), "cfm_rnnt_decoder_backward")
+        return demb, dwi, dwh, (dbi if want[3] else None), dbh
 
     def greedy(self, enc_bdt: torch.Tensor, enc_len: torch.Tensor, joint_params: Sequence[torch.Tensor],
                activation: str, max_symbols: int, log_normalize: bool, sos_until_label: bool = False):

@@ -80,6 +80,21 @@ __device__ __forceinline__ float drop_mul(const Drop& d, uint64_t e) {
   return h >= d.thr ? d.scale : 0.0f;
 }
 
+// host: keep(e) iff hash(seed, site, e) >= thr, thr = p * 2^32; kept values scaled by 1/(1-p)
+inline uint32_t host_mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+inline Drop make_drop(float p, uint64_t seed, int site) {
+  Drop d{0u, 0u, 1.0f};
+  if (p <= 0.0f) return d;
+  const double t = (p < 1.0f ? (double)p : 1.0) * 4294967296.0;
+  d.thr = (uint32_t)(t > 4294967295.0 ? 4294967295.0 : (t < 1.0 ? 1.0 : t));
+  d.key = host_mix32((uint32_t)seed ^ host_mix32((uint32_t)(seed >> 32) + 0x632be5abu * (uint32_t)site));
+  d.scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
+  return d;
+}
+
 struct GemmEpi {
   int mode;
   const float* bias;   // [Npad] fp32 (may be null)

@@ -14,6 +14,8 @@
 #include <cstring>
 
 #include "../../include/cfm_joint.h"
+#include "../../include/cfm_train.h"
+#include <string>
 #include "cfm_abi.h"
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(256) void bdl_to_rows_kernel(const float* __restric
 template <typename TO>
 __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restrict__ f, const float* __restrict__ g,
                                                            int B, int T, int U, int H, int Hp, int act,
-                                                           TO* __restrict__ out) {
+                                                           TO* __restrict__ out, Drop drop) {
   const int HG = Hp / 8;
   const long n = (long)B * T * U * HG;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
       if (act == CFM_JOINT_RELU) x = fmaxf(x, 0.0f);
       else if (act == CFM_JOINT_SIGMOID) x = 1.0f / (1.0f + expf(-x));
       else x = tanhf(x);
-      v[j] = h < H ? x : 0.0f;
+      v[j] = h < H ? x * drop_mul(drop, (uint64_t)row * H + h) : 0.0f;   // joint_net's Dropout (training)
     }
     TO* o = out + row * Hp + hg * 8;
     if constexpr (sizeof(TO) == 2) {
@@ -129,6 +131,72 @@ GemmEpi epi_f32(const float* bias, float* X, long ldx, int scalar) {
   e.ldx = ldx;
   e.out_scalar = scalar;
   return e;
+}
+
+// dz[(b,t,u)][j] = dh * dropout'(row, j) * act'(z), z = f[b,t][j] + g[b,u][j]; reduced over u (per (b, t))
+__device__ __forceinline__ float act_grad(int act, float z) {
+  if (act == CFM_JOINT_RELU) return z > 0.0f ? 1.0f : 0.0f;
+  if (act == CFM_JOINT_SIGMOID) { const float s = 1.0f / (1.0f + expf(-z)); return s * (1.0f - s); }
+  const float t = tanhf(z);
+  return 1.0f - t * t;
+}
+__global__ __launch_bounds__(256) void joint_act_bwd_t_kernel(const float* __restrict__ f, const float* __restrict__ g,
+                                                              const float* __restrict__ dh, int B, int T, int U, int H,
+                                                              int act, Drop drop, float* __restrict__ df) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const long bt = blockIdx.y;
+  if (j >= H) return;
+  const int b = (int)(bt / T);
+  const float fv = f[bt * H + j];
+  float s = 0.0f;
+  for (int u = 0; u < U; ++u) {
+    const long row = bt * U + u;
+    const float z = fv + g[((long)b * U + u) * H + j];
+    s += dh[row * H + j] * drop_mul(drop, (uint64_t)row * H + j) * act_grad(act, z);
+  }
+  df[bt * H + j] = s;
+}
+// ... reduced over t (per (b, u))
+__global__ __launch_bounds__(256) void joint_act_bwd_u_kernel(const float* __restrict__ f, const float* __restrict__ g,
+                                                              const float* __restrict__ dh, int B, int T, int U, int H,
+                                                              int act, Drop drop, float* __restrict__ dp) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const long bu = blockIdx.y;
+  if (j >= H) return;
+  const int b = (int)(bu / U), u = (int)(bu % U);
+  const float gv = g[bu * H + j];
+  float s = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    const long row = ((long)b * T + t) * U + u;
+    const float z = f[((long)b * T + t) * H + j] + gv;
+    s += dh[row * H + j] * drop_mul(drop, (uint64_t)row * H + j) * act_grad(act, z);
+  }
+  dp[bu * H + j] = s;
+}
+
+struct JBWs { long er, dr, fp, gp, hid, dh, df, dp, dx, lin, total; };
+JBWs jbws(const cfm_rnnt_joint* h, int B, int T, int U) {
+  JBWs w;
+  long off = 0;
+  auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(std::max(bytes, 1L), 256); return o; };
+  const long rows = (long)B * T * U;
+  const int mode = h->dtype == DT_F32 ? CFM_COMPUTE_FP32 : CFM_COMPUTE_BF16;
+  w.er = take((long)B * T * h->H1 * 4);
+  w.dr = take((long)B * U * h->H2 * 4);
+  w.fp = take((long)B * T * h->H * 4);
+  w.gp = take((long)B * U * h->H * 4);
+  w.hid = take(rows * h->H * 4);
+  // dh also holds the compute-type projection inputs before it is written
+  w.dh = take(std::max(rows * h->H * 4, (long)B * T * h->kp(h->H1) * h->es + (long)B * U * h->kp(h->H2) * h->es + 512));
+  w.df = take((long)B * T * h->H * 4);
+  w.dp = take((long)B * U * h->H * 4);
+  w.dx = take((long)std::max(B * T * h->H1, B * U * h->H2) * 4);
+  const size_t l1 = cfm_op_linear_backward_ws_size(mode, (int)rows, h->H, h->C);
+  const size_t l2 = cfm_op_linear_backward_ws_size(mode, B * T, h->H1, h->H);
+  const size_t l3 = cfm_op_linear_backward_ws_size(mode, B * U, h->H2, h->H);
+  w.lin = take((long)std::max(l1, std::max(l2, l3)));
+  w.total = round_up(off, 256);
+  return w;
 }
 
 }  // namespace
@@ -214,9 +282,12 @@ size_t cfm_rnnt_joint_workspace_size(const cfm_rnnt_joint* h, int B, int T, int 
   return (size_t)jws(h, B, T, U).total;
 }
 
-cfm_status cfm_rnnt_joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T, int U,
-                                  int log_softmax, float* out, void* workspace, size_t workspace_bytes, void* stream) {
-  return guarded([&] {
+}  // extern "C"
+
+namespace {
+// RNNTJoint.joint (rnnt.py:951-1008) with joint_net's Dropout as `drop` (training; none in eval)
+void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T, int U, int log_softmax,
+                   float* out, void* workspace, size_t workspace_bytes, hipStream_t stream, Drop drop) {
     if (!h || !enc_bdt || !dec_bdu || !out) fail(CFM_ERR_INVALID_ARG, "null argument");
     if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
     if (B <= 0 || T <= 0 || U <= 0) fail(CFM_ERR_INVALID_ARG, "B, T and U must be positive");
@@ -224,7 +295,7 @@ cfm_status cfm_rnnt_joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const
     if (rows > 0x7fffffffL) fail(CFM_ERR_UNSUPPORTED, "B*T*U exceeds 2^31 rows");
     const JWs w = jws(h, B, T, U);
     if (!workspace || workspace_bytes < (size_t)w.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
-    hipStream_t st = (hipStream_t)stream;
+    hipStream_t st = stream;
     char* ws = (char*)workspace;
     const int dt = h->dtype;
     const int H1p = (int)h->kp(h->H1), H2p = (int)h->kp(h->H2);
@@ -251,14 +322,121 @@ cfm_status cfm_rnnt_joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const
     const long nh = rows * (Hp / 8);
     if (dt == DT_F32)
       cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
-                 T, U, h->H, Hp, h->act, (float*)(ws + w.hid));
+                 T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop);
     else
       cfm_launch(joint_hidden_kernel<bf16_t>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp,
-                 B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid));
+                 B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop);
     gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), h->C,
          epi_f32((const float*)(h->wbuf + h->b_out), out, h->C, h->C % 4 ? 1 : 0), h->zero, st);
     if (log_softmax)
       cfm_launch(row_log_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, out, rows, h->C);
+    HIP_OK(hipGetLastError());
+}
+}  // namespace
+
+extern "C" {
+
+cfm_status cfm_rnnt_joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T, int U,
+                                  int log_softmax, float* out, void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    joint_forward(h, enc_bdt, dec_bdu, B, T, U, log_softmax, out, workspace, workspace_bytes, (hipStream_t)stream,
+                  Drop{0u, 0u, 1.0f});
+  });
+}
+
+cfm_status cfm_rnnt_joint_forward_train(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T,
+                                        int U, float dropout, uint64_t seed, float* out, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    joint_forward(h, enc_bdt, dec_bdu, B, T, U, 0, out, workspace, workspace_bytes, (hipStream_t)stream,
+                  make_drop(dropout, seed, 1));
+  });
+}
+
+size_t cfm_rnnt_joint_backward_workspace_size(const cfm_rnnt_joint* h, int B, int T, int U) {
+  if (!h || B <= 0 || T <= 0 || U <= 0) return 0;
+  return (size_t)jbws(h, B, T, U).total;
+}
+
+cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu, int B, int T, int U,
+                                   float dropout, uint64_t seed, const float* dlogits, const float* w_enc,
+                                   const float* w_pred, const float* w_out, float* d_enc_bdt, float* d_dec_bdu,
+                                   float* dw_enc, float* db_enc, float* dw_pred, float* db_pred, float* dw_out,
+                                   float* db_out, void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    if (!h || !enc_bdt || !dec_bdu || !dlogits || !w_enc || !w_pred || !w_out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
+    if (B <= 0 || T <= 0 || U <= 0) fail(CFM_ERR_INVALID_ARG, "B, T and U must be positive");
+    const long rows = (long)B * T * U;
+    if (rows > 0x7fffffffL) fail(CFM_ERR_UNSUPPORTED, "B*T*U exceeds 2^31 rows");
+    if (h->H % 4 || h->H1 % 4 || h->H2 % 4) fail(CFM_ERR_UNSUPPORTED, "joint backward: hidden sizes must be multiples of 4");
+    const JBWs w = jbws(h, B, T, U);
+    if (!workspace || workspace_bytes < (size_t)w.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    HIP_OK(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    const int dt = h->dtype, mode = dt == DT_F32 ? CFM_COMPUTE_FP32 : CFM_COMPUTE_BF16;
+    const int H = h->H, H1 = h->H1, H2 = h->H2, C = h->C;
+    const Drop drop = make_drop(dropout, seed, 1);
+    float* er = (float*)(ws + w.er);   // encoder rows (B*T, H1) fp32
+    float* dr = (float*)(ws + w.dr);   // decoder rows (B*U, H2) fp32
+    float* fp = (float*)(ws + w.fp);
+    float* gp = (float*)(ws + w.gp);
+    float* hid = (float*)(ws + w.hid);
+    float* dh = (float*)(ws + w.dh);
+    float* df = (float*)(ws + w.df);
+    float* dp = (float*)(ws + w.dp);
+    float* dxr = (float*)(ws + w.dx);
+    char* lws = ws + w.lin;
+    const size_t lws_bytes = (size_t)(w.total - w.lin);
+    cfm_launch(bdl_to_rows_kernel<float>, dim3((T + 31) / 32, (H1 + 31) / 32, B), dim3(256), 0, st, enc_bdt, H1, T, er, H1);
+    cfm_launch(bdl_to_rows_kernel<float>, dim3((U + 31) / 32, (H2 + 31) / 32, B), dim3(256), 0, st, dec_bdu, H2, U, dr, H2);
+    // the forward's projections and hidden, recomputed (fp32 hidden = the output Linear's input)
+    {
+      const int H1p = (int)h->kp(H1), H2p = (int)h->kp(H2);
+      char* af = (char*)dh;   // scratch: the compute-type rows live in dh until it is written
+      char* ag = af + round_up((long)B * T * H1p * h->es, 256);
+      if (dt == DT_F32) {
+        cfm_launch(bdl_to_rows_kernel<float>, dim3((T + 31) / 32, (H1p + 31) / 32, B), dim3(256), 0, st, enc_bdt, H1, T,
+                   (float*)af, H1p);
+        cfm_launch(bdl_to_rows_kernel<float>, dim3((U + 31) / 32, (H2p + 31) / 32, B), dim3(256), 0, st, dec_bdu, H2, U,
+                   (float*)ag, H2p);
+      } else {
+        cfm_launch(bdl_to_rows_kernel<bf16_t>, dim3((T + 31) / 32, (H1p + 31) / 32, B), dim3(256), 0, st, enc_bdt, H1,
+                   T, (bf16_t*)af, H1p);
+        cfm_launch(bdl_to_rows_kernel<bf16_t>, dim3((U + 31) / 32, (H2p + 31) / 32, B), dim3(256), 0, st, dec_bdu, H2,
+                   U, (bf16_t*)ag, H2p);
+      }
+      gemm(dt, af, H1p, B * T, H1, h->wbuf + h->w_enc, H1p, H, epi_f32((const float*)(h->wbuf + h->b_enc), fp, H, H % 4 ? 1 : 0),
+           h->zero, st);
+      gemm(dt, ag, H2p, B * U, H2, h->wbuf + h->w_pred, H2p, H,
+           epi_f32((const float*)(h->wbuf + h->b_pred), gp, H, H % 4 ? 1 : 0), h->zero, st);
+      const long nh = rows * (H / 8 + (H % 8 ? 1 : 0));
+      if (H % 8 == 0)
+        cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
+                   T, U, H, H, h->act, hid, drop);
+      else
+        fail(CFM_ERR_UNSUPPORTED, "joint backward: joint_hidden must be a multiple of 8");
+    }
+    auto lin_bwd = [&](const float* x, long M, int K, const float* wt, int N, const float* dy, float* dx, float* dw,
+                       float* db) {
+      const size_t need = cfm_op_linear_backward_ws_size(mode, (int)M, K, N);
+      if (need > lws_bytes) fail(CFM_ERR_WORKSPACE, "joint backward: linear workspace");
+      const cfm_status r = cfm_op_linear_backward(mode, x, (int)M, K, wt, N, dy, dx, dw, db, lws, lws_bytes, st);
+      if (r != CFM_OK) fail(r, std::string("joint backward: ") + cfm_last_error());
+    };
+    // joint_net[-1]: logits = hid . W_out^T + b_out
+    lin_bwd(hid, rows, H, w_out, C, dlogits, dh, dw_out, db_out);
+    // dz = dh * dropout mask * act'(z); df = sum over u, dp = sum over t
+    cfm_launch(joint_act_bwd_t_kernel, dim3((H + 255) / 256, B * T), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act, drop,
+               df);
+    cfm_launch(joint_act_bwd_u_kernel, dim3((H + 255) / 256, B * U), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act, drop,
+               dp);
+    // enc / pred Linears
+    lin_bwd(er, (long)B * T, H1, w_enc, H, df, d_enc_bdt ? dxr : nullptr, dw_enc, db_enc);
+    if (d_enc_bdt) transpose_out(dxr, B, T, H1, d_enc_bdt, st);
+    lin_bwd(dr, (long)B * U, H2, w_pred, H, dp, d_dec_bdu ? dxr : nullptr, dw_pred, db_pred);
+    if (d_dec_bdu) transpose_out(dxr, B, U, H2, d_dec_bdu, st);
     HIP_OK(hipGetLastError());
   });
 }

@@ -23,7 +23,10 @@
 #include <vector>
 
 #include "../../include/cfm_rnnt_decode.h"
+#include "../../include/cfm_train.h"
 #include "cfm_abi.h"
+#include "cfm_common.h"
+#include "cfm_kernels.h"
 
 using namespace cfm;
 
@@ -135,7 +138,9 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(const float* __restrict_
                                                         const float* __restrict__ h, const float* __restrict__ c,
                                                         float* __restrict__ h2, float* __restrict__ c2,
                                                         float* __restrict__ gout, long gstride, int B, int I, int H,
-                                                        const int* __restrict__ run_flag) {
+                                                        const int* __restrict__ run_flag,
+                                                        float* __restrict__ gates_out = nullptr, Drop gdrop = Drop{0u, 0u, 1.0f},
+                                                        int gstep = 0) {
   extern __shared__ float lds[];
   const int K = I + H;
   const int b0 = blockIdx.y * RB, nb = min(RB, B - b0);
@@ -174,7 +179,12 @@ __global__ __launch_bounds__(256) void lstm_step_kernel(const float* __restrict_
   const float hn = go * tanhf(cn);
   c2[b * H + j] = cn;
   h2[b * H + j] = hn;
-  if (gout) gout[b * gstride + j] = hn;
+  // LSTMDropout's output Dropout (rnn.py:151-237; training), mask index (b, step, j) of g (B, S, H)
+  if (gout) gout[b * gstride + j] = hn * drop_mul(gdrop, ((uint64_t)b * (gstride / H) + gstep) * H + j);
+  if (gates_out) {   // training tape: post-activation gates [i | f | g | o] of this step
+    float* gr = gates_out + b * 4L * H;
+    gr[j] = gi; gr[H + j] = gf; gr[2 * H + j] = gg; gr[3 * H + j] = go;
+  }
 }
 
 // hid[b][n] = act(F[b, t_b][n] + sum_k h[b][k] Wp[n][k] + bp[n]),  n < J
@@ -488,6 +498,110 @@ GreedyWs greedy_layout(const cfm_rnnt_decoder* d, int B, int T, int J) {
   return w;
 }
 
+// training tape: per layer l and step u, gates (B, 4H), c (B, H), h (B, H); then the step labels
+struct TrainTape {
+  float* base;
+  long B, H, S;
+  int32_t* xlab;
+  float* zero;
+  float* gates(int l, int u) const { return base + ((long)l * S + u) * B * 6 * H; }
+  float* c(int l, int u) const { return gates(l, u) + B * 4 * H; }
+  float* h(int l, int u) const { return gates(l, u) + B * 5 * H; }
+};
+TrainTape train_tape(const cfm_rnnt_decoder* d, char* tape, int B, int S) {
+  TrainTape t;
+  t.base = (float*)tape;
+  t.B = B; t.H = d->H; t.S = S;
+  char* after = tape + (long)d->L * S * B * 6 * d->H * 4;
+  t.xlab = (int32_t*)after;
+  t.zero = (float*)(after + round_up((long)(S + 1) * B * 4, 256));   // (B, H) zeros: the initial state
+  return t;
+}
+struct BwdWs { long dy, dgates, dh, dc, x, hp, lin, total; };
+BwdWs bwd_ws(const cfm_rnnt_decoder* d, int B, int S) {
+  BwdWs w{};
+  long o = 0;
+  auto take = [&](long bytes) { const long at = round_up(o, 256); o = at + round_up(std::max(bytes, 1L), 256); return at; };
+  const long sbh = (long)S * B * d->H * 4;
+  w.dy = take(sbh);
+  w.dgates = take(4 * sbh);
+  w.dh = take((long)B * d->H * 4);
+  w.dc = take((long)B * d->H * 4);
+  w.x = take(sbh);
+  w.hp = take(sbh);
+  w.lin = take((long)cfm_op_linear_backward_ws_size(CFM_COMPUTE_FP32, S * B, d->H, 4 * d->H));
+  w.total = round_up(o, 256);
+  return w;
+}
+
+// dy[u][b][j] = dg[b][u][j] * dropout'(b, u, j)  (LSTMDropout's output dropout)
+__global__ void dg_to_dy_kernel(const float* __restrict__ dg, int B, int S, int H, Drop drop, float* __restrict__ dy) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)S * B * H) return;
+  const int j = (int)(i % H);
+  const long r = i / H;
+  const int b = (int)(r % B), u = (int)(r / B);
+  const uint64_t e = ((uint64_t)b * S + u) * H + j;
+  dy[i] = dg[e] * drop_mul(drop, e);
+}
+
+// LSTM cell backward (gate order i, f, g, o; c = f*c' + i*g, h = o*tanh(c)) for one step:
+// dh = dy + dh_rec (recurrent, in/out: becomes the W_hh . dgates input of the previous step after
+// lstm_hh_bwd), dc (in/out), dgates (B, 4H) pre-activation gradients
+__global__ void lstm_cell_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ gates,
+                                     const float* __restrict__ c, const float* __restrict__ cprev, int B, int H,
+                                     float* __restrict__ dh, float* __restrict__ dc, float* __restrict__ dgates) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * H) return;
+  const int b = i / H, j = i - b * H;
+  const float* gr = gates + (long)b * 4 * H;
+  const float gi = gr[j], gf = gr[H + j], gg = gr[2 * H + j], go = gr[3 * H + j];
+  const float ct = c[i], tc = tanhf(ct);
+  const float dht = dy[i] + dh[i];
+  const float dct = dht * go * (1.0f - tc * tc) + dc[i];
+  float* dgr = dgates + (long)b * 4 * H;
+  dgr[j] = dct * gg * gi * (1.0f - gi);
+  dgr[H + j] = dct * cprev[i] * gf * (1.0f - gf);
+  dgr[2 * H + j] = dct * gi * (1.0f - gg * gg);
+  dgr[3 * H + j] = dht * tc * go * (1.0f - go);
+  dc[i] = dct * gf;
+  dh[i] = 0.0f;   // consumed; lstm_hh_bwd writes the next step's recurrent part
+}
+
+// dh[b][k] = sum_r W_hh[r][k] * dgates[b][r]  (r < 4H; W_hh the reference (4H, H) weight)
+__global__ void lstm_hh_bwd_kernel(const float* __restrict__ dgates, const float* __restrict__ whh, int B, int H,
+                                   float* __restrict__ dh) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= H) return;
+  const float* dgr = dgates + (long)b * 4 * H;
+  float s = 0.0f;
+  for (int r = 0; r < 4 * H; ++r) s = fmaf(whh[(long)r * H + k], dgr[r], s);
+  dh[(long)b * H + k] = s;
+}
+
+// layer-0 input rows: the embedding row of each step's label (zero for the SOS step)
+__global__ void gather_emb_kernel(const int32_t* __restrict__ xlab, const float* __restrict__ emb, int S, int B, int H,
+                                  int nemb, float* __restrict__ x) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)S * B * H) return;
+  const long r = i / H;
+  const int j = (int)(i % H);
+  const int lab = xlab[r];
+  x[i] = lab >= 0 ? emb[(long)min(lab, nemb - 1) * H + j] : 0.0f;
+}
+
+// d_embed[label] += dx rows; the blank (padding_idx = V) and SOS rows get none (nn.Embedding padding_idx)
+__global__ void scatter_emb_kernel(const int32_t* __restrict__ xlab, const float* __restrict__ dx, int S, int B, int H,
+                                   int V, float* __restrict__ demb) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)S * B * H) return;
+  const long r = i / H;
+  const int j = (int)(i % H);
+  const int lab = xlab[r];
+  if (lab >= 0 && lab < V) atomicAdd(demb + (long)lab * H + j, dx[i]);
+}
+
 long predict_ws_bytes(const cfm_rnnt_decoder* d, int B, int U) {
   const long lbh = round_up((long)d->L * B * d->H * 4, 256);
   return 4 * lbh + round_up((long)(U + 2) * B * 4, 256);
@@ -602,6 +716,121 @@ cfm_status cfm_rnnt_decoder_predict(cfm_rnnt_decoder* d, const int64_t* y, int B
     }
     HIP_OK(hipMemcpyAsync(h_out, hs[cur], lbh * 4, hipMemcpyDeviceToDevice, st));
     HIP_OK(hipMemcpyAsync(c_out, cs[cur], lbh * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipGetLastError());
+  });
+}
+
+// ---- training: BPTT through the prediction network (rnnt.py:190-283 under autograd) -------------
+size_t cfm_rnnt_decoder_train_tape_size(const cfm_rnnt_decoder* d, int B, int U, int add_sos) {
+  if (!d || B < 1 || U < 1) return 0;
+  const long S = U + (add_sos ? 1 : 0);
+  return (size_t)(d->L * S * (long)B * 6 * d->H * 4 + round_up((S + 1) * (long)B * 4, 256) + (long)B * d->H * 4 + 256);
+}
+
+cfm_status cfm_rnnt_decoder_train_forward(cfm_rnnt_decoder* d, const int64_t* y, int B, int U, int add_sos,
+                                          float dropout, uint64_t seed, float* g, void* tape, size_t tape_bytes,
+                                          void* stream) {
+  return guarded([&] {
+    if (!d || !y || !g || !tape) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (B < 1 || U < 1) fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_decoder_train_forward: B, U >= 1");
+    if (tape_bytes < cfm_rnnt_decoder_train_tape_size(d, B, U, add_sos)) fail(CFM_ERR_WORKSPACE, "tape too small");
+    check_device(d);
+    hipStream_t st = (hipStream_t)stream;
+    const int H = d->H, L = d->L, S = U + (add_sos ? 1 : 0);
+    const long bh = (long)B * H;
+    TrainTape tp = train_tape(d, (char*)tape, B, S);
+    hipLaunchKernelGGL(predict_labels_kernel, dim3((unsigned)(((long)S * B + 255) / 256)), dim3(256), 0, st, y, B, U, S,
+                       add_sos ? 1 : 0, d->V + 1, tp.xlab);
+    HIP_OK(hipMemsetAsync(tp.zero, 0, (size_t)bh * 4, st));
+    const Drop gdrop = make_drop(dropout, seed, 2);
+    const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
+    for (int u = 0; u < S; ++u)
+      for (int l = 0; l < L; ++l) {
+        const bool top = l == L - 1;
+        const float* hprev = u ? tp.h(l, u - 1) : tp.zero;
+        const float* cprev = u ? tp.c(l, u - 1) : tp.zero;
+        hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(2 * H), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
+                           tp.xlab + (long)u * B, l ? tp.h(l - 1, u) : nullptr, hprev, cprev, tp.h(l, u), tp.c(l, u),
+                           top ? g + (long)u * H : nullptr, (long)S * H, B, H, H, (const int*)nullptr, tp.gates(l, u),
+                           gdrop, u);
+      }
+    HIP_OK(hipGetLastError());
+  });
+}
+
+size_t cfm_rnnt_decoder_backward_workspace_size(const cfm_rnnt_decoder* d, int B, int U, int add_sos) {
+  if (!d || B < 1 || U < 1) return 0;
+  const int S = U + (add_sos ? 1 : 0);
+  return (size_t)bwd_ws(d, B, S).total;
+}
+
+cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int B, int U, int add_sos, float dropout,
+                                     uint64_t seed, const void* tape, const float* dg, const float* const* w_ih,
+                                     const float* const* w_hh, float* d_embed, float* const* dw_ih,
+                                     float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    if (!d || !tape || !dg || !w_ih || !w_hh) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (B < 1 || U < 1) fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_decoder_backward: B, U >= 1");
+    check_device(d);
+    const int H = d->H, L = d->L, S = U + (add_sos ? 1 : 0);
+    const BwdWs w = bwd_ws(d, B, S);
+    if (!workspace || (long)workspace_bytes < w.total) fail(CFM_ERR_WORKSPACE, "workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    char* ws = (char*)workspace;
+    TrainTape tp = train_tape(d, (char*)tape, B, S);
+    float* dy = (float*)(ws + w.dy);          // (S, B, H): the current layer's output gradient
+    float* dgt = (float*)(ws + w.dgates);     // (S, B, 4H)
+    float* dh = (float*)(ws + w.dh);          // (B, H) recurrent dh
+    float* dc = (float*)(ws + w.dc);          // (B, H) recurrent dc
+    float* xin = (float*)(ws + w.x);          // (S, B, H) the layer's input rows
+    float* hpv = (float*)(ws + w.hp);         // (S, B, H) h_{u-1}
+    char* lws = ws + w.lin;
+    const size_t lws_bytes = (size_t)(w.total - w.lin);
+    const long n = (long)S * B * H;
+    const Drop gdrop = make_drop(dropout, seed, 2);
+    hipLaunchKernelGGL(dg_to_dy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dg, B, S, H, gdrop, dy);
+    auto lin_bwd = [&](const float* x, const float* wt, float* dx, float* dw, float* db) {
+      const cfm_status r = cfm_op_linear_backward(CFM_COMPUTE_FP32, x, S * B, H, wt, 4 * H, dgt, dx, dw, db, lws,
+                                                  lws_bytes, st);
+      if (r != CFM_OK) fail(r, std::string("prediction-net backward: ") + cfm_last_error());
+    };
+    for (int l = L - 1; l >= 0; --l) {
+      HIP_OK(hipMemsetAsync(dh, 0, (size_t)B * H * 4, st));
+      HIP_OK(hipMemsetAsync(dc, 0, (size_t)B * H * 4, st));
+      for (int u = S - 1; u >= 0; --u) {
+        hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((B * H + 255) / 256)), dim3(256), 0, st,
+                           dy + (long)u * B * H, tp.gates(l, u), tp.c(l, u), u ? tp.c(l, u - 1) : tp.zero, B, H, dh, dc,
+                           dgt + (long)u * B * 4 * H);
+        if (u > 0)
+          hipLaunchKernelGGL(lstm_hh_bwd_kernel, dim3((unsigned)((H + 255) / 256), B), dim3(256), 0, st,
+                             dgt + (long)u * B * 4 * H, w_hh[l], B, H, dh);
+      }
+      // the layer's input rows and h_{u-1} rows (S, B, H)
+      if (l == 0)
+        hipLaunchKernelGGL(gather_emb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tp.xlab, d->emb(), S, B,
+                           H, d->V + 1, xin);
+      else   // the tape's h rows of layer l-1 (one (B, H) block per step, 6BH apart)
+        HIP_OK(hipMemcpy2DAsync(xin, (size_t)B * H * 4, tp.h(l - 1, 0), (size_t)6 * B * H * 4, (size_t)B * H * 4, S,
+                                hipMemcpyDeviceToDevice, st));
+      HIP_OK(hipMemsetAsync(hpv, 0, (size_t)B * H * 4, st));
+      if (S > 1)
+        HIP_OK(hipMemcpy2DAsync(hpv + (long)B * H, (size_t)B * H * 4, tp.h(l, 0), (size_t)6 * B * H * 4,
+                                (size_t)B * H * 4, S - 1, hipMemcpyDeviceToDevice, st));
+      // W_ih (+ both biases) and the input gradient; W_hh
+      lin_bwd(xin, w_ih[l], dy, dw_ih ? dw_ih[l] : nullptr, db_ih ? db_ih[l] : nullptr);
+      lin_bwd(hpv, w_hh[l], nullptr, dw_hh ? dw_hh[l] : nullptr, nullptr);
+      if (db_hh && db_hh[l] && db_ih && db_ih[l])
+        HIP_OK(hipMemcpyAsync(db_hh[l], db_ih[l], (size_t)4 * H * 4, hipMemcpyDeviceToDevice, st));
+      else if (db_hh && db_hh[l])
+        fail(CFM_ERR_INVALID_ARG, "db_hh needs db_ih (the two bias gradients are equal)");
+    }
+    // dy now holds d(embedding rows) (S, B, H): scatter-add into the label rows (not blank = padding_idx)
+    if (d_embed) {
+      HIP_OK(hipMemsetAsync(d_embed, 0, (size_t)(d->V + 1) * H * 4, st));
+      hipLaunchKernelGGL(scatter_emb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tp.xlab, dy, S, B, H,
+                         d->V, d_embed);
+    }
     HIP_OK(hipGetLastError());
   });
 }

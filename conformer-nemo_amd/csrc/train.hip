@@ -36,20 +36,6 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // dropout masks: keep(e) iff hash(seed, site, e) >= thr, thr = p * 2^32; kept values * 1/(1-p)
 // ---------------------------------------------------------------------------------------------
-inline uint32_t host_mix32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
-  return x;
-}
-Drop make_drop(float p, uint64_t seed, int site) {
-  Drop d{0u, 0u, 1.0f};
-  if (p <= 0.0f) return d;
-  const double t = std::min(1.0, (double)p) * 4294967296.0;
-  d.thr = (uint32_t)std::min(4294967295.0, std::max(1.0, t));
-  d.key = host_mix32((uint32_t)seed ^ host_mix32((uint32_t)(seed >> 32) + 0x632be5abu * (uint32_t)site));
-  d.scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
-  return d;
-}
-
 unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
 
 // ---------------------------------------------------------------------------------------------

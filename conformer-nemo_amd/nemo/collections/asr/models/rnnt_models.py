@@ -7,10 +7,10 @@ Same construction: decoder.vocab_size and joint.num_classes / vocabulary from `l
 tokenizer (BPE), joint.jointnet.encoder_hidden / pred_hidden from `model_defaults`, RNNTLoss from
 the `loss:` block, greedy decoding from `decoding:`, the fused joint step wired when
 `joint.fuse_loss_wer` is set (rnnt_models.py:117-122).  `forward` is the encoder step (returns
-(encoded, encoded_len)); `validation_step` runs prediction net + joint + loss (fused or not) and the
-WER.  Differences by design: the prediction net and the joint have no backward (SURVEY §8 a-ext4 is
-the cfg-4 forward), so `training_step` runs only where autograd is off and otherwise raises
-NotImplementedError; beam / TSD / ALSD decoding strategies are out of scope.
+(encoded, encoded_len)); `training_step` / `validation_step` run prediction net + joint + loss (fused or
+not) and the WER; under autograd every stage has a native backward (encoder: cfm_train.h; prediction
+net and joint: the training sections of cfm_rnnt_decode.h / cfm_joint.h; loss: cfm_rnnt_loss.h).
+Beam / TSD / ALSD decoding strategies are out of scope.
 """
 from __future__ import annotations
 
@@ -150,12 +150,9 @@ class EncDecRNNTModel(ModelPT):
                           transcripts=transcript, transcript_lengths=transcript_len, compute_wer=compute_wer)
 
     def training_step(self, batch, batch_nb, processed_signal: bool = False):
-        """rnnt_models.py:672-741 (loss only where autograd is off: the prediction net / joint have no
-        backward here, see the module docstring)."""
-        if torch.is_grad_enabled():
-            raise NotImplementedError("RNN-T training needs the prediction-net and joint backward, which are not "
-                                      "built (the native transducer path is the cfg-4 forward); evaluate the loss "
-                                      "under torch.no_grad() or train a CTC model")
+        """rnnt_models.py:673-739: encoder forward, prediction net on the transcripts, then the joint + RNN-T
+        loss (fused in sub-batches when fuse_loss_wer, rnnt.py:824-949); loss.backward() runs the native
+        RNN-T loss gradient, joint backward, prediction-net BPTT and the encoder's native backward."""
         _, _, transcript, transcript_len = batch[:4]
         encoded, encoded_len = self._forward_batch(batch, processed_signal)
         every = getattr(self._trainer, "log_every_n_steps", 1) if self._trainer is not None else 1

@@ -7,9 +7,12 @@ blank_as_pad), the same `prediction.embed` / `prediction.dec_rnn.lstm` parameter
 unchanged; init as rnn.py:151-237: forget-gate bias, chrono init, weights_init_scale), keyword-only
 forward(targets, target_length, states) -> (g (B, H, U+1), target_length, states), `predict`, and the
 state bookkeeping helpers the decoders use.  The embedding + LSTM recurrence runs in libcfm.so (fp32).
-Differences by design: inference only (a forward that requires grad raises NotImplementedError);
-normalization_mode must be None and blank_as_pad True (the reference's defaults and the transducer
-configs' values); rnn_hidden_size > pred_hidden (LSTM projection) is not built.
+Under autograd (training) `predict` runs the native teacher-forced forward with LSTMDropout's output
+dropout and a tape, and the native backpropagation through time (include/cfm_rnnt_decode.h, training
+section) fills the embedding / LSTM gradients.  Differences by design: training starts from the zero
+state (the reference's training call, rnnt.py:190-283 with state=None); normalization_mode must be None
+and blank_as_pad True (the reference's defaults and the transducer configs' values); rnn_hidden_size >
+pred_hidden (LSTM projection) is not built.
 
 Same constructor (jointnet dict with encoder_hidden / pred_hidden / joint_hidden / activation /
 dropout, num_classes, vocabulary, log_softmax, preserve_memory, fuse_loss_wer, fused_batch_size),
@@ -23,10 +26,9 @@ on a GPU), True -> log-probs, False -> logits.
 (rnnt.py:824-949): per `fused_batch_size` sub-batch, the native joint on the sub-batch's own
 (T', U') extent, the loss module set by `set_loss` (the native RNN-T loss, losses/rnnt.py) with its
 reduction forced to None, optional WER through `set_wer`; returns (mean loss, wer, wer_num,
-wer_denom).  Difference by design: the joint has no backward (the joint / prediction-net gradients
-are not built; the path is the cfg-4 forward, SURVEY §8 a-ext4), so a joint whose inputs require
-grad (or a training-mode joint with trainable parameters under autograd) raises
-NotImplementedError: the fused loss is the validation / no-grad loss.
+wer_denom).  Under autograd the joint runs cfm_rnnt_joint_forward_train (joint_net's Dropout in training
+mode) and its backward (cfm_rnnt_joint_backward) gives the encoder-output, decoder-output and parameter
+gradients, so the fused step trains as the reference's does (rnnt_models.py:673-739).
 """
 from __future__ import annotations
 
@@ -71,6 +73,57 @@ class _LSTMDropout(torch.nn.Module):
                 if "weight" in name or "bias" in name:
                     p *= float(weights_init_scale)
         self.dropout = torch.nn.Dropout(dropout) if dropout else None
+
+
+def _seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class _PredictTrainFn(torch.autograd.Function):
+    """RNNTDecoder.predict under autograd: native teacher-forced forward + BPTT (cfm_rnnt_decode.h)."""
+
+    @staticmethod
+    def forward(ctx, nat, y, add_sos, dropout, seed, emb, *lstm):
+        g, tape = nat.train_forward(y, add_sos, dropout, seed)
+        L = len(lstm) // 4
+        ctx.nat, ctx.y, ctx.add_sos, ctx.dropout, ctx.seed, ctx.tape, ctx.L = nat, y, add_sos, dropout, seed, tape, L
+        ctx.save_for_backward(*lstm[:2 * L])
+        ctx.mark_non_differentiable(tape)
+        return g, tape
+
+    @staticmethod
+    def backward(ctx, dg, _dtape):
+        L = ctx.L
+        w = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        want = (need[5], any(need[6:6 + L]), any(need[6 + L:6 + 2 * L]), any(need[6 + 2 * L:6 + 3 * L]),
+                any(need[6 + 3 * L:6 + 4 * L]))
+        if dg is None:
+            dg = torch.zeros((ctx.y.shape[0], ctx.y.shape[1] + (1 if ctx.add_sos else 0), ctx.nat.H),
+                             device=ctx.nat.device)
+        demb, dwi, dwh, dbi, dbh = ctx.nat.backward(ctx.y, ctx.add_sos, ctx.dropout, ctx.seed, ctx.tape, dg,
+                                                    list(w[:L]), list(w[L:2 * L]), want)
+        ctx.tape = None
+        per = lambda lst: list(lst) if lst is not None else [None] * L  # noqa: E731
+        return (None, None, None, None, None, demb, *per(dwi), *per(dwh), *per(dbi), *per(dbh))
+
+
+class _JointTrainFn(torch.autograd.Function):
+    """RNNTJoint.joint under autograd: cfm_rnnt_joint_forward_train + cfm_rnnt_joint_backward."""
+
+    @staticmethod
+    def forward(ctx, nat, dropout, seed, enc_bdt, dec_bdu, w_enc, b_enc, w_pred, b_pred, w_out, b_out):
+        out = nat.forward_train(enc_bdt, dec_bdu, dropout, seed)
+        ctx.nat, ctx.dropout, ctx.seed = nat, dropout, seed
+        ctx.save_for_backward(enc_bdt, dec_bdu, w_enc, w_pred, w_out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        enc, dec, w_enc, w_pred, w_out = ctx.saved_tensors
+        want = tuple(bool(x) for x in ctx.needs_input_grad[3:11])
+        outs = ctx.nat.backward(enc, dec, dlogits, ctx.dropout, ctx.seed, w_enc, w_pred, w_out, want)
+        return (None, None, None, *outs)
 
 
 class RNNTDecoder(NeuralModule):
@@ -154,8 +207,7 @@ class RNNTDecoder(NeuralModule):
         _p = next(self.parameters())
         if _p.device.type != "cuda":
             raise RuntimeError("RNNTDecoder (MI355X-native) needs its parameters on a ROCm GPU")
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("the native prediction network is inference-only; use torch.no_grad() or .eval()")
+        train = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         if y is not None:
             y = y.to(_p.device)
             if y.numel() and (int(y.min()) < 0 or int(y.max()) > self.blank_idx):
@@ -166,7 +218,27 @@ class RNNTDecoder(NeuralModule):
         if state is None and self.random_state_sampling and self.training:
             state = self.initialize_state(torch.empty(B, 1, device=_p.device))
         h0, c0 = (None, None) if state is None else (state[0], state[1])
+        if train and y is not None and state is None:
+            return self._predict_train(y, add_sos)
+        if train:
+            raise NotImplementedError("the native prediction-net backward starts from the zero state with labels "
+                                      "(the training call); use torch.no_grad() for stateful decoding")
         g, (h, c) = self.native_for(_p.device).predict(y, h0, c0, add_sos, B)
+        return g, [h, c]
+
+    def _predict_train(self, y: torch.Tensor, add_sos: bool):
+        nat = self.native_for(y.device)
+        drop = self.prediction["dec_rnn"].dropout
+        p = float(drop.p) if (drop is not None and self.training) else 0.0
+        lists = self._lstm_tensors()
+        g, tape = _PredictTrainFn.apply(nat, y, bool(add_sos), p, _seed() if p > 0 else 0, self.prediction["embed"].weight,
+                                        *[t for ts in lists for t in ts])
+        # final states (detached): the top of every layer's last step on the tape
+        B, S, H, L = y.shape[0], g.shape[1], self.pred_hidden, self.pred_rnn_layers
+        # (cfm_rnnt_decode.h: per layer and step one block [gates (B, 4H) | c (B, H) | h (B, H)])
+        tf = tape[: L * S * B * 6 * H * 4].view(torch.float32).view(L, S, 6 * B, H)
+        h = tf[:, S - 1, 5 * B:6 * B].clone()
+        c = tf[:, S - 1, 4 * B:5 * B].clone()
         return g, [h, c]
 
     def initialize_state(self, y: torch.Tensor) -> List[torch.Tensor]:
@@ -322,12 +394,17 @@ class RNNTJoint(NeuralModule):
     def _run(self, enc_bdt, dec_bdu):
         if not enc_bdt.is_cuda:
             raise RuntimeError("RNNTJoint (MI355X-native) expects its inputs on a ROCm GPU")
-        if torch.is_grad_enabled() and (enc_bdt.requires_grad or dec_bdu.requires_grad or
-                                        (self.training and any(p.requires_grad for p in self.parameters()))):
-            raise NotImplementedError("the native RNN-T joint has no backward (joint and prediction-net gradients "
-                                      "are not built); run it under torch.no_grad() or in .eval() with inputs "
-                                      "that do not require grad")
         nat = self._native_for(enc_bdt.device)
+        if torch.is_grad_enabled() and (enc_bdt.requires_grad or dec_bdu.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            if self.log_softmax:
+                raise NotImplementedError("the native joint backward takes raw logits (log_softmax None / False, the "
+                                          "GPU training configuration)")
+            drop = [m for m in self.joint_net if isinstance(m, torch.nn.Dropout)]
+            p = float(drop[0].p) if (drop and self.training) else 0.0
+            out = self.joint_net[-1]
+            return _JointTrainFn.apply(nat, p, _seed() if p > 0 else 0, enc_bdt, dec_bdu, self.enc.weight, self.enc.bias,
+                                       self.pred.weight, self.pred.bias, out.weight, out.bias)
         return nat.forward(enc_bdt, dec_bdu, log_softmax=bool(self.log_softmax))
 
     @typecheck()

@@ -75,6 +75,27 @@ cfm_status cfm_rnnt_greedy_decode(cfm_rnnt_decoder* h, const float* enc_bdt, con
                                   int32_t* timesteps, int32_t* ntok, double* scores, float* h_out, float* c_out,
                                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- training (RNNTDecoder.predict under autograd, rnnt.py:190-283; rnnt_models.py:673-739) ------ */
+/* Teacher-forced prediction network from the zero state: y (B, U) int64 labels (+ the zero SOS step when
+ * add_sos) -> g (B, S, H), S = U + add_sos, with LSTMDropout's output Dropout(p = dropout) (rnn.py:151-237;
+ * counter-hash mask keyed by seed, regenerated by the backward).  Records a tape (gates, cells, hidden
+ * states of every layer and step) of cfm_rnnt_decoder_train_tape_size bytes for the backward. */
+size_t cfm_rnnt_decoder_train_tape_size(const cfm_rnnt_decoder* h, int B, int U, int add_sos);
+cfm_status cfm_rnnt_decoder_train_forward(cfm_rnnt_decoder* h, const int64_t* y, int B, int U, int add_sos,
+                                          float dropout, uint64_t seed, float* g, void* tape, size_t tape_bytes,
+                                          void* stream);
+/* Backpropagation through time given dg (B, S, H): d_embed (V+1, H) (the blank / padding row and the SOS
+ * step get no gradient), per layer dw_ih / dw_hh (4H, H) and db_ih = db_hh (4H); any output pointer (or
+ * array) may be NULL, db_hh needs db_ih.  w_ih / w_hh: the reference weights of each layer (fp32).
+ * Workspace of cfm_rnnt_decoder_backward_workspace_size bytes.  The embedding gradient is accumulated
+ * with float atomics (summation order not fixed). */
+size_t cfm_rnnt_decoder_backward_workspace_size(const cfm_rnnt_decoder* h, int B, int U, int add_sos);
+cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* h, const int64_t* y, int B, int U, int add_sos, float dropout,
+                                     uint64_t seed, const void* tape, const float* dg, const float* const* w_ih,
+                                     const float* const* w_hh, float* d_embed, float* const* dw_ih,
+                                     float* const* dw_hh, float* const* db_ih, float* const* db_hh, void* workspace,
+                                     size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,136 @@
+"""RNN-T training on the GPU (VERDICT r02 'What's missing' #1; reference rnnt_models.py:673-739):
+the native prediction-net BPTT (cfm_rnnt_decoder_train_forward / _backward) and joint backward
+(cfm_rnnt_joint_forward_train / cfm_rnnt_joint_backward) against the REFERENCE modules' autograd
+(tests/golden/rnnt_train_*.npz, gen_rnnt_train_goldens.py: eval mode, upstream gradient G of the logits),
+and EncDecRNNTBPEModel.training_step end to end (native RNN-T loss -> joint -> prediction net ->
+encoder backward, AdamW steps lower the loss).  Gates: fp32 relL2 <= 1e-4, bf16 joint relL2 <= 2e-2."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_l2
+
+pytestmark = pytest.mark.gpu
+CASES = ["rnnt_train_small", "rnnt_train_2layer_tanh"]
+
+
+def _modules(z, compute):
+    from nemo.collections.asr.modules import RNNTDecoder, RNNTJoint
+    V, Hp, L, H1, J = (int(v) for v in z["meta"][:5])
+    dec = RNNTDecoder(prednet=dict(pred_hidden=Hp, pred_rnn_layers=L, dropout=0.0), vocab_size=V)
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=H1, pred_hidden=Hp, joint_hidden=J, activation=str(z["act"])),
+                      num_classes=V, log_softmax=False)
+    for name, m in (("dec", dec), ("joint", joint)):
+        sd = m.state_dict()
+        m.load_state_dict({k: torch.from_numpy(z[f"w::{name}.{k}"]) if f"w::{name}.{k}" in z.files else v
+                           for k, v in sd.items()})
+    joint.set_compute_mode(compute)
+    return dec.cuda().eval(), joint.cuda().eval()
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CASES)
+def test_prediction_net_and_joint_gradients_match_reference(case, compute):
+    z = np.load(os.path.join(GOLDEN, f"{case}.npz"))
+    dec, joint = _modules(z, compute)
+    enc = torch.from_numpy(z["enc"]).cuda().requires_grad_(True)
+    y = torch.from_numpy(z["y"]).cuda()
+    yl = torch.full((y.shape[0],), y.shape[1], dtype=torch.int64, device="cuda")
+    g, _, states = dec(targets=y, target_length=yl)
+    out = joint(encoder_outputs=enc, decoder_outputs=g)
+    tol = 1e-4 if compute == "fp32" else 2e-2
+    assert rel_l2(out.detach().cpu().numpy(), z["logits"]) < tol
+    # bf16 + relu: hidden units whose fp32 pre-activation lies within bf16 rounding of zero switch the
+    # relu mask (~0.3% of units at these sizes), and each carries its whole gradient, so the gradients
+    # upstream of the activation sit at relL2 ~ sqrt(flipped fraction) ~ 6e-2 from the fp32 golden.
+    gtol = 1e-1 if (compute == "bf16" and str(z["act"]) == "relu") else tol
+    (out * torch.from_numpy(z["G"]).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    errs = {"enc": rel_l2(enc.grad.cpu().numpy(), z["g::enc"])}
+    for name, m in (("dec", dec), ("joint", joint)):
+        for k, p in m.named_parameters():
+            assert p.grad is not None, f"{name}.{k} has no gradient"
+            errs[f"{name}.{k}"] = rel_l2(p.grad.cpu().numpy(), z[f"g::{name}.{k}"])
+    bad = {k: e for k, e in errs.items() if e > gtol}
+    assert not bad, f"{case}/{compute}: " + ", ".join(f"{k} {e:.2e}" for k, e in sorted(bad.items()))
+    # LSTM final states equal the inference predict's
+    with torch.no_grad():
+        _, _, st2 = dec(targets=y, target_length=yl)
+    assert torch.allclose(states[0], st2[0], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(states[1], st2[1], rtol=1e-5, atol=1e-6)
+
+
+def test_dropout_masks_match_between_forward_and_backward():
+    """Training-mode dropout (joint_net Dropout, LSTMDropout output): the backward regenerates the
+    forward's masks, so the gradient w.r.t. the logits' own inputs is consistent: d/d(enc) of
+    sum(logits * G) equals the finite-difference slope along a random direction (fp32 joint)."""
+    from nemo.collections.asr.modules import RNNTDecoder, RNNTJoint
+    torch.manual_seed(3)
+    dec = RNNTDecoder(prednet=dict(pred_hidden=16, pred_rnn_layers=1, dropout=0.5), vocab_size=12).cuda().train()
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=8, pred_hidden=16, joint_hidden=16, activation="tanh", dropout=0.5),
+                      num_classes=12, log_softmax=False).cuda().train()
+    joint.set_compute_mode("fp32")
+    enc = torch.randn(2, 8, 5, device="cuda", dtype=torch.float32).requires_grad_(True)
+    y = torch.randint(0, 12, (2, 3), device="cuda")
+    yl = torch.full((2,), 3, dtype=torch.int64, device="cuda")
+    g, _, _ = dec(targets=y, target_length=yl)
+    out = joint(encoder_outputs=enc, decoder_outputs=g)
+    G = torch.randn_like(out)
+    (out * G).sum().backward()
+    # replay the same masks: same seeds through the autograd node's saved state
+    node = out.grad_fn
+    nat, p, seed = node.nat, node.dropout, node.seed
+    dirn = torch.randn_like(enc)
+    eps = 1e-2
+    assert p == 0.5 and seed != 0
+    with torch.no_grad():
+        fp = nat.forward_train(enc + eps * dirn, g, p, seed)
+        fm = nat.forward_train(enc - eps * dirn, g, p, seed)
+        f0 = nat.forward_train(enc, g, p, seed)
+    assert torch.equal(f0, out.detach())                     # the same seed gives the same masks
+    slope = float(((fp - fm) * G).sum() / (2 * eps))
+    assert abs(slope - float((enc.grad * dirn).sum())) <= 2e-3 * max(1.0, abs(slope))
+
+
+def _rnnt_model(tok_dir):
+    from model_configs import RNNT_BPE_SMALL
+    from nemo.collections.asr.models import EncDecRNNTBPEModel
+    from nemo.core.config import load_config
+    torch.manual_seed(0)
+    return EncDecRNNTBPEModel(load_config(RNNT_BPE_SMALL, {"model.tokenizer.dir": tok_dir}).model).cuda()
+
+
+def test_rnnt_training_step_trains(tmp_path):
+    """EncDecRNNTBPEModel.training_step (fused joint + loss sub-batches) under autograd: every parameter
+    of encoder, prediction net and joint receives a finite gradient, and AdamW steps on one batch lower
+    the loss."""
+    from model_configs import make_bpe_tokenizer
+    tok = make_bpe_tokenizer(str(tmp_path))
+    m = _rnnt_model(tok).train()
+    V = m.tokenizer.vocab_size
+    g = torch.Generator().manual_seed(0)
+    B, T, U = 4, 240, 10
+    x = torch.randn(B, 80, T, generator=g).cuda()
+    xl = torch.tensor([T - 17 * i for i in range(B)], dtype=torch.int64).cuda()
+    y = torch.randint(0, V, (B, U), generator=g).cuda()
+    yl = torch.tensor([U - 2 * i for i in range(B)], dtype=torch.int64).cuda()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    losses = []
+    for step in range(6):
+        opt.zero_grad(set_to_none=True)
+        out = m.training_step((x, xl, y, yl), step, processed_signal=True)
+        loss = out["loss"]
+        assert torch.isfinite(loss).item()
+        loss.backward()
+        if step == 0:
+            for n, p in m.named_parameters():
+                if p.requires_grad and not n.startswith("preprocessor"):
+                    assert p.grad is not None, n
+                    assert torch.isfinite(p.grad).all().item(), n
+            assert any(float(p.grad.abs().sum()) > 0 for n, p in m.named_parameters() if n.startswith("decoder."))
+            assert any(float(p.grad.abs().sum()) > 0 for n, p in m.named_parameters() if n.startswith("joint."))
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0], losses
