@@ -592,14 +592,18 @@ __global__ void gather_emb_kernel(const int32_t* __restrict__ xlab, const float*
 }
 
 // d_embed[label] += dx rows; the blank (padding_idx = V) and SOS rows get none (nn.Embedding padding_idx)
-__global__ void scatter_emb_kernel(const int32_t* __restrict__ xlab, const float* __restrict__ dx, int S, int B, int H,
-                                   int V, float* __restrict__ demb) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)S * B * H) return;
-  const long r = i / H;
-  const int j = (int)(i % H);
-  const int lab = xlab[r];
-  if (lab >= 0 && lab < V) atomicAdd(demb + (long)lab * H + j, dx[i]);
+// d(embedding) row v = sum of dx over the steps whose label is v, in step order (deterministic: one
+// block column per row, no atomics); the padding row (blank = V) and unused rows come out zero
+__global__ __launch_bounds__(256) void embed_grad_kernel(const int32_t* __restrict__ xlab, const float* __restrict__ dx,
+                                                         int SB, int H, int V, float* __restrict__ demb) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int v = blockIdx.y;
+  if (j >= H) return;
+  float s = 0.0f;
+  if (v < V)
+    for (int r = 0; r < SB; ++r)
+      if (xlab[r] == v) s += dx[(long)r * H + j];
+  demb[(long)v * H + j] = s;
 }
 
 long predict_ws_bytes(const cfm_rnnt_decoder* d, int B, int U) {
@@ -825,11 +829,10 @@ cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int 
       else if (db_hh && db_hh[l])
         fail(CFM_ERR_INVALID_ARG, "db_hh needs db_ih (the two bias gradients are equal)");
     }
-    // dy now holds d(embedding rows) (S, B, H): scatter-add into the label rows (not blank = padding_idx)
+    // dy now holds d(embedding rows) (S, B, H): summed per label row (not blank = padding_idx)
     if (d_embed) {
-      HIP_OK(hipMemsetAsync(d_embed, 0, (size_t)(d->V + 1) * H * 4, st));
-      hipLaunchKernelGGL(scatter_emb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, tp.xlab, dy, S, B, H,
-                         d->V, d_embed);
+      hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)((H + 255) / 256), (unsigned)(d->V + 1)), dim3(256), 0, st,
+                         tp.xlab, dy, S * B, H, d->V, d_embed);
     }
     HIP_OK(hipGetLastError());
   });

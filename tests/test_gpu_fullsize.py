@@ -150,3 +150,50 @@ def test_cfg3_training_step_b32_t1000_deterministic():
     for a, b in zip(runs[0][2], runs[1][2]):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+def test_cfg4_rnnt_training_step_b16_t1600_deterministic():
+    """The Conformer-Transducer-Large training step at the cfg-4 workload: 17-layer
+    encoder at B=16, T=1600 (T'=400) in training mode (dropout 0.1), the prediction net (pred_hidden 640,
+    dropout 0.2) on U=100 labels, the joint (joint_hidden 640, relu, dropout 0.2) to raw logits
+    (B, 400, 101, 1025) and the native RNN-T loss; loss.backward() runs the loss gradient, the joint
+    backward, the prediction-net BPTT and the encoder backward.  Finite, and the same seed gives a
+    bitwise-identical loss and every parameter gradient (conformer_transducer_bpe.yaml shapes)."""
+    from nemo.collections.asr.losses import RNNTLoss
+    from nemo.collections.asr.modules import ConformerEncoder, RNNTDecoder, RNNTJoint
+    B, T, V, U = 16, 1600, 1024, 100
+    torch.manual_seed(0)
+    enc = ConformerEncoder(feat_in=80, n_layers=17, d_model=512, n_heads=8, subsampling_factor=4, dropout=0.1,
+                           dropout_emb=0.0, dropout_att=0.1).cuda().train()
+    dec = RNNTDecoder(prednet=dict(pred_hidden=640, pred_rnn_layers=1, dropout=0.2), vocab_size=V).cuda().train()
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=512, pred_hidden=640, joint_hidden=640, activation="relu",
+                                    dropout=0.2), num_classes=V, log_softmax=False).cuda().train()
+    loss_fn = RNNTLoss(num_classes=V, reduction="mean_batch")
+    g = torch.Generator(device="cuda").manual_seed(12)
+    x = torch.randn(B, 80, T, device="cuda", generator=g)
+    lengths = torch.full((B,), T, dtype=torch.int64, device="cuda")
+    lengths[1::4] = 1203
+    y = torch.randint(0, V, (B, U), device="cuda", generator=g)
+    ylen = torch.full((B,), U, dtype=torch.int64, device="cuda")
+    ylen[2::4] = 71
+    params = [p for m in (enc, dec, joint) for p in m.parameters()]
+    runs = []
+    for _ in range(2):
+        for p in params:
+            p.grad = None
+        torch.manual_seed(4321)                               # -> every dropout seed of the step
+        e, el = enc(audio_signal=x, length=lengths)
+        d, _, _ = dec(targets=y, target_length=ylen)
+        logits = joint(encoder_outputs=e, decoder_outputs=d)
+        assert logits.shape == (B, 400, U + 1, V + 1)
+        loss = loss_fn(log_probs=logits, targets=y, input_lengths=el, target_lengths=ylen)
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((float(loss.detach()), [p.grad.clone() for p in params]))
+        del logits, e, d, loss
+    assert np.isfinite(runs[0][0]) and runs[0][0] > 0
+    assert runs[0][0] == runs[1][0]
+    for p, a, b in zip(params, runs[0][1], runs[1][1]):
+        assert torch.isfinite(a).all()
+        assert torch.equal(a, b)
+    assert all(float(a.abs().sum()) > 0 for a in runs[0][1][-8:])     # the decoder and joint receive gradient
