@@ -47,7 +47,7 @@ class NativeCtcHead:
         b = None if bias is None else bias.detach().to(self.device, torch.float32).contiguous()
         _lib.check(self.lib.cfm_ctc_head_set_weights(self.handle, w.data_ptr(), _ptr(b), _stream(self.device)),
                    "cfm_ctc_head_set_weights")
-        torch.cuda.current_stream(self.device).synchronize()   # w, b may be temporaries
+        # stream-ordered: a temporary w / b freed here is only reused by work queued after the pack
 
     def _workspace(self, B: int, T: int) -> torch.Tensor:
         n = self.lib.cfm_ctc_head_workspace_size(self.handle, B, T)

@@ -86,7 +86,8 @@ class NativePredictionNet:
         keep = [_ptrs(ts) for ts in lists]
         _lib.check(self.lib.cfm_rnnt_decoder_set_weights(self.handle, emb.data_ptr(), *[k[0] for k in keep],
                                                          self._stream()), "cfm_rnnt_decoder_set_weights")
-        torch.cuda.current_stream(self.device).synchronize()   # the borrowed copies may be freed after return
+        # stream-ordered: the copies freed here are only reused by work queued after the pack (torch's
+        # caching allocator), so no host synchronisation (it would drain the queue every training step)
 
     def predict(self, y: Optional[torch.Tensor], h0: Optional[torch.Tensor], c0: Optional[torch.Tensor],
                 add_sos: bool, batch_size: int) -> Tuple[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:

@@ -272,7 +272,6 @@ cfm_status cfm_rnnt_joint_set_weights(cfm_rnnt_joint* h, const float* w_enc, con
     packw(w_out, h->C, h->H, h->w_out);
     packb(b_out, h->C, h->b_out);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipStreamSynchronize(st));   // the sources may be temporaries
     h->weights_set = true;
   });
 }

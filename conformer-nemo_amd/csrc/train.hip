@@ -492,6 +492,35 @@ void colred(const float* src, const float* y, const float* mean, long ld, int M,
   cfm_launch(colred_final_kernel, dim3((N + 15) / 16), b, 0, st, (const float*)ws, nch, N, alpha, out, accumulate);
 }
 
+// Up to 10 independent column reductions of [nchunks][N] partials in one launch (grid.y = entry; a null
+// output is skipped): the weight and bias gradients of a layer's five LayerNorms.
+struct ColredList {
+  const float* p[10];
+  float* o[10];
+  int count;
+};
+__global__ __launch_bounds__(256) void colred_multi_kernel(ColredList l, int nchunks, int N) {
+  __shared__ float red[16][17];
+  const int y = blockIdx.y;
+  if (y >= l.count || l.o[y] == nullptr) return;
+  const float* partial = l.p[y];
+  float* out = l.o[y];
+  const int c = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 16 + c;
+  const int nc = min(n, N - 1);
+  float s = 0.0f;
+#pragma unroll 8
+  for (int k = rl; k < nchunks; k += 16) s += partial[(long)k * N + nc];
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][c];
+    out[n] = v;
+  }
+}
+
 // Two independent column reductions of [nchunks][N] partials in one launch (grid.y = 0, 1; a null
 // output is skipped): the LayerNorm weight and bias gradients.
 __global__ __launch_bounds__(256) void colred_final2_kernel(const float* __restrict__ p0, float* __restrict__ o0,
@@ -521,12 +550,15 @@ __global__ __launch_bounds__(256) void colred_final2_kernel(const float* __restr
 // block, with the weight/bias gradient column partials reduced in-block (fixed order):
 //   dx (+)= rstd * (g - mean(g) - xhat * mean(g * xhat)),  g = dy * w
 //   pw[blk][c] = sum over the block's rows of dy * xhat,  pb[blk][c] = sum of dy
+// pk (bf16, optional): the next consumer's GEMM operand, pk[row][c] = bf16(dx * pscale * dropout'(row*d + c))
+// - what tpack2 would make of dx for that consumer, written here instead of re-read in another pass
 constexpr int kLnRowsPerWave = 4;
 template <int E4>
 __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ dy, int M, int d,
                                                            float* __restrict__ dx, int accumulate,
-                                                           float* __restrict__ pw, float* __restrict__ pb) {
+                                                           float* __restrict__ pw, float* __restrict__ pb,
+                                                           bf16_t* __restrict__ pk, float pscale, Drop pdr) {
 #pragma clang fp contract(off)
   __shared__ float4 red[2][4][64 * E4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -603,6 +635,18 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restri
           o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
         }
         dxr[g] = o;
+        if (pk) {
+          float f[4] = {o.x, o.y, o.z, o.w};
+          if (pscale != 1.0f || pdr.thr) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              f[k] *= pscale * drop_mul(pdr, (uint64_t)row * (uint64_t)d + (uint64_t)(4 * g + k));
+          }
+          uint2 u;
+          u.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+          u.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+          *(uint2*)(pk + (long)row * d + 4 * g) = u;
+        }
         aw[e].x += dv[e].x * xh[e].x; aw[e].y += dv[e].y * xh[e].y;
         aw[e].z += dv[e].z * xh[e].z; aw[e].w += dv[e].w * xh[e].w;
         ab[e].x += dv[e].x; ab[e].y += dv[e].y; ab[e].z += dv[e].z; ab[e].w += dv[e].w;
@@ -1190,7 +1234,7 @@ struct Ws {
   long w1, b1, w2, b2, w1b, b1b, w2b, b2b, wqkv, bqkv, uv, wout, bout, wpos, wpw1, bpw1, dww, wpw2, bpw2, wc2, bc2, wsub, bsub;
   long u, br, dwo, gt, s1, s2, sync;
   // backward
-  long gA, gB, dbr, dU, pa, pat, pbt, wt, wtl[7], part, dqkv, dctx, dP, dpre, dG, dD, red;
+  long gA, gB, dbr, lnp, dU, pa, pat, pbt, wt, wtl[7], part, dqkv, dctx, dP, dpre, dG, dD, red;
   long dX2, dcol, i2c, dy1, c1part, gtmp, attws;
   long ped;   // dropout_emb: the dropped positional window (2T'-1, d) in the compute type
   long total;
@@ -1238,6 +1282,7 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.gA = a.take(M * d * 4);
   w.gB = a.take(M * d * 4);
   w.dbr = a.take(M * d * 4);
+  w.lnp = a.take(5L * 2 * ((M + 15) / 16) * d * 4);   // the layer's five LayerNorm backward column partials
   w.dU = a.take(M * std::max(dff, 3 * d) * 4);
   w.pa = a.take(M * kp(Kmax) * es);                                   // dgrad A operand [M][N]
   const long NT = std::max({dff, 3 * d, 2 * d, (long)g.C});
@@ -1781,12 +1826,13 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   //   applied while packing (or by one elementwise pass into dbr when no transposed pack is needed)
   auto linear_bwd = [&](const float* dy, int N, const float* w, int K, const void* xin, long ldxin, int xfn, Drop xdr,
                         float* dx, long ldx, bool acc, int gw, int gb, const void* wtp, float ysc = 1.0f,
-                        Drop ydr = Drop{0, 0, 1.0f}) {
+                        Drop ydr = Drop{0, 0, 1.0f}, bool prepacked = false) {
     const bool want_w = gw >= 0 && Gp(gw), want_b = gb >= 0 && Gp(gb);
     if ((want_w || want_b) && S.wgrad_rm_ok(N, K, S.kpad(N), ldxin)) {
       // dy packed once (row-major, scale + dropout applied), used by the dgrad GEMM and, as it lies,
-      // by the weight gradient; the saved input is read in place
-      S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, ysc, ydr);
+      // by the weight gradient; the saved input is read in place.  prepacked: the LayerNorm backward
+      // that produced dy already wrote that operand into pa (ln_bwd pk)
+      if (!prepacked) S.pack2(dy, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, ysc, ydr);
       if (dx) {
         const void* W = wtp;
         if (!W) {
@@ -1821,20 +1867,39 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       S.wgrad(pat, pbt, Mq, N, K, M, want_w ? Gp(gw) : nullptr, want_b ? Gp(gb) : nullptr);
     }
   };
-  auto ln_bwd = [&](const float* x, int wi, int bi, const float* dy, float* dx, bool acc) {
+  // pk: also write the next consumer's bf16 GEMM operand (pa) = bf16(dx * pscale * dropout'), see
+  // ln_bwd_fused_kernel; only where pa is that operand as it lies (bf16, kpad(d) == d)
+  static const bool ln_pack_env = [] {   // CFM_LN_PACK=0: separate pack passes (A/B, equality tests)
+    const char* e = getenv("CFM_LN_PACK");
+    return !(e && e[0] == '0');
+  }();
+  const bool ln_pack = ln_pack_env && dt == DT_BF16 && S.kpad(d) == d;
+  ColredList ln_slots{};   // this layer's LayerNorm partials awaiting ln_flush (five per layer)
+  auto ln_bwd = [&](const float* x, int wi, int bi, const float* dy, float* dx, bool acc, bool pk = false,
+                    float pscale = 1.0f, Drop pdr = Drop{0, 0, 1.0f}) {
+    bf16_t* pkp = (pk && ln_pack) ? (bf16_t*)pa : nullptr;
+    const int slot = ln_slots.count / 2;
     // dx (+)= LN backward; per-block column partials of dy*xhat and dy (in dbr), then folded
     const int nblk = (M + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave);
-    float* pw = dbr;
-    float* pb = dbr + (long)nblk * d;
+    // column partials into the layer's slot; one colred_multi launch per layer folds all five
+    float* pw = S.W_<float>(S.wl.lnp) + (long)slot * 2 * nblk * d;
+    float* pb = pw + (long)nblk * d;
     const int E4 = (d / 4 + 63) / 64;
     const dim3 grid(nblk), blk(256);
-    if (E4 <= 1) cfm_launch(ln_bwd_fused_kernel<1>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
-    else if (E4 <= 2) cfm_launch(ln_bwd_fused_kernel<2>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
-    else if (E4 <= 4) cfm_launch(ln_bwd_fused_kernel<4>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
-    else cfm_launch(ln_bwd_fused_kernel<8>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb);
-    if (Gp(wi) || Gp(bi))
-      cfm_launch(colred_final2_kernel, dim3((d + 15) / 16, 2), blk, 0, st, (const float*)pw, Gp(wi), (const float*)pb,
-                 Gp(bi), nblk, d);
+    if (E4 <= 1) cfm_launch(ln_bwd_fused_kernel<1>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb, pkp, pscale, pdr);
+    else if (E4 <= 2) cfm_launch(ln_bwd_fused_kernel<2>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb, pkp, pscale, pdr);
+    else if (E4 <= 4) cfm_launch(ln_bwd_fused_kernel<4>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb, pkp, pscale, pdr);
+    else cfm_launch(ln_bwd_fused_kernel<8>, grid, blk, 0, st, x, S.prm(wi), dy, M, d, dx, acc ? 1 : 0, pw, pb, pkp, pscale, pdr);
+    ln_slots.p[ln_slots.count] = pw; ln_slots.o[ln_slots.count++] = Gp(wi);
+    ln_slots.p[ln_slots.count] = pb; ln_slots.o[ln_slots.count++] = Gp(bi);
+  };
+  auto ln_flush = [&]() {
+    const int nblk = (M + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave);
+    bool any = false;
+    for (int i = 0; i < ln_slots.count; ++i) any = any || ln_slots.o[i] != nullptr;
+    if (any)
+      cfm_launch(colred_multi_kernel, dim3((d + 15) / 16, ln_slots.count), dim3(256), 0, st, ln_slots, nblk, d);
+    ln_slots = ColredList{};
   };
 
   // dy (B, d, T') -> gA (B*T', d)
@@ -1867,10 +1932,13 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       S.flush(b);
     }
     // norm_out: gB = d x4
-    ln_bwd(X[4], q.ln_w[LN_OUT], q.ln_b[LN_OUT], gA, gB, false);
+    ln_bwd(X[4], q.ln_w[LN_OUT], q.ln_b[LN_OUT], gA, gB, false, true, 0.5f, S.drop(site(l, 5)));   // + FFN2's operand
 
     // FFN block backward: residual grad g (d xout) -> += d xin through the branch
-    auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, long u, float* gres) {
+    // packed: pa already holds bf16(0.5 * dropout'(gres)) (the preceding ln_bwd); the block's own
+    // closing ln_bwd writes the next consumer's operand (nscale, ndrop) when npack
+    auto ffn_bwd = [&](int f, const float* xin, const void* hn, long z, long u, float* gres, bool packed, bool npack,
+                       float nscale, Drop ndrop) {
       float* dU = S.W_<float>(S.wl.dU);
       const Drop dres = S.drop(site(l, f ? 5 : 1));
       const Drop di = S.drop(site(l, f ? 4 : 0));
@@ -1885,7 +1953,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
           const bool want_w = Gp(q.ff_w2[f]) != nullptr, want_b = Gp(q.ff_b2[f]) != nullptr;
           const bool rm = S.wgrad_rm_ok(N, K, S.kpad(N), K) && S.wgrad_rm_ok(K, N, K, d);
           if (rm) {
-            S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, 0.5f, dres);
+            if (!(packed && ln_pack)) S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), nullptr, 0, 0, 0, 0.5f, dres);
           } else if (want_w || want_b) {
             S.pack2(gres, N, M, N, pa, S.kpad(N), M, S.kpad(N), pat, Mq, N, (int)Mq, 0.5f, dres);
           } else {
@@ -1932,15 +2000,15 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
         linear_bwd(dU, g.dff, S.prm(q.ff_w1[f]), d, hn, d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.ff_w1[f],
                    q.ff_b1[f], WT[f ? WT_FF2_W1 : WT_FF1_W1]);
       }
-      ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true);
+      ln_bwd(xin, q.ln_w[f ? LN_FF2 : LN_FF1], q.ln_b[f ? LN_FF2 : LN_FF1], dhn, gres, true, npack, nscale, ndrop);
     };
-    ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, t.u2, gB);   // gB = d x3
+    ffn_bwd(1, X[3], S.T_(t.hn[3]), t.z2, t.u2, gB, true, true, 1.0f, S.drop(site(l, 3)));   // gB = d x3 (+ pw2's operand)
 
     // ---- convolution module ----
     {
       float* dS = S.W_<float>(S.wl.dD);
       linear_bwd(gB, d, S.prm(q.pw2_w), d, S.T_(t.s), d, 0, Drop{0, 0, 1.0f}, dS, d, false, q.pw2_w, q.pw2_b,
-                 WT[WT_PW2], 1.0f, S.drop(site(l, 3)));
+                 WT[WT_PW2], 1.0f, S.drop(site(l, 3)), ln_pack);
       float* dZ = S.W_<float>(S.wl.dG);
       const float* xhat = S.T_<const float>(t.xhat);
       cfm_launch(bn_swish_bwd_kernel, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)dS, xhat, S.prm(q.bn_w),
@@ -1973,14 +2041,14 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
       float* dhn = S.W_<float>(S.wl.dctx);
       linear_bwd(dpre, 2 * d, S.prm(q.pw1_w), d, S.T_(t.hn[2]), d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.pw1_w,
                  q.pw1_b, WT[WT_PW1]);
-      ln_bwd(X[2], q.ln_w[LN_CONV], q.ln_b[LN_CONV], dhn, gB, true);   // gB = d x2
+      ln_bwd(X[2], q.ln_w[LN_CONV], q.ln_b[LN_CONV], dhn, gB, true, true, 1.0f, S.drop(site(l, 2)));   // gB = d x2 (+ out's operand)
     }
 
     // ---- attention ----
     {
       float* dctx = S.W_<float>(S.wl.dctx);
       linear_bwd(gB, d, S.prm(q.o_w), d, S.T_(t.ctx), d, 0, Drop{0, 0, 1.0f}, dctx, d, false, q.o_w, q.o_b,
-                 WT[WT_OUT], 1.0f, S.drop(site(l, 2)));
+                 WT[WT_OUT], 1.0f, S.drop(site(l, 2)), ln_pack);
       float* dqkv = S.W_<float>(S.wl.dqkv);
       float* dP = S.W_<float>(S.wl.dP);
       const int dk = g.dk;
@@ -2029,10 +2097,11 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
           cl.count = 6;
           cfm_launch(copy_multi_kernel, dim3(ew_grid((long)d * d), 6), dim3(256), 0, st, cl);
         }
-        ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true);   // gB = d x1
+        ln_bwd(X[1], q.ln_w[LN_ATT], q.ln_b[LN_ATT], dhn, gB, true, true, 0.5f, S.drop(site(l, 1)));   // gB = d x1 (+ FFN1's operand)
       }
     }
-    ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, t.u1, gB);   // gB = d x0
+    ffn_bwd(0, X[0], S.T_(t.hn[0]), t.z1, t.u1, gB, true, false, 1.0f, Drop{0, 0, 1.0f});   // gB = d x0
+    ln_flush();
     std::swap(gA, gB);
     grad_ready(S, kPreEncodeRows + l * layer_rows, layer_rows);   // every gradient of layer l is enqueued
   }

@@ -31,7 +31,8 @@ typedef struct cfm_ctc_head cfm_ctc_head;
 cfm_status cfm_ctc_head_create(int feat_in, int num_classes, int device, int compute_mode, cfm_ctc_head** out);
 void cfm_ctc_head_destroy(cfm_ctc_head* h);
 /* weight (num_classes, feat_in) [the Conv1d (C, D, 1) weight], bias (num_classes): device fp32.
- * Packs private copies (W and W^T in the compute type) on `stream`; call again after an update. */
+ * Packs private copies (W and W^T in the compute type) on `stream`; call again after an update.
+ * Stream-ordered (no host synchronisation): the sources must stay valid until `stream` reaches the call. */
 cfm_status cfm_ctc_head_set_weights(cfm_ctc_head* h, const float* weight, const float* bias, void* stream);
 size_t cfm_ctc_head_workspace_size(const cfm_ctc_head* h, int B, int T);
 

@@ -45,7 +45,8 @@ cfm_status cfm_rnnt_decoder_create(int vocab_size, int pred_hidden, int layers, 
 void cfm_rnnt_decoder_destroy(cfm_rnnt_decoder* h);
 /* Reference parameters (device fp32, borrowed): prediction.embed.weight (V+1, H) and per layer l
  * prediction.dec_rnn.lstm.{weight_ih_l, weight_hh_l} (4H, H), {bias_ih_l, bias_hh_l} (4H).
- * Packs private copies ([W_ih | W_hh] rows, b_ih + b_hh). */
+ * Packs private copies ([W_ih | W_hh] rows, b_ih + b_hh) on `stream` (stream-ordered, no host
+ * synchronisation: the sources must stay valid until `stream` reaches the call). */
 cfm_status cfm_rnnt_decoder_set_weights(cfm_rnnt_decoder* h, const float* embed, const float* const* w_ih,
                                         const float* const* w_hh, const float* const* b_ih,
                                         const float* const* b_hh, void* stream);
