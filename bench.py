@@ -260,10 +260,12 @@ def main():
                     help="forward mode: skip the config-3 training-step leg reported under 'train'")
     ap.add_argument("--train-steps", type=int, default=10)
     ap.add_argument("--train-warmup", type=int, default=3)
-    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "stream", "cache_stream", "mel", "decode"],
+    ap.add_argument("--mode", default="forward", choices=["forward", "train", "joint", "rnnt_train", "stream", "cache_stream", "mel", "decode"],
                     help="forward: the north-star encoder forward (default); train: the BASELINE config-3 "
                          "training step (encoder fwd+bwd + CTC head/loss + gradient all-reduce + AdamW); "
                          "joint: config 4 (Large-17 encoder B=16 T=1600 + RNN-T joint U=100 V=1024); "
+                         "rnnt_train: the config-4 transducer training step (encoder + prediction net + joint "
+                         "+ RNN-T loss, fwd+bwd, AdamW); "
                          "stream: config 5 (XL d1024/24 layers, B=64 streams, 400-frame buffers, 160-frame chunks); "
                          "cache_stream: the same 64 streams and 160-frame chunks through the cache-aware chunked "
                          "encoder (SURVEY f3, causal variant, 60 frames of attention history); "
@@ -301,6 +303,8 @@ def main():
         return run_train(args, world, rank, dev, dist, barrier)
     if args.mode == "joint":
         return run_joint(args, world, rank, dev, dist, barrier)
+    if args.mode == "rnnt_train":
+        return run_rnnt_train(args, world, rank, dev, dist, barrier)
     if args.mode == "stream":
         return run_stream(args, world, rank, dev, dist, barrier)
     if args.mode == "cache_stream":
@@ -567,6 +571,82 @@ def run_joint(args, world, rank, dev, dist, barrier):
                         "joint_GFLOP": round(f_joint / 1e9, 1), "prediction_net_GFLOP": round(f_pred / 1e9, 2),
                         "TFLOP/s_per_gpu": round(tot / (ms_step * 1e-3) / 1e12, 1),
                         "frac_of_peak": round(tot / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+    })
+
+
+RNNT_TRAIN_METRIC = ("transducer training-step audio-frames/sec, Conformer-Transducer-Large B=16/GPU T=1600 U=100 "
+                     "V=1024 (BASELINE config 4 workload, fwd+bwd)")
+
+
+def run_rnnt_train(args, world, rank, dev, dist, barrier):
+    """The config-4 workload as a training step (EncDecRNNTModel.training_step, rnnt_models.py:673-739, on
+    the drop-in modules): Large-17 encoder in train mode (conformer_transducer_bpe.yaml regularisation:
+    dropout 0.1, dropout_att 0.1) at B=16, T=1600; RNNTDecoder (LSTM 640, dropout 0.2) over U=100 targets;
+    RNNTJoint (640, relu, dropout 0.2) to raw logits (B, 400, 101, 1025); native RNN-T loss (mean_batch);
+    loss.backward() (loss gradient -> joint backward -> prediction-net BPTT -> encoder backward, per-layer
+    gradient buckets over RCCL at N>1) and AdamW."""
+    from conformer_amd import dist as cdist
+    from nemo.collections.asr.losses import RNNTLoss
+    from nemo.collections.asr.modules import ConformerEncoder, RNNTDecoder, RNNTJoint
+    torch.manual_seed(0)
+    d, H, L, B, T, U, V = 512, 8, args.layers, 16, 1600, 100, 1024
+    enc = ConformerEncoder(feat_in=80, n_layers=L, d_model=d, n_heads=H, dropout=0.1, dropout_emb=0.0,
+                           dropout_att=0.1).to(dev).train()
+    enc.set_compute_mode(args.compute)
+    dec = RNNTDecoder(prednet=dict(pred_hidden=640, pred_rnn_layers=1, dropout=0.2), vocab_size=V).to(dev).train()
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=d, pred_hidden=640, joint_hidden=640, activation="relu",
+                                    dropout=0.2), num_classes=V, log_softmax=False).to(dev).train()
+    joint.set_compute_mode(args.compute)
+    if dist:
+        cdist.convert_sync_batchnorm(enc)
+    loss_fn = RNNTLoss(num_classes=V, reduction="mean_batch")
+    params = [p for m in (enc, dec, joint) for p in m.parameters()]
+    opt = torch.optim.AdamW(params, lr=1e-4, betas=(0.9, 0.98), weight_decay=1e-3, fused=True)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(B, 80, T, device=dev, generator=g)
+    lengths = torch.full((B,), T, dtype=torch.int64, device=dev)
+    targets = torch.randint(0, V, (B, U), device=dev, generator=g)
+    tlen = torch.full((B,), U, dtype=torch.int64, device=dev)
+    if dist:
+        cdist.enable_gradient_buckets(torch.nn.ModuleList([enc, dec, joint]))
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        y, yl = enc(audio_signal=x, length=lengths)
+        pred, _, _ = dec(targets=targets, target_length=tlen)
+        logits = joint(encoder_outputs=y, decoder_outputs=pred)
+        loss = loss_fn(log_probs=logits, targets=targets, input_lengths=yl, target_lengths=tlen)
+        loss.backward()
+        opt.step()
+        return loss
+
+    elapsed, loss = timed_loop(step, args.warmup, args.steps, barrier)
+    finite = bool(torch.isfinite(loss).item())
+    t_max = max_over_ranks(elapsed, dev, dist)
+    ms_step = 1000.0 * t_max / args.steps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops
+    Tp = (((T - 1) // 2 + 1) - 1) // 2 + 1
+    f_enc = encoder_flops(B, T, d, L)
+    f_joint = 2 * B * Tp * d * 640 + 2 * B * (U + 1) * 640 * 640 + 2 * B * Tp * (U + 1) * 640 * (V + 1)
+    f_pred = 2 * B * (U + 1) * (2 * 640) * (4 * 640)
+    tot = 3 * (f_enc + f_joint + f_pred)
+    emit(rank, dist, {
+        "metric": RNNT_TRAIN_METRIC, "value": round(job_throughput(t_max, world, B, T, args.steps), 1),
+        "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.compute, "data": "synthetic",
+        "config": {"workload": f"Conformer-Transducer-Large training step: encoder ({L} layers, dropout 0.1, "
+                               f"dropout_att 0.1) + RNNTDecoder (LSTM 640, dropout 0.2, U={U} + SOS) + RNNTJoint "
+                               f"(640, relu, dropout 0.2, V+1={V + 1}, raw logits) + RNN-T loss + backward + AdamW, "
+                               f"B={B}/GPU, T={T}",
+                   "global_batch": B * world, "seq_len": T,
+                   "parallelism": f"dp{world}" + (" (per-layer RCCL gradient buckets)" if dist else "")},
+        "model_flops": {"GFLOP_per_step_per_gpu_(3x_fwd)": round(tot / 1e9, 1),
+                        "TFLOP/s_per_gpu": round(tot / (ms_step * 1e-3) / 1e12, 1),
+                        "frac_of_peak": round(tot / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+        "loss": round(float(loss.detach()), 4), "loss_finite": finite,
+        "params": sum(p.numel() for p in params),
     })
 
 

@@ -174,24 +174,56 @@ __global__ __launch_bounds__(256) void joint_act_bwd_u_kernel(const float* __res
   dp[bu * H + j] = s;
 }
 
-struct JBWs { long er, dr, fp, gp, hid, dh, df, dp, dx, lin, total; };
+// joint_net[-1] weight/bias gradient partials (bf16 path): [S][C][H + 4] -> dW (C, H) and db at column H
+__global__ __launch_bounds__(256) void joint_slab_kernel(const float* __restrict__ part, int S, int N, int K,
+                                                         float* __restrict__ w, float* __restrict__ b) {
+  const int ldk = K + 4;
+  const long n = (long)N * ldk;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / ldk), k = (int)(i - (long)r * ldk);
+    if (k > K) continue;
+    float a = part[i];
+    for (int s2 = 1; s2 < S; ++s2) a += part[(long)s2 * n + i];
+    if (k < K) { if (w) w[(long)r * K + k] = a; }
+    else if (b) b[r] = a;
+  }
+}
+
+// bf16 output-layer backward (joint_net[-1]): dlogits packed once to bf16 rows, the dgrad GEMM on them and
+// the weight gradient on the frame-major TN kernel (row splits, bias in-kernel) - no transposed copies of
+// the (B*T*U, C) gradient or of the hidden
+bool joint_fast_bwd(const cfm_rnnt_joint* h) { return h->dtype == DT_BF16 && h->H % 8 == 0 && h->H <= 4096; }
+struct JFast { long S, chunk; };
+JFast joint_fast_splits(const cfm_rnnt_joint* h, long rows) {
+  const long tiles = ((h->C + 127) / 128) * ((h->H + 127) / 128);
+  long S = std::max<long>(1, std::min<long>({(512 + tiles - 1) / tiles, rows / 64, 16L}));
+  const long chunk = round_up((rows + S - 1) / S, 32);
+  return JFast{(rows + chunk - 1) / chunk, chunk};
+}
+
+struct JBWs { long er, dr, fp, gp, hid, dh, df, dp, dx, lin, a1, wtp, part, total; };
 JBWs jbws(const cfm_rnnt_joint* h, int B, int T, int U) {
   JBWs w;
   long off = 0;
   auto take = [&](long bytes) { const long o = round_up(off, 256); off = o + round_up(std::max(bytes, 1L), 256); return o; };
   const long rows = (long)B * T * U;
   const int mode = h->dtype == DT_F32 ? CFM_COMPUTE_FP32 : CFM_COMPUTE_BF16;
+  const bool fast = joint_fast_bwd(h);
+  const long Cp = round_up(h->C, 64);
   w.er = take((long)B * T * h->H1 * 4);
   w.dr = take((long)B * U * h->H2 * 4);
   w.fp = take((long)B * T * h->H * 4);
   w.gp = take((long)B * U * h->H * 4);
-  w.hid = take(rows * h->H * 4);
+  w.hid = take(rows * h->H * (fast ? 2 : 4));   // the output Linear's input (bf16 on the fast path)
+  w.a1 = fast ? take(rows * Cp * 2) : 0;
+  w.wtp = fast ? take(round_up(h->H, 256) * Cp * 2) : 0;
+  w.part = fast ? take(joint_fast_splits(h, rows).S * h->C * (h->H + 4) * 4) : 0;
   // dh also holds the compute-type projection inputs before it is written
   w.dh = take(std::max(rows * h->H * 4, (long)B * T * h->kp(h->H1) * h->es + (long)B * U * h->kp(h->H2) * h->es + 512));
   w.df = take((long)B * T * h->H * 4);
   w.dp = take((long)B * U * h->H * 4);
   w.dx = take((long)std::max(B * T * h->H1, B * U * h->H2) * 4);
-  const size_t l1 = cfm_op_linear_backward_ws_size(mode, (int)rows, h->H, h->C);
+  const size_t l1 = fast ? 0 : cfm_op_linear_backward_ws_size(mode, (int)rows, h->H, h->C);
   const size_t l2 = cfm_op_linear_backward_ws_size(mode, B * T, h->H1, h->H);
   const size_t l3 = cfm_op_linear_backward_ws_size(mode, B * U, h->H2, h->H);
   w.lin = take((long)std::max(l1, std::max(l2, l3)));
@@ -411,11 +443,14 @@ cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, cons
       gemm(dt, ag, H2p, B * U, H2, h->wbuf + h->w_pred, H2p, H,
            epi_f32((const float*)(h->wbuf + h->b_pred), gp, H, H % 4 ? 1 : 0), h->zero, st);
       const long nh = rows * (H / 8 + (H % 8 ? 1 : 0));
-      if (H % 8 == 0)
+      if (H % 8)
+        fail(CFM_ERR_UNSUPPORTED, "joint backward: joint_hidden must be a multiple of 8");
+      else if (joint_fast_bwd(h))
+        cfm_launch(joint_hidden_kernel<bf16_t>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp,
+                   B, T, U, H, H, h->act, (bf16_t*)hid, drop);
+      else
         cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
                    T, U, H, H, h->act, hid, drop);
-      else
-        fail(CFM_ERR_UNSUPPORTED, "joint backward: joint_hidden must be a multiple of 8");
     }
     auto lin_bwd = [&](const float* x, long M, int K, const float* wt, int N, const float* dy, float* dx, float* dw,
                        float* db) {
@@ -425,7 +460,23 @@ cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, cons
       if (r != CFM_OK) fail(r, std::string("joint backward: ") + cfm_last_error());
     };
     // joint_net[-1]: logits = hid . W_out^T + b_out
-    lin_bwd(hid, rows, H, w_out, C, dlogits, dh, dw_out, db_out);
+    if (joint_fast_bwd(h)) {
+      const long Cp = round_up(C, 64);
+      bf16_t* a1 = (bf16_t*)(ws + w.a1);
+      pack_matrix(DT_BF16, dlogits, C, (int)rows, C, false, a1, Cp, (int)rows, (int)Cp, st);
+      if (dw_out || db_out) {
+        const JFast js = joint_fast_splits(h, rows);
+        float* part = (float*)(ws + w.part);
+        wgrad_tn(a1, Cp, C, hid, H, H, true, 0, Drop{0u, 0u, 1.0f}, rows, (int)js.S, js.chunk, part, H + 4, H + 4,
+                 (long)C * (H + 4), st);
+        cfm_launch(joint_slab_kernel, dim3(ew_grid((long)C * (H + 4))), dim3(256), 0, st, (const float*)part, (int)js.S,
+                   C, H, dw_out, db_out);
+      }
+      pack_matrix(DT_BF16, w_out, H, C, H, true, ws + w.wtp, Cp, (int)round_up(H, 256), (int)Cp, st);
+      gemm(DT_BF16, a1, Cp, (int)rows, C, ws + w.wtp, (int)Cp, H, epi_f32(nullptr, dh, H, 0), h->zero, st);
+    } else {
+      lin_bwd(hid, rows, H, w_out, C, dlogits, dh, dw_out, db_out);
+    }
     // dz = dh * dropout mask * act'(z); df = sum over u, dp = sum over t
     cfm_launch(joint_act_bwd_t_kernel, dim3((H + 255) / 256, B * T), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act, drop,
                df);

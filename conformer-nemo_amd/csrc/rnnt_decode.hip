@@ -518,6 +518,7 @@ TrainTape train_tape(const cfm_rnnt_decoder* d, char* tape, int B, int S) {
   return t;
 }
 struct BwdWs { long dy, dgates, dh, dc, x, hp, lin, total; };
+constexpr int kHhSplits = 16;   // row splits of the recurrent W_hh^T . dgates product
 BwdWs bwd_ws(const cfm_rnnt_decoder* d, int B, int S) {
   BwdWs w{};
   long o = 0;
@@ -525,7 +526,7 @@ BwdWs bwd_ws(const cfm_rnnt_decoder* d, int B, int S) {
   const long sbh = (long)S * B * d->H * 4;
   w.dy = take(sbh);
   w.dgates = take(4 * sbh);
-  w.dh = take((long)B * d->H * 4);
+  w.dh = take((long)kHhSplits * B * d->H * 4);   // recurrent dh partials (lstm_hh_bwd_kernel)
   w.dc = take((long)B * d->H * 4);
   w.x = take(sbh);
   w.hp = take(sbh);
@@ -546,18 +547,21 @@ __global__ void dg_to_dy_kernel(const float* __restrict__ dg, int B, int S, int 
 }
 
 // LSTM cell backward (gate order i, f, g, o; c = f*c' + i*g, h = o*tanh(c)) for one step:
-// dh = dy + dh_rec (recurrent, in/out: becomes the W_hh . dgates input of the previous step after
-// lstm_hh_bwd), dc (in/out), dgates (B, 4H) pre-activation gradients
+// dh = dy + the recurrent part (the nparts row-split partials lstm_hh_bwd wrote for the step after this
+// one, summed in split order), dc (in/out), dgates (B, 4H) pre-activation gradients
 __global__ void lstm_cell_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ gates,
                                      const float* __restrict__ c, const float* __restrict__ cprev, int B, int H,
-                                     float* __restrict__ dh, float* __restrict__ dc, float* __restrict__ dgates) {
+                                     const float* __restrict__ dhp, int nparts, float* __restrict__ dc,
+                                     float* __restrict__ dgates) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * H) return;
   const int b = i / H, j = i - b * H;
   const float* gr = gates + (long)b * 4 * H;
   const float gi = gr[j], gf = gr[H + j], gg = gr[2 * H + j], go = gr[3 * H + j];
   const float ct = c[i], tc = tanhf(ct);
-  const float dht = dy[i] + dh[i];
+  float rec = 0.0f;
+  for (int s = 0; s < nparts; ++s) rec += dhp[(long)s * B * H + i];
+  const float dht = dy[i] + rec;
   const float dct = dht * go * (1.0f - tc * tc) + dc[i];
   float* dgr = dgates + (long)b * 4 * H;
   dgr[j] = dct * gg * gi * (1.0f - gi);
@@ -565,19 +569,43 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ dy, const float* 
   dgr[2 * H + j] = dct * gi * (1.0f - gg * gg);
   dgr[3 * H + j] = dht * tc * go * (1.0f - go);
   dc[i] = dct * gf;
-  dh[i] = 0.0f;   // consumed; lstm_hh_bwd writes the next step's recurrent part
 }
 
-// dh[b][k] = sum_r W_hh[r][k] * dgates[b][r]  (r < 4H; W_hh the reference (4H, H) weight)
-__global__ void lstm_hh_bwd_kernel(const float* __restrict__ dgates, const float* __restrict__ whh, int B, int H,
-                                   float* __restrict__ dh) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = blockIdx.y;
-  if (k >= H) return;
-  const float* dgr = dgates + (long)b * 4 * H;
-  float s = 0.0f;
-  for (int r = 0; r < 4 * H; ++r) s = fmaf(whh[(long)r * H + k], dgr[r], s);
-  dh[(long)b * H + k] = s;
+// part[s][b][k] = sum over the rows r of split s of W_hh[r][k] * dgates[b][r]  (W_hh the reference
+// (4H, H) weight).  Block (column group of 64, split s), 4 waves: lane = column, wave w takes rows
+// r = r0 + w, r0 + w + 4, ...; the wave-uniform dgates values are scalar loads; 16 batch rows per pass;
+// the 4 waves' sums are added through LDS in wave order (deterministic).
+__global__ __launch_bounds__(256) void lstm_hh_bwd_kernel(const float* __restrict__ dgates,
+                                                          const float* __restrict__ whh, int B, int H,
+                                                          float* __restrict__ part) {
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int s = blockIdx.y;
+  const int R = (4 * H + kHhSplits - 1) / kHhSplits;
+  const int r0 = s * R, r1 = min(4 * H, r0 + R);
+  const int kc = min(k, H - 1);
+  for (int b0 = 0; b0 < B; b0 += 16) {
+    const int nb = min(16, B - b0);
+    float acc[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0.0f;
+    for (int r = r0 + w; r < r1; r += 4) {
+      const float wv = whh[(long)r * H + kc];
+      const float* dgr = dgates + (long)b0 * 4 * H + r;
+#pragma unroll
+      for (int b = 0; b < 16; ++b)
+        if (b < nb) acc[b] = fmaf(wv, dgr[(long)b * 4 * H], acc[b]);
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b) red[w][b][lane] = acc[b];
+    __syncthreads();
+    for (int b = w; b < nb; b += 4) {
+      const float v = ((red[0][b][lane] + red[1][b][lane]) + red[2][b][lane]) + red[3][b][lane];
+      if (k < H) part[((long)s * B + b0 + b) * H + k] = v;
+    }
+    __syncthreads();
+  }
 }
 
 // layer-0 input rows: the embedding row of each step's label (zero for the SOS step)
@@ -785,7 +813,7 @@ cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int 
     TrainTape tp = train_tape(d, (char*)tape, B, S);
     float* dy = (float*)(ws + w.dy);          // (S, B, H): the current layer's output gradient
     float* dgt = (float*)(ws + w.dgates);     // (S, B, 4H)
-    float* dh = (float*)(ws + w.dh);          // (B, H) recurrent dh
+    float* dh = (float*)(ws + w.dh);          // (kHhSplits, B, H) recurrent dh partials
     float* dc = (float*)(ws + w.dc);          // (B, H) recurrent dc
     float* xin = (float*)(ws + w.x);          // (S, B, H) the layer's input rows
     float* hpv = (float*)(ws + w.hp);         // (S, B, H) h_{u-1}
@@ -800,14 +828,13 @@ cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int 
       if (r != CFM_OK) fail(r, std::string("prediction-net backward: ") + cfm_last_error());
     };
     for (int l = L - 1; l >= 0; --l) {
-      HIP_OK(hipMemsetAsync(dh, 0, (size_t)B * H * 4, st));
       HIP_OK(hipMemsetAsync(dc, 0, (size_t)B * H * 4, st));
       for (int u = S - 1; u >= 0; --u) {
         hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((B * H + 255) / 256)), dim3(256), 0, st,
-                           dy + (long)u * B * H, tp.gates(l, u), tp.c(l, u), u ? tp.c(l, u - 1) : tp.zero, B, H, dh, dc,
-                           dgt + (long)u * B * 4 * H);
+                           dy + (long)u * B * H, tp.gates(l, u), tp.c(l, u), u ? tp.c(l, u - 1) : tp.zero, B, H,
+                           (const float*)dh, u == S - 1 ? 0 : kHhSplits, dc, dgt + (long)u * B * 4 * H);
         if (u > 0)
-          hipLaunchKernelGGL(lstm_hh_bwd_kernel, dim3((unsigned)((H + 255) / 256), B), dim3(256), 0, st,
+          hipLaunchKernelGGL(lstm_hh_bwd_kernel, dim3((unsigned)((H + 63) / 64), kHhSplits), dim3(256), 0, st,
                              dgt + (long)u * B * 4 * H, w_hh[l], B, H, dh);
       }
       // the layer's input rows and h_{u-1} rows (S, B, H)
