@@ -52,30 +52,47 @@ __global__ __launch_bounds__(256) void bdl_to_rows_kernel(const float* __restric
   }
 }
 
-// Hj[(b,t,u)][h] = act(f[b*T+t][h] + g[b*U+u][h]); 8 h per thread (16-byte bf16 / 2x16-byte fp32 stores)
+// Hj[(b,t,u)][h] = act(f[b*T+t][h] + g[b*U+u][h]); 8 h per thread (16-byte bf16 / 2x16-byte fp32 stores).
+// Block (b*T + t, chunk of kHidU u's): 32-bit index math only, f's row loaded once per thread item,
+// 16-byte f / g loads when H % 8 == 0.
+constexpr int kHidU = 16;
 template <typename TO>
 __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restrict__ f, const float* __restrict__ g,
                                                            int B, int T, int U, int H, int Hp, int act,
                                                            TO* __restrict__ out, Drop drop) {
   const int HG = Hp / 8;
-  const long n = (long)B * T * U * HG;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int hg = (int)(i % HG);
-    const long row = i / HG;
-    const int u = (int)(row % U);
-    const long bt = row / U;
-    const int b = (int)(bt / T);
-    const float* fr = f + bt * H;
+  const int bt = blockIdx.x;
+  const int b = bt / T;
+  const int u0 = blockIdx.y * kHidU;
+  const int nu = min(kHidU, U - u0);
+  const bool vec = (H & 7) == 0;
+  const float* fr = f + (long)bt * H;
+  for (int j = threadIdx.x; j < nu * HG; j += 256) {
+    const int uu = j / HG, hg = j - uu * HG;
+    const int u = u0 + uu;
+    const long row = (long)bt * U + u;
     const float* gr = g + ((long)b * U + u) * H;
     float v[8];
+    if (vec && hg * 8 < H) {
+      const float4 f0 = *(const float4*)(fr + hg * 8), f1 = *(const float4*)(fr + hg * 8 + 4);
+      const float4 g0 = *(const float4*)(gr + hg * 8), g1 = *(const float4*)(gr + hg * 8 + 4);
+      v[0] = f0.x + g0.x; v[1] = f0.y + g0.y; v[2] = f0.z + g0.z; v[3] = f0.w + g0.w;
+      v[4] = f1.x + g1.x; v[5] = f1.y + g1.y; v[6] = f1.z + g1.z; v[7] = f1.w + g1.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int h = hg * 8 + j;
-      float x = h < H ? fr[h] + gr[h] : 0.0f;
+      for (int e = 0; e < 8; ++e) {
+        const int h = hg * 8 + e;
+        v[e] = h < H ? fr[h] + gr[h] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int h = hg * 8 + e;
+      float x = v[e];
       if (act == CFM_JOINT_RELU) x = fmaxf(x, 0.0f);
       else if (act == CFM_JOINT_SIGMOID) x = 1.0f / (1.0f + expf(-x));
       else x = tanhf(x);
-      v[j] = h < H ? x * drop_mul(drop, (uint64_t)row * H + h) : 0.0f;   // joint_net's Dropout (training)
+      v[e] = h < H ? x * drop_mul(drop, (uint64_t)row * H + h) : 0.0f;   // joint_net's Dropout (training)
     }
     TO* o = out + row * Hp + hg * 8;
     if constexpr (sizeof(TO) == 2) {
@@ -85,6 +102,12 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
       *(uint4*)(o + 4) = Vec16<float>::from_f32(v + 4);
     }
   }
+}
+template <typename TO>
+void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, int Hp, int act, TO* out, Drop drop,
+                  hipStream_t st) {
+  cfm_launch(joint_hidden_kernel<TO>, dim3((unsigned)(B * T), (unsigned)((U + kHidU - 1) / kHidU)), dim3(256), 0, st,
+             f, g, B, T, U, H, Hp, act, out, drop);
 }
 
 // in-place log_softmax over rows of C fp32 values, one wave per row
@@ -350,13 +373,10 @@ void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu
          epi_f32((const float*)(h->wbuf + h->b_enc), fp, h->H, sc), h->zero, st);
     gemm(dt, ws + w.ag, H2p, B * U, h->H2, h->wbuf + h->w_pred, H2p, h->H,
          epi_f32((const float*)(h->wbuf + h->b_pred), gp, h->H, sc), h->zero, st);
-    const long nh = rows * (Hp / 8);
     if (dt == DT_F32)
-      cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
-                 T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop);
+      joint_hidden<float>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop, st);
     else
-      cfm_launch(joint_hidden_kernel<bf16_t>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp,
-                 B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop);
+      joint_hidden<bf16_t>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop, st);
     gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), h->C,
          epi_f32((const float*)(h->wbuf + h->b_out), out, h->C, h->C % 4 ? 1 : 0), h->zero, st);
     if (log_softmax)
@@ -442,15 +462,12 @@ cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, cons
            h->zero, st);
       gemm(dt, ag, H2p, B * U, H2, h->wbuf + h->w_pred, H2p, H,
            epi_f32((const float*)(h->wbuf + h->b_pred), gp, H, H % 4 ? 1 : 0), h->zero, st);
-      const long nh = rows * (H / 8 + (H % 8 ? 1 : 0));
       if (H % 8)
         fail(CFM_ERR_UNSUPPORTED, "joint backward: joint_hidden must be a multiple of 8");
       else if (joint_fast_bwd(h))
-        cfm_launch(joint_hidden_kernel<bf16_t>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp,
-                   B, T, U, H, H, h->act, (bf16_t*)hid, drop);
+        joint_hidden<bf16_t>((const float*)fp, (const float*)gp, B, T, U, H, H, h->act, (bf16_t*)hid, drop, st);
       else
-        cfm_launch(joint_hidden_kernel<float>, dim3(ew_grid(nh)), dim3(256), 0, st, (const float*)fp, (const float*)gp, B,
-                   T, U, H, H, h->act, hid, drop);
+        joint_hidden<float>((const float*)fp, (const float*)gp, B, T, U, H, H, h->act, hid, drop, st);
     }
     auto lin_bwd = [&](const float* x, long M, int K, const float* wt, int N, const float* dy, float* dx, float* dw,
                        float* db) {

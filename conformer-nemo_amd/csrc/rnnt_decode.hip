@@ -572,12 +572,15 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ dy, const float* 
 }
 
 // part[s][b][k] = sum over the rows r of split s of W_hh[r][k] * dgates[b][r]  (W_hh the reference
-// (4H, H) weight).  Block (column group of 64, split s), 4 waves: lane = column, wave w takes rows
-// r = r0 + w, r0 + w + 4, ...; the wave-uniform dgates values are scalar loads; 16 batch rows per pass;
-// the 4 waves' sums are added through LDS in wave order (deterministic).
+// (4H, H) weight).  Block (column group of 64, split s), 4 waves: the split's dgates [r][16 b] staged in
+// LDS, lane = column, wave w takes rows r0 + w, r0 + w + 4, ... (one coalesced W row load and four
+// broadcast 16-byte LDS reads per row), 16 batch rows per pass; the 4 waves' sums are added through
+// LDS in wave order (deterministic).
+constexpr int kHhRows = 4 * 1536 / kHhSplits + 1;   // rows of a split (4H / kHhSplits, H <= 1536)
 __global__ __launch_bounds__(256) void lstm_hh_bwd_kernel(const float* __restrict__ dgates,
                                                           const float* __restrict__ whh, int B, int H,
                                                           float* __restrict__ part) {
+  __shared__ float4 dgl[kHhRows][4];        // [row - r0][b / 4] for the pass's 16 batch rows
   __shared__ float red[4][16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
@@ -587,15 +590,24 @@ __global__ __launch_bounds__(256) void lstm_hh_bwd_kernel(const float* __restric
   const int kc = min(k, H - 1);
   for (int b0 = 0; b0 < B; b0 += 16) {
     const int nb = min(16, B - b0);
+    for (int i = threadIdx.x; i < (r1 - r0) * 16; i += 256) {
+      const int rr = i >> 4, b = i & 15;
+      ((float*)dgl[rr])[b] = b < nb ? dgates[(long)(b0 + b) * 4 * H + r0 + rr] : 0.0f;
+    }
+    __syncthreads();
     float acc[16];
 #pragma unroll
     for (int b = 0; b < 16; ++b) acc[b] = 0.0f;
     for (int r = r0 + w; r < r1; r += 4) {
       const float wv = whh[(long)r * H + kc];
-      const float* dgr = dgates + (long)b0 * 4 * H + r;
 #pragma unroll
-      for (int b = 0; b < 16; ++b)
-        if (b < nb) acc[b] = fmaf(wv, dgr[(long)b * 4 * H], acc[b]);
+      for (int q = 0; q < 4; ++q) {
+        const float4 d4 = dgl[r - r0][q];
+        acc[4 * q] = fmaf(wv, d4.x, acc[4 * q]);
+        acc[4 * q + 1] = fmaf(wv, d4.y, acc[4 * q + 1]);
+        acc[4 * q + 2] = fmaf(wv, d4.z, acc[4 * q + 2]);
+        acc[4 * q + 3] = fmaf(wv, d4.w, acc[4 * q + 3]);
+      }
     }
 #pragma unroll
     for (int b = 0; b < 16; ++b) red[w][b][lane] = acc[b];
