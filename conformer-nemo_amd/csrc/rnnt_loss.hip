@@ -56,6 +56,7 @@ __device__ __forceinline__ int label_at(const Dims& d, const int32_t* labels, in
   return min(max(labels[(long)b * d.ld + u], 0), d.V - 1);
 }
 
+constexpr int kDenomRegs = 32;   // V <= 2048: single read of the logits row
 __global__ __launch_bounds__(256) void rnnt_denom_kernel(const float* __restrict__ acts, const int32_t* __restrict__ labels,
                                                          const int32_t* __restrict__ act_lens,
                                                          const int32_t* __restrict__ label_lens, Dims d,
@@ -71,11 +72,24 @@ __global__ __launch_bounds__(256) void rnnt_denom_kernel(const float* __restrict
   lens(d, act_lens, label_lens, b, Tb, Ub);
   if (t >= Tb || u >= Ub) return;
   const float* a = acts + row * d.V;
-  float m = kNegInf;
-  for (int v = lane; v < d.V; v += 64) m = fmaxf(m, a[v]);
-  m = wave_max(m);
-  float s = 0.0f;
-  for (int v = lane; v < d.V; v += 64) s += expf(a[v] - m);
+  float m = kNegInf, s = 0.0f;
+  if (d.V <= 64 * kDenomRegs) {
+    // one pass over HBM: the row's logits stay in registers for the max and the exp-sum
+    float r[kDenomRegs];
+#pragma unroll
+    for (int k = 0; k < kDenomRegs; ++k) {
+      const int v = lane + 64 * k;
+      r[k] = v < d.V ? a[v] : kNegInf;
+      m = fmaxf(m, r[k]);
+    }
+    m = wave_max(m);
+#pragma unroll
+    for (int k = 0; k < kDenomRegs; ++k) s += lane + 64 * k < d.V ? expf(r[k] - m) : 0.0f;
+  } else {
+    for (int v = lane; v < d.V; v += 64) m = fmaxf(m, a[v]);
+    m = wave_max(m);
+    for (int v = lane; v < d.V; v += 64) s += expf(a[v] - m);
+  }
   s = wave_sumf(s);
   if (lane == 0) {
     const float dn = -(m + logf(s));
@@ -191,16 +205,26 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
   const float be_u1 = u < Ub - 1 ? betas[row + 1] : 0.0f;
   const float lp_lab = lab >= 0 ? dn + a[lab] : 0.0f;
   const float l1p = log1pf(fastemit_lambda);
-  for (int v = lane; v < d.V; v += 64) {
-    const float logpk = dn + a[v];
+  auto gval = [&](int v, float av) {
+    const float logpk = dn + av;
     float gr = expf(al + be + logpk - ll);
     if (fastemit_lambda > 0.0f && u < Ub - 1) gr = gr + fastemit_lambda * expf(al + lp_lab + be_u1 + logpk - ll);
     if (v == d.blank && t == Tb - 1 && u == Ub - 1) gr -= expf(al + logpk - ll);
     if (v == d.blank && t < Tb - 1) gr -= expf(al + logpk - ll + be_t1);
     if (u < Ub - 1 && v == lab) gr -= expf(l1p + al + logpk - ll + be_u1);
     if (clamp > 0.0f) gr = fmaxf(fminf(gr, clamp), -clamp);
-    g[v] = gr;
+    return gr;
+  };
+  // four logits in flight per lane (independent loads, then the math)
+  int v0 = lane;
+  for (; v0 + 192 < d.V; v0 += 256) {
+    float av[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) av[k] = a[v0 + 64 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g[v0 + 64 * k] = gval(v0 + 64 * k, av[k]);
   }
+  for (int v = v0; v < d.V; v += 64) g[v] = gval(v, a[v]);
 }
 
 size_t ws_floats(int B, int T, int U) { return (size_t)5 * B * T * U + 2 * (size_t)B + 64; }
