@@ -100,7 +100,7 @@ class CfmError(RuntimeError):
 _lib: Optional[ctypes.CDLL] = None
 
 
-ABI_VERSION = 2   # include/cfm_encoder.h CFM_ABI_VERSION: the struct layouts these bindings declare
+ABI_VERSION = 3   # include/cfm_encoder.h CFM_ABI_VERSION: the struct layouts these bindings declare
 
 
 def load() -> ctypes.CDLL:

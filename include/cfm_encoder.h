@@ -80,8 +80,12 @@ const char* cfm_last_error(void);
  * built with before passing any struct:
  *   1  round 1;
  *   2  cfm_train_opts (cfm_train.h) gained grad_ready / grad_ready_user, and dropout_emb / dropout_att
- *      became active (an older host's shorter struct would leave the callback pointer unset). */
-#define CFM_ABI_VERSION 2
+ *      became active (an older host's shorter struct would leave the callback pointer unset);
+ *   3  the *_set_weights of cfm_ctc.h / cfm_joint.h / cfm_rnnt_decode.h are stream-ordered (they no
+ *      longer synchronise the stream: a host must keep the sources valid until the stream passes the
+ *      call); new entry points cfm_encoder_layers_forward, cfm_op_conv_glu_dwconv, the transducer
+ *      training entries of cfm_joint.h / cfm_rnnt_decode.h. */
+#define CFM_ABI_VERSION 3
 int cfm_version(void);
 
 /* calc_length (subsampling.py:272-282) on the host: encoder frames for `len` input frames. */

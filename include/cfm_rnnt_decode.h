@@ -88,8 +88,9 @@ cfm_status cfm_rnnt_decoder_train_forward(cfm_rnnt_decoder* h, const int64_t* y,
 /* Backpropagation through time given dg (B, S, H): d_embed (V+1, H) (the blank / padding row and the SOS
  * step get no gradient), per layer dw_ih / dw_hh (4H, H) and db_ih = db_hh (4H); any output pointer (or
  * array) may be NULL, db_hh needs db_ih.  w_ih / w_hh: the reference weights of each layer (fp32).
- * Workspace of cfm_rnnt_decoder_backward_workspace_size bytes.  The embedding gradient is accumulated
- * with float atomics (summation order not fixed). */
+ * Workspace of cfm_rnnt_decoder_backward_workspace_size bytes.  Deterministic: the embedding gradient
+ * row of label v sums the steps labelled v in step order, the recurrent product its 16 row splits in
+ * split order (no atomics; bitwise reproducible). */
 size_t cfm_rnnt_decoder_backward_workspace_size(const cfm_rnnt_decoder* h, int B, int U, int add_sos);
 cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* h, const int64_t* y, int B, int U, int add_sos, float dropout,
                                      uint64_t seed, const void* tape, const float* dg, const float* const* w_ih,

@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 bash tools/gpu_verify.sh || exit $?
-for m in joint stream mel decode; do
+for m in joint rnnt_train stream cache_stream mel decode; do
   timeout -k 10 300 python bench.py --mode $m > gpurun_out/verify_$m.json 2> gpurun_out/verify_$m.err; rc=$?; echo ${m}_rc=$rc
   [ $rc -eq 0 ] || exit $rc
 done
