@@ -155,6 +155,9 @@ struct CtcArgs {
   float scale;
   float* E;       // [B][T][U+1]: emissions of the extended classes (0 = blank, 1 + k = label k)
   float* A;       // [B][T][S]: log alphas, S = 2U + 1
+  float* Bt;      // [B][T][S]: log betas (gradient only)
+  int32_t* fl;    // [B][U]: label k is the first occurrence of its class (gradient only)
+  int32_t* nx;    // [B][U]: next k' > k with the same class, -1 none
   float* nll; float* grad;
   uint8_t* dead;  // [B]: 1 where zero_infinity zeroed an infinite loss (its gradient is 0 too)
 };
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(256) void ctc_gather_kernel(CtcArgs a) {
 CFM_DEV int ctc_ecol(int s) { return (s & 1) ? 1 + (s >> 1) : 0; }
 
 template <int SPL>
-__global__ __launch_bounds__(64) void ctc_alpha_kernel(CtcArgs a) {
+CFM_DEV void ctc_alpha_run(const CtcArgs& a) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int Tb = min(a.ilen[b], a.T), Ub = min(a.tlen[b], a.U), S = 2 * Ub + 1;
   const int K1 = a.U + 1;
@@ -240,35 +243,26 @@ __global__ __launch_bounds__(64) void ctc_alpha_kernel(CtcArgs a) {
   }
 }
 
-// grad[b][t][c] = scale * exp(lp) for t < Tb (0 beyond, and 0 for zero_infinity'd utterances);
-// the posterior terms of the target classes are subtracted by ctc_beta_kernel afterwards.
-__global__ __launch_bounds__(256) void ctc_grad_base_kernel(CtcArgs a) {
-  const int b = blockIdx.y;
-  const int Tb = min(a.ilen[b], a.T);
-  const bool dead = a.dead[b] != 0;
-  const long n = (long)a.T * a.C;
-  const float* lpb = a.lp + (long)b * n;
-  float* gb = a.grad + (long)b * n;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int t = (int)(i / a.C);
-    gb[i] = (t < Tb && !dead) ? a.scale * expf(lpb[i]) : 0.0f;
-  }
-}
-
+// The beta recursion alone (gradient): log betas into a.Bt, plus the per-utterance label bookkeeping
+// the posterior kernel needs (a.fl / a.nx).  Independent of the alphas, so it runs beside them.
 template <int SPL>
-__global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
-  extern __shared__ float vs[];   // [S] posterior log-terms of the current t
+CFM_DEV void ctc_beta_run(const CtcArgs& a) {
   const int b = blockIdx.x, lane = threadIdx.x;
-  if (a.dead[b]) return;
   const int Tb = min(a.ilen[b], a.T), Ub = min(a.tlen[b], a.U), S = 2 * Ub + 1;
-  if (Tb <= 0) return;
   const int K1 = a.U + 1;
   const int32_t* tg = a.tgt + (long)b * a.U;
+  for (int k = lane; k < Ub; k += 64) {
+    const int c = tg[k];
+    int first = 1, nk = -1;
+    for (int k2 = 0; k2 < k; ++k2) first &= tg[k2] != c;
+    for (int k2 = Ub - 1; k2 > k; --k2)
+      if (tg[k2] == c) nk = k2;
+    a.fl[(long)b * a.U + k] = first;
+    a.nx[(long)b * a.U + k] = nk;
+  }
+  if (Tb <= 0) return;
   const float* Eb = a.E + (long)b * a.T * K1;
-  const float* Ab = a.A + (long)b * a.T * (2 * a.U + 1);
-  const float* lpb = a.lp + (long)b * a.T * a.C;
-  float* gb = a.grad + (long)b * a.T * a.C;
-  const float nll = a.nll[b];
+  float* Bb = a.Bt + (long)b * a.T * (2 * a.U + 1);
   int col[SPL];
   bool skipn[SPL];   // the s -> s+2 link of beta (exists iff state s+2 has its s-2 link)
 #pragma unroll
@@ -278,41 +272,17 @@ __global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
     const int s2 = s + 2;
     skipn[j] = (s2 < S) && (s2 & 1) && s2 >= 3 && tg[(s2 >> 1)] != tg[(s2 >> 1) - 1];
   }
-  // label bookkeeping once per utterance (LDS): fl[k] = k is the first occurrence of its class,
-  // nx[k] = next k' > k with the same class (-1: none)
-  int* fl = (int*)(vs + 2 * a.U + 1);
-  int* nx = fl + a.U;
-  for (int k = lane; k < Ub; k += 64) {
-    const int c = tg[k];
-    int first = 1, nk = -1;
-    for (int k2 = 0; k2 < k; ++k2) first &= tg[k2] != c;
-    for (int k2 = Ub - 1; k2 > k; --k2)
-      if (tg[k2] == c) nk = k2;
-    fl[k] = first;
-    nx[k] = nk;
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  __builtin_amdgcn_wave_barrier();
   float bt[SPL];
 #pragma unroll
   for (int j = 0; j < SPL; ++j) bt[j] = NEG_INF;
-  float e[SPL], av[SPL];
+  float e[SPL];
 #pragma unroll
-  for (int j = 0; j < SPL; ++j) {
-    const int s = lane * SPL + j;
-    e[j] = Eb[(long)(Tb - 1) * K1 + col[j]];
-    av[j] = s < S ? Ab[(long)(Tb - 1) * S + s] : NEG_INF;
-  }
+  for (int j = 0; j < SPL; ++j) e[j] = Eb[(long)(Tb - 1) * K1 + col[j]];
   for (int t = Tb - 1; t >= 0; --t) {
-    // prefetch the next (earlier) frame's emissions and alphas while this frame is processed
-    float e_n[SPL], av_n[SPL];
+    float e_n[SPL];
     const int tn = max(t - 1, 0);
 #pragma unroll
-    for (int j = 0; j < SPL; ++j) {
-      const int s = lane * SPL + j;
-      e_n[j] = Eb[(long)tn * K1 + col[j]];
-      av_n[j] = Ab[(long)tn * S + min(s, S - 1)];
-    }
+    for (int j = 0; j < SPL; ++j) e_n[j] = Eb[(long)tn * K1 + col[j]];
     const float dn1 = __shfl_down(bt[0], 1, 64);
     const float dn2 = __shfl_down(SPL >= 2 ? bt[1] : NEG_INF, 1, 64);
     const float n1l = lane == 63 ? NEG_INF : dn1, n2l = lane == 63 ? NEG_INF : dn2;
@@ -334,38 +304,78 @@ __global__ __launch_bounds__(64) void ctc_beta_kernel(CtcArgs a) {
     for (int j = 0; j < SPL; ++j) {
       bt[j] = nw[j];
       const int s = lane * SPL + j;
-      if (s < S) vs[s] = av[j] + bt[j];
+      if (s < S) Bb[(long)t * S + s] = bt[j];
+      e[j] = e_n[j];
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    // blank: all even states
-    float lb = NEG_INF;
-    for (int s = 2 * lane; s < S; s += 128) lb = lse2(lb, vs[s]);
-    const float mb = wave_max(lb);
-    float sb = mb == NEG_INF ? 0.0f : expf(lb - mb);
-    sb = wave_sum(sb);
-    const float lcab_blank = mb == NEG_INF ? NEG_INF : mb + logf(sb);
-    const float* lpt = lpb + (long)t * a.C;
-    float* gt = gb + (long)t * a.C;
-    if (lane == 0 && lcab_blank != NEG_INF) {
-      const float lpv = lpt[a.blank];
-      gt[a.blank] = a.scale * (expf(lpv) - expf(lcab_blank + nll - lpv));
+  }
+}
+
+// blockIdx.y == 0: alphas + nll; == 1: betas (gradient launches only)
+template <int SPL>
+__global__ __launch_bounds__(64) void ctc_lattice_kernel(CtcArgs a) {
+  if (blockIdx.y == 0) ctc_alpha_run<SPL>(a);
+  else ctc_beta_run<SPL>(a);
+}
+
+// grad[b][t][c] = scale * exp(lp) for t < Tb (0 beyond, and 0 for zero_infinity'd utterances);
+// the posterior terms of the target classes are subtracted by ctc_post_kernel afterwards.
+__global__ __launch_bounds__(256) void ctc_grad_base_kernel(CtcArgs a) {
+  const int b = blockIdx.y;
+  const int Tb = min(a.ilen[b], a.T);
+  const bool dead = a.dead[b] != 0;
+  const long n = (long)a.T * a.C;
+  const float* lpb = a.lp + (long)b * n;
+  float* gb = a.grad + (long)b * n;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int t = (int)(i / a.C);
+    gb[i] = (t < Tb && !dead) ? a.scale * expf(lpb[i]) : 0.0f;
+  }
+}
+
+// Posterior terms of the target classes, one wave per (b, t) (after ctc_grad_base_kernel): with
+// v[s] = alpha_t(s) + beta_t(s), grad[b][t][blank] = scale * (exp(lp) - exp(lse_even(v) + nll - lp)) and
+// for each class c of the labels the same with the lse over the odd states of every k with label c
+// (the first occurrence of the class writes it, walking the nx chain) - the arithmetic of the fused beta
+// kernel this replaces, moved out of the serial recursion.
+__global__ __launch_bounds__(256) void ctc_post_kernel(CtcArgs a) {
+  extern __shared__ float vsm[];   // [4 waves][S]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.y, t = blockIdx.x * 4 + w;
+  const int Tb = min(a.ilen[b], a.T), Ub = min(a.tlen[b], a.U), S = 2 * Ub + 1;
+  if (a.dead[b] || t >= Tb) return;
+  const int Sld = 2 * a.U + 1;
+  float* vs = vsm + w * Sld;
+  // the lattices' rows have the utterance's own stride S (as the recursions write them)
+  const float* Ar = a.A + (long)b * a.T * Sld + (long)t * S;
+  const float* Br = a.Bt + (long)b * a.T * Sld + (long)t * S;
+  for (int s = lane; s < S; s += 64) vs[s] = Ar[s] + Br[s];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const float nll = a.nll[b];
+  const int32_t* tg = a.tgt + (long)b * a.U;
+  float lb = NEG_INF;
+  for (int s = 2 * lane; s < S; s += 128) lb = lse2(lb, vs[s]);
+  const float mb = wave_max(lb);
+  float sb = mb == NEG_INF ? 0.0f : expf(lb - mb);
+  sb = wave_sum(sb);
+  const float lcab_blank = mb == NEG_INF ? NEG_INF : mb + logf(sb);
+  const float* lpt = a.lp + ((long)b * a.T + t) * a.C;
+  float* gt = a.grad + ((long)b * a.T + t) * a.C;
+  if (lane == 0 && lcab_blank != NEG_INF) {
+    const float lpv = lpt[a.blank];
+    gt[a.blank] = a.scale * (expf(lpv) - expf(lcab_blank + nll - lpv));
+  }
+  const int32_t* fl = a.fl + (long)b * a.U;
+  const int32_t* nx = a.nx + (long)b * a.U;
+  for (int k = lane; k < Ub; k += 64) {
+    if (!fl[k]) continue;
+    float lc = NEG_INF;
+    for (int k2 = k; k2 >= 0; k2 = nx[k2]) lc = lse2(lc, vs[2 * k2 + 1]);
+    if (lc != NEG_INF) {
+      const int c = tg[k];
+      const float lpv = lpt[c];
+      gt[c] = a.scale * (expf(lpv) - expf(lc + nll - lpv));
     }
-    // labels: the first occurrence k of each class sums every k' with the same label (nx chain)
-    for (int k = lane; k < Ub; k += 64) {
-      if (!fl[k]) continue;
-      float lc = NEG_INF;
-      for (int k2 = k; k2 >= 0; k2 = nx[k2]) lc = lse2(lc, vs[2 * k2 + 1]);
-      if (lc != NEG_INF) {
-        const int c = tg[k];
-        const float lpv = lpt[c];
-        gt[c] = a.scale * (expf(lpv) - expf(lc + nll - lpv));
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int j = 0; j < SPL; ++j) { e[j] = e_n[j]; av[j] = av_n[j]; }
   }
 }
 
@@ -568,8 +578,8 @@ size_t cfm_ctc_loss_workspace_size(int B, int T, int C, int U) {
   (void)C;
   if (B <= 0 || T <= 0 || U < 0) return 0;
   const long S = 2L * U + 1;
-  return (size_t)(round_up((long)B * T * (U + 1) * 4, 256) + round_up((long)B * T * S * 4, 256) + round_up(B, 256) +
-                  256);
+  return (size_t)(round_up((long)B * T * (U + 1) * 4, 256) + 2 * round_up((long)B * T * S * 4, 256) + round_up(B, 256) +
+                  2 * round_up((long)B * std::max(U, 1) * 4, 256) + 256);
 }
 
 cfm_status cfm_ctc_loss(const float* logprobs_btc, const int32_t* targets_bu, const int32_t* input_lengths,
@@ -593,24 +603,27 @@ cfm_status cfm_ctc_loss(const float* logprobs_btc, const int32_t* targets_bu, co
     a.E = (float*)ws;
     a.A = (float*)(ws + round_up((long)B * T * (U + 1) * 4, 256));
     a.dead = (uint8_t*)(ws + round_up((long)B * T * (U + 1) * 4, 256) + round_up((long)B * T * S * 4, 256));
+    a.Bt = (float*)((char*)a.dead + round_up(B, 256));
+    a.fl = (int32_t*)((char*)a.Bt + round_up((long)B * T * S * 4, 256));
+    a.nx = (int32_t*)((char*)a.fl + round_up((long)B * std::max(U, 1) * 4, 256));
     a.nll = nll_b;
     a.grad = grad_btc;
     if (U == 0) a.tgt = input_lengths;   // never dereferenced for a label (no odd states)
     cfm_launch(ctc_gather_kernel, dim3((unsigned)std::min<long>(((long)T * (U + 1) + 255) / 256, 256), B), dim3(256), 0,
                st, a);
     const int spl = (int)((S + 63) / 64);
-    auto per_spl = [&](auto kalpha, auto kbeta) {
-      cfm_launch(kalpha, dim3(B), dim3(64), 0, st, a);
-      if (grad_btc) {
-        cfm_launch(ctc_grad_base_kernel, dim3((unsigned)std::min<long>(((long)T * C + 255) / 256, 512), B), dim3(256), 0,
-                   st, a);
-        cfm_launch(kbeta, dim3(B), dim3(64), (uint32_t)((S + 2 * U) * 4), st, a);
-      }
-    };
-    if (spl <= 2) per_spl(ctc_alpha_kernel<2>, ctc_beta_kernel<2>);
-    else if (spl <= 4) per_spl(ctc_alpha_kernel<4>, ctc_beta_kernel<4>);
-    else if (spl <= 8) per_spl(ctc_alpha_kernel<8>, ctc_beta_kernel<8>);
-    else per_spl(ctc_alpha_kernel<16>, ctc_beta_kernel<16>);
+    // alphas (+ nll) and, for the gradient, betas in one launch (independent recursions, grid.y);
+    // then scale * exp(lp) everywhere and the target classes' posterior terms, fully parallel
+    auto lattice = [&](auto klat) { cfm_launch(klat, dim3(B, grad_btc ? 2 : 1), dim3(64), 0, st, a); };
+    if (spl <= 2) lattice(ctc_lattice_kernel<2>);
+    else if (spl <= 4) lattice(ctc_lattice_kernel<4>);
+    else if (spl <= 8) lattice(ctc_lattice_kernel<8>);
+    else lattice(ctc_lattice_kernel<16>);
+    if (grad_btc) {
+      cfm_launch(ctc_grad_base_kernel, dim3((unsigned)std::min<long>(((long)T * C + 255) / 256, 512), B), dim3(256), 0, st,
+                 a);
+      cfm_launch(ctc_post_kernel, dim3((unsigned)((T + 3) / 4), B), dim3(256), (uint32_t)(4 * S * 4), st, a);
+    }
     HIP_OK(hipGetLastError());
   });
 }
