@@ -167,7 +167,13 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
-constexpr int NST = 4;                    // ring stages (prefetch distance NST - 1)
+#ifndef CFM_TN_NST
+#define CFM_TN_NST 3
+#endif
+// ring stages (prefetch distance NST - 1): 3 x 16 KB, so three blocks (12 waves) share a CU's LDS; same-box
+// training A/B (tools/train_lib_ab.sh): 31.49-31.61 ms/step at 3 stages against 31.70-31.77 at 4, 2 and 5
+// stages slower than 4
+constexpr int NST = CFM_TN_NST;
 constexpr int STAGE = 2 * TK * 256;       // A and B images of one K-step (16 KB)
 
 // General form (both weight gradients and the attention backward's batched products):
