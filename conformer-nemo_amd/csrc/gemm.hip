@@ -920,21 +920,27 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
   const uint32_t sbase = lds_addr(smem);
   const int nk = p.kb / 128;
 
-  const int tapb = (int)aload.tapb;   // bytes of one 3x3 tap (C * 2); a K-half never straddles two
   auto issue = [&](int kt, int h) {   // K-half h of K-tile kt, A then B: 4 glds
     const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
     const bool live = kt < nk;        // past the end: the zero page (uniform vmcnt counts)
     const int kb0 = kt * 128 + h * 64;
-    int tap = 0;                      // wave-uniform: count the tap boundaries below kb0 (no division)
+    if constexpr (ALoad::kConv) {
+      const int tapb = (int)aload.tapb;   // bytes of one 3x3 tap (C * 2); a K-half never straddles two
+      int tap = 0;                        // wave-uniform: count the tap boundaries below kb0 (no division)
 #pragma unroll
-    for (int t = 1; t < 9; ++t) tap += kb0 >= t * tapb ? 1 : 0;
-    const int tr = (tap >= 3 ? 1 : 0) + (tap >= 6 ? 1 : 0), tf = tap - 3 * tr;
-    const long toff = ((long)tr * aload.F1 + tf) * tapb + (kb0 - tap * tapb);
+      for (int t = 1; t < 9; ++t) tap += kb0 >= t * tapb ? 1 : 0;
+      const int tr = (tap >= 3 ? 1 : 0) + (tap >= 6 ? 1 : 0), tf = tap - 3 * tr;
+      const long toff = ((long)tr * aload.F1 + tf) * tapb + (kb0 - tap * tapb);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool v = live && ((ast.valid[i] >> tap) & 1u);
-      const char* src = v ? ast.base[i] + toff + lo[i] : zsrc;
-      glds16_asm(src, base + (i * 8 + wave) * 1024);
+      for (int i = 0; i < 2; ++i) {
+        const bool v = live && ((ast.valid[i] >> tap) & 1u);
+        const char* src = v ? ast.base[i] + toff + lo[i] : zsrc;
+        glds16_asm(src, base + (i * 8 + wave) * 1024);
+      }
+    } else {   // dense rows (GEMM A operand): rows past M and bytes past K read the zero page
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        glds16_asm(live ? aload.src(ast, i, kb0, lo[i]) : (const void*)zsrc, base + (i * 8 + wave) * 1024);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
@@ -1318,6 +1324,10 @@ int packed_width(const GemmEpi& epi, int N) {
 int g_tile_override = [] { const char* s = getenv("CFM_GEMM_TILE"); return s ? atoi(s) : -1; }();
 // the 8-phase kernel for the conv2 implicit GEMM (CFM_GEMM8=0: the tiled kernel, A/B)
 int g_gemm8 = [] { const char* s = getenv("CFM_GEMM8"); return s ? atoi(s) : 1; }();
+// ... and for the dense Swish GEMMs (CFM_GEMM8_DENSE=1; off by default: at K = 512 the 8-phase loop
+// measured no faster than the tiled 256x256 kernel in the forward (4.957-4.966 against 4.963-4.968 ms)
+// and 0.07 ms slower per training step - these GEMMs lose their time in the fill and the epilogue)
+int g_gemm8_dense = [] { const char* s = getenv("CFM_GEMM8_DENSE"); return s ? atoi(s) : 0; }();
 // write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 
@@ -1452,6 +1462,21 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
   p.probe = g_gemm_probe;
+  // the 8-phase 256x256 kernel for the un-folded Swish GEMMs (FFN linear1 + Swish; training's z / u
+  // pair): bf16, 128-byte K-tiles, N on the 256 granule of the packed weight, no LayerNorm fold
+  if (dtype == DT_BF16 && g_gemm8_dense && g_tile_override < 0 && !epi.ln_in && epi.utt_tp <= 0 &&
+      (epi.mode == EPI_SWISH || epi.mode == EPI_SWISH_Z) && p.kb % 128 == 0 && M >= 4096 && N >= 1024 &&
+      (lda * es) % 16 == 0) {
+    ALoadDense<2> al;
+    a.fill(al);
+    p.Mtiles = (M + 255) / 256;
+    p.Ntiles = (N + 255) / 256;
+    if (epi.mode == EPI_SWISH)
+      cfm_launch((gemm8_kernel<EPI_SWISH, ALoadDense<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    else
+      cfm_launch((gemm8_kernel<EPI_SWISH_Z, ALoadDense<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    return;
+  }
   int tile = pick_tile(dtype, M, packed_width(epi, N), epi.mode, false, K);
   if (dtype == DT_F32) dispatch<float, ALoadDense>(tile, p, a, st);
   else dispatch<bf16_t, ALoadDense>(tile, p, a, st);
