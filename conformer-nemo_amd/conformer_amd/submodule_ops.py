@@ -213,3 +213,47 @@ class LayerRunner:
         enc.set_pad_mask(use_pad_mask)
         pe = None if pos_emb is None else pos_emb.reshape(-1, d)
         return enc.layers_forward(x, lengths, pe)
+
+
+def _heads_for(d: int) -> int:
+    """A head count the zero-layer handle accepts (d % h == 0, d / h <= 128); heads are unused there."""
+    h = max(1, -(-d // 128))
+    while d % h:
+        h += 1
+    return h
+
+
+class SubsamplingRunner:
+    """ConvSubsampling ('striding', factor 4) on a zero-layer native encoder handle without xscaling:
+    cfm_encoder_forward then runs exactly conv.0 + ReLU, conv.2 + ReLU (implicit-GEMM MFMA) and the
+    output Linear - the encoder's own front-end kernels (subsampling.py:163-176)."""
+
+    def __init__(self):
+        self._handles = {}
+        self._versions = {}
+
+    def forward(self, module, x: torch.Tensor, lengths: torch.Tensor, compute: str):
+        from .runtime import NativeEncoder, make_cfg
+        B, T, F = x.shape
+        C = module.conv[0].out_channels
+        d = module.out.out_features
+        dev = x.device
+        key = (dev.index, compute, F, C, d)
+        enc = self._handles.get(key)
+        if enc is None:
+            with torch.cuda.device(dev):
+                cfg = make_cfg(F, 0, d, n_heads=_heads_for(d), subsampling_conv_channels=C, xscaling=False)
+                enc = NativeEncoder(cfg, device=dev.index, compute=compute)
+            self._handles[key] = enc
+        sd = module.state_dict(keep_vars=True)
+        version = tuple((t.data_ptr(), t._version) for t in sd.values())
+        if self._versions.get(key) != version:
+            with torch.cuda.device(dev):
+                enc.set_weights({"pre_encode." + k: v for k, v in sd.items()})
+            self._versions[key] = version
+        x_bft = x.detach().transpose(1, 2).to(torch.float32).contiguous()
+        y, ylen = enc.forward(x_bft, lengths)
+        return y.transpose(1, 2), ylen
+
+
+SUBSAMPLING = SubsamplingRunner()

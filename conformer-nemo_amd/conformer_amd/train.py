@@ -66,6 +66,7 @@ class EncoderTrainer:
         self._ready_cb = None
         self._group = None
         self.world = 1
+        self.use_pad_mask = True   # ConformerEncoder.enable_pad_mask: the conv module's pad mask
         self.grad_buckets = None   # conformer_amd.dist.GradBuckets (data parallelism), or None
 
     # ---- SyncBatchNorm plumbing ---------------------------------------------------------------
@@ -159,6 +160,7 @@ class EncoderTrainer:
         tape = torch.empty(int(self.lib.cfm_train_tape_size(self.native.handle, B, T)), dtype=torch.uint8,
                            device=self.device)
         ws = self._workspace(B, T)
+        self.native.set_pad_mask(self.use_pad_mask)
         o = self._opts(dropout, seed, update_running_stats, bn_momentum, dropout_emb, dropout_att)
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_forward(self.native.handle, self._ptrs(params), len(params), x.data_ptr(),
@@ -166,7 +168,7 @@ class EncoderTrainer:
                                               y.data_ptr(), ylen.data_ptr(), tape.data_ptr(), tape.numel(),
                                               ws.data_ptr(), ws.numel(), st), "cfm_train_forward")
         state = dict(tape=tape, B=B, T=T, dropout=dropout, seed=seed, bn_momentum=bn_momentum, x=x, ln=ln,
-                     dropout_emb=dropout_emb, dropout_att=dropout_att)
+                     dropout_emb=dropout_emb, dropout_att=dropout_att, use_pad_mask=self.use_pad_mask)
         return y, ylen, state
 
     def backward(self, dy_bdt: torch.Tensor, state: Dict, params: Sequence[torch.Tensor],
@@ -197,6 +199,7 @@ class EncoderTrainer:
             # backward is done
             gb.queue_finish()
         tape = state["tape"]
+        self.native.set_pad_mask(state.get("use_pad_mask", True))   # the forward's setting
         st = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
         _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
                                                state["B"], state["T"], ctypes.byref(o), self._ptrs(out),

@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) void glu_fwd_kernel(const float* __restrict__ 
     const int c = (int)(i - m * d);
     const int b = (int)(m / Tp), t = (int)(m - (long)b * Tp);
     const float a = pre[m * 2 * d + c], gg = pre[m * 2 * d + d + c];
-    const float v = (t < lens[b]) ? a * (1.0f / (1.0f + expf(-gg))) : 0.0f;
+    const float v = (!lens || t < lens[b]) ? a * (1.0f / (1.0f + expf(-gg))) : 0.0f;   // lens null: no pad mask
     g[i] = v;
     st_f<T>(gt + i, v);
   }
@@ -1633,6 +1633,9 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
   const long HP = (long)H * dkp;
   int32_t* lens = S.T_<int32_t>(S.tp.lens);
   calc_length(len_b, lens, g.B, g.T, 2, st);
+  // enable_pad_mask(False) (conformer_encoder.py:269-272): the conv module's GLU output is not zeroed on
+  // padded frames (the attention masks stay); the backward reads the same handle flag
+  const int32_t* glu_lens = S.h->use_pad_mask ? lens : nullptr;
   HIP_OK(hipMemcpyAsync(S.T_(S.tp.xin), x_bft, (size_t)g.B * g.F * g.T * 4, hipMemcpyDeviceToDevice, st));
 
   // ---- ConvSubsampling (subsampling.py:163-176) + xscale + embedding dropout ----
@@ -1735,10 +1738,10 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
       S.gemm_f32out(S.T_(t.hn[2]), d, M, d, S.W_(S.wl.wpw1), 2 * d, S.W_<float>(S.wl.bpw1), 1.0f, pre, 2 * d, false);
       if (dt == DT_F32)
         cfm_launch(glu_fwd_kernel<float>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)pre,
-                   (const int32_t*)lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<float>(S.wl.gt));
+                   (const int32_t*)glu_lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<float>(S.wl.gt));
       else
         cfm_launch(glu_fwd_kernel<bf16_t>, dim3(ew_grid(n_md)), dim3(256), 0, st, (const float*)pre,
-                   (const int32_t*)lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<bf16_t>(S.wl.gt));
+                   (const int32_t*)glu_lens, g.Tp, d, (long)M, S.T_<float>(t.g), S.W_<bf16_t>(S.wl.gt));
       // depthwise conv + bias (fp32 pre-norm output; [K][d] weight layout of the forward kernel)
       pack_matrix(DT_F32, S.prm(q.dw_w), g.K, d, g.K, true, S.W_(S.wl.dww), d, g.K, d, st);
       float* dwo = S.W_<float>(S.wl.dwo);
@@ -2036,7 +2039,8 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
                                                   Gp(q.dw_w), Gp(q.dw_b), red, dwws, st);
       if (s != CFM_OK) fail(s, std::string("dwconv backward: ") + g_last_error);
       float* dpre = S.W_<float>(S.wl.dpre);
-      const cfm_status s2 = cfm_op_glu_backward(S.T_<const float>(t.pre), dG, lens, g.B, g.Tp, d, dpre, st);
+      const cfm_status s2 = cfm_op_glu_backward(S.T_<const float>(t.pre), dG, h->use_pad_mask ? lens : nullptr, g.B,
+                                                g.Tp, d, dpre, st);
       if (s2 != CFM_OK) fail(s2, std::string("glu backward: ") + g_last_error);
       float* dhn = S.W_<float>(S.wl.dctx);
       linear_bwd(dpre, 2 * d, S.prm(q.pw1_w), d, S.T_(t.hn[2]), d, 0, Drop{0, 0, 1.0f}, dhn, d, false, q.pw1_w,

@@ -2,8 +2,9 @@
 
 Only the 'striding' mode (2 x Conv2d(3, stride 2, pad 1) + ReLU, then Linear(C * F/4 -> d)) is
 on the north-star path and implemented natively (the 2nd conv runs as an implicit-GEMM MFMA
-kernel, csrc/gemm.hip).  The module holds the parameters with the reference's names; its
-arithmetic runs inside ConformerEncoder's native forward.
+kernel, csrc/gemm.hip).  The module holds the parameters with the reference's names; inside
+ConformerEncoder its arithmetic runs in the encoder's native forward, and called on its own (eval) it
+runs the same front-end kernels on a zero-layer handle.
 """
 from __future__ import annotations
 
@@ -49,4 +50,13 @@ class ConvSubsampling(nn.Module):
         self.out = nn.Linear(conv_channels * f, feat_out)
 
     def forward(self, x, lengths):
-        raise NotImplementedError("ConvSubsampling runs inside ConformerEncoder's native forward")
+        """subsampling.py:163-176: x (B, T, feat_in) -> ((B, T', feat_out), lengths (B,) int32), on the
+        encoder's front-end kernels (eval; a zero-layer native handle, see submodule_ops.SubsamplingRunner)."""
+        from conformer_amd import submodule_ops as ops
+        ops.check_inference(self, x)
+        if not isinstance(self.conv[1], nn.ReLU):
+            raise NotImplementedError("the native subsampling fuses ReLU; other activations are not implemented")
+        if x.dim() != 3:
+            raise ValueError("ConvSubsampling expects x of shape (B, T, feat_in)")
+        lengths = torch.as_tensor(lengths, device=x.device)
+        return ops.SUBSAMPLING.forward(self, x, lengths, ops.compute_mode(self))

@@ -1,5 +1,5 @@
 """Golden fixtures for the standalone submodules (ConformerLayer, ConformerFeedForward, ConformerConvolution,
-RelPositionMultiHeadAttention, MultiHeadAttention) from the REFERENCE modules (only where /root/reference
+RelPositionMultiHeadAttention, MultiHeadAttention, ConvSubsampling) from the REFERENCE modules (only where /root/reference
 exists; loaded as gen_goldens.load_reference does):
 
     python tests/golden/gen_submodule_goldens.py      # writes tests/golden/sub_*.npz
@@ -101,6 +101,16 @@ def main():
         x2 = torch.randn(B, T, d, generator=g)
         y = mha(query=x, key=x2, value=x2, mask=att)
         save("mha", x=x.numpy(), x2=x2.numpy(), att_mask=att.numpy(), y=y.numpy(), **w)
+        # ConvSubsampling ('striding', factor 4): x (B, T, feat_in) with ragged lengths (subsampling.py:163-176)
+        for case, (Bs, Ts, F, C, dd, seed) in (("subsampling", (3, 101, 80, 64, 96, 8)),
+                                                 ("subsampling_c176", (2, 64, 40, 176, 176, 9))):
+            sub = R.sub.ConvSubsampling(subsampling="striding", subsampling_factor=4, feat_in=F, feat_out=dd,
+                                        conv_channels=C, activation=torch.nn.ReLU()).eval()
+            w = randomize(sub, seed)
+            xs = torch.randn(Bs, Ts, F, generator=g)
+            ls = torch.tensor([Ts - 29 * i for i in range(Bs)])
+            ys, ylen = sub(xs, ls)
+            save(case, x=xs.numpy(), lengths=ls.numpy(), y=ys.numpy(), y_len=ylen.numpy(), **w)
 
 
 if __name__ == "__main__":

@@ -18,7 +18,7 @@ import torch
 from conftest import GOLDEN, rel_l2
 
 pytestmark = pytest.mark.gpu
-CASES = ["train_tiny", "train_tiny_dk10", "train_tiny_ctx"]
+CASES = ["train_tiny", "train_tiny_dk10", "train_tiny_ctx", "train_tiny_nopad"]
 GATE_Y = {"fp32": 1e-3, "bf16": 2e-2}
 GATE_G = {"fp32": 1e-3, "bf16": 6e-2}
 
@@ -32,6 +32,8 @@ def _encoder(z, compute, dropout=0.0):
     ref = enc.state_dict()
     enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref[k].shape) for k, v in sd.items()})
     enc.set_compute_mode(compute)
+    if "use_pad_mask" in z.files and not bool(z["use_pad_mask"]):   # train_tiny_nopad: enable_pad_mask(False)
+        enc.enable_pad_mask(False)
     return enc.cuda().train()
 
 
