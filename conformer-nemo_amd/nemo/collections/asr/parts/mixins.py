@@ -61,11 +61,18 @@ class ASRBPEMixin:
                              "based tokenizer")
         tdir = tokenizer_cfg["dir"]        # `???` in the yamls: MissingMandatoryValue until set
         self.tokenizer_dir, self.tokenizer_type = tdir, ttype
+        # the files are registered as .nemo artifacts (mixins.py:85-151): save_to packs them, a restored
+        # config's `nemo:` paths resolve to the archive's copies (no dependency on the original dir)
         if ttype == "bpe":
             path = tokenizer_cfg.get("model_path") or os.path.join(tdir, "tokenizer.model")
+            path = self.register_artifact("tokenizer.model_path", path)
+            for key, default in (("vocab_path", "vocab.txt"), ("spe_tokenizer_vocab", "tokenizer.vocab")):
+                self.register_artifact("tokenizer." + key, tokenizer_cfg.get(key) or os.path.join(tdir, default),
+                                       verify_src_exists=False)
             self.tokenizer = SentencePieceTokenizer(path)
         else:
             path = tokenizer_cfg.get("vocab_path") or os.path.join(tdir, "vocab.txt")
+            path = self.register_artifact("tokenizer.vocab_path", path)
             self.tokenizer = WordPieceTokenizer(path)
 
     def _tokenizer_vocabulary(self) -> List[str]:

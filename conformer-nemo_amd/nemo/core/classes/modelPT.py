@@ -7,7 +7,13 @@ through the SaveRestoreConnector, and sets up the optimizer + scheduler its `opt
 from __future__ import annotations
 
 import math
-from typing import Any, Mapping, Optional
+import os
+import shutil
+import tempfile
+import threading
+import uuid
+import weakref
+from typing import Any, Dict, Mapping, Optional
 
 import torch
 
@@ -67,9 +73,37 @@ def _check_targets(conf: Any, where: str, path: str = "model") -> None:
             _check_targets(v, where, f"{path}[{i}]")
 
 
+# The artifact folder of the .nemo being restored (thread-local, set while restore_from builds the model):
+# `nemo:<name>` artifact paths in its config resolve there (save_restore_connector.py:333-336).
+_RESTORE = threading.local()
+
+
+def _restored_member(name: str) -> str:
+    """Path of archive member `name` of the .nemo being restored; only plain member names resolve (no
+    directories, no '..'), so a config cannot point outside the extraction folder."""
+    folder = getattr(_RESTORE, "folder", None)
+    if folder is None:
+        raise FileNotFoundError(f"nemo:{name}: artifact paths resolve only while restoring a .nemo file")
+    if not name or name != os.path.basename(name) or name in (".", ".."):
+        raise FileNotFoundError(f"nemo:{name}: not a plain archive member name")
+    path = os.path.join(folder, name)
+    if not os.path.isfile(path):
+        raise FileNotFoundError(f"nemo:{name}: no such member in the archive")
+    return path
+
+
+def _set_path(cfg: Dict[str, Any], dotted: str, value: Any) -> None:
+    node = cfg
+    keys = dotted.split(".")
+    for k in keys[:-1]:
+        node = node.setdefault(k, {})
+    node[keys[-1]] = value
+
+
 class ModelPT(NeuralModule):
     def __init__(self, cfg: Any, trainer=None):
         super().__init__()
+        self.__dict__.setdefault("_artifacts", {})   # config path -> local file (register_artifact)
         if isinstance(cfg, Mapping) and not isinstance(cfg, Config):
             cfg = Config(cfg)
         if isinstance(cfg, Config) and "model" in cfg and "encoder" not in cfg:
@@ -88,19 +122,64 @@ class ModelPT(NeuralModule):
         """Build from a reference experiment yaml (`model:` block), `${}` resolved, `???` kept."""
         return cls(load_config(path, overrides).model, trainer=trainer)
 
+    # --- artifacts (modelPT.py register_artifact -> save_restore_connector.py:304-358) -----------
+    def register_artifact(self, config_path: str, src: Optional[str], verify_src_exists: bool = True) -> Optional[str]:
+        """A file the model needs (tokenizer model / vocabulary) that its .nemo carries: `src` is a local
+        path, or `nemo:<member>` while restoring.  Returns the local path to use (None for a missing
+        optional artifact); save_to packs the file and writes `nemo:<uuid>_<name>` at `config_path`."""
+        src = "" if src is None else str(src)
+        if src.startswith("nemo:"):
+            path = _restored_member(src[5:])
+        elif src and os.path.exists(os.path.abspath(src)):
+            path = os.path.abspath(src)
+        elif verify_src_exists:
+            raise FileNotFoundError(f"src path does not exist or it is not a path in nemo file. src value I got "
+                                    f"was: {src}. Absolute: {os.path.abspath(src)}")
+        else:
+            return None
+        self.__dict__.setdefault("_artifacts", {})[config_path] = path
+        return path
+
+    @property
+    def artifacts(self) -> Dict[str, str]:
+        return dict(self.__dict__.get("_artifacts", {}))
+
     # --- .nemo I/O (modelPT.py save_to / restore_from through the connector) -----------------
     def save_to(self, save_path: str) -> None:
         from nemo.core.connectors.save_restore_connector import SaveRestoreConnector
-        SaveRestoreConnector().save_to({"model": self._cfg.to_dict()} if isinstance(self._cfg, Config) else self._cfg,
-                                       self.state_dict(), save_path)
+        cfg = self._cfg.to_dict() if isinstance(self._cfg, Config) else dict(self._cfg)
+        packed: Dict[str, bytes] = {}
+        for config_path, local in self.artifacts.items():   # _handle_artifacts (:360-396): copy into the archive
+            with open(local, "rb") as f:
+                data = f.read()
+            name = f"{uuid.uuid4().hex}_{os.path.basename(local)}"
+            packed[name] = data
+            _set_path(cfg, config_path, "nemo:" + name)
+        SaveRestoreConnector().save_to({"model": cfg}, self.state_dict(), save_path, artifacts=packed)
 
     @classmethod
     def restore_from(cls, restore_path: str, map_location=None, strict: bool = True, override_config_path=None):
         from nemo.core.connectors.save_restore_connector import SaveRestoreConnector
-        conf, sd = SaveRestoreConnector().load_config_and_state_dict(
-            restore_path, override_config_path=override_config_path, map_location="cpu")
+        conn = SaveRestoreConnector()
+        conf, sd = conn.load_config_and_state_dict(restore_path, override_config_path=override_config_path,
+                                                   map_location="cpu")
         _check_targets(conf, restore_path)
-        model = cls(Config(conf))
+        # the archive's artifact members, written under plain names into a private folder that lives as
+        # long as the model (nemo: paths in the config resolve there while the model is built)
+        folder = tempfile.mkdtemp(prefix="nemo_artifacts_")
+        for name, data in conn.artifact_members(restore_path).items():
+            with open(os.path.join(folder, name), "wb") as f:
+                f.write(data)
+        prev = getattr(_RESTORE, "folder", None)
+        _RESTORE.folder = folder
+        try:
+            model = cls(Config(conf))
+        except BaseException:
+            shutil.rmtree(folder, ignore_errors=True)
+            raise
+        finally:
+            _RESTORE.folder = prev
+        weakref.finalize(model, shutil.rmtree, folder, True)
         model.load_state_dict(sd, strict=strict)
         if map_location is not None:
             model = model.to(map_location)

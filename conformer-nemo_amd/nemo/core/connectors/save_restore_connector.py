@@ -145,6 +145,18 @@ class SaveRestoreConnector:
         state_dict = self._load_state_dict_from_bytes(members[self.model_weights_ckpt], map_location)
         return conf, state_dict
 
+    def artifact_members(self, restore_path: str) -> Dict[str, bytes]:
+        """The archive's artifact files (every member but the config and the weights) whose names are plain
+        file names - what `nemo:<name>` config paths refer to (:333-336); anything with a directory
+        part or '..' is ignored, so nothing is written outside the caller's folder."""
+        out = {}
+        for name, data in self._read_nemo_members(restore_path).items():
+            if name in (self.model_config_yaml, self.model_weights_ckpt):
+                continue
+            if name and name == os.path.basename(name) and name not in (".", ".."):
+                out[name] = data
+        return out
+
     def extract_state_dict_from(self, restore_path: str, save_dir: str, split_by_module: bool = False):
         """`extract_state_dict_from` (:212-285): model_weights.ckpt, or one `<module>.ckpt` per
         top-level prefix when split_by_module; returns the full state dict."""

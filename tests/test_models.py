@@ -114,6 +114,46 @@ def test_save_restore_roundtrip(tok_dir, tmp_path):
     assert a.keys() == b.keys() and all(torch.equal(a[k], b[k]) for k in a)
 
 
+def test_nemo_carries_tokenizer(tok_dir, tmp_path):
+    """The tokenizer files are .nemo artifacts (reference mixins.py:85-151, save_restore_connector.py:304-396):
+    a saved model restores after its tokenizer directory is gone, with the same vocabulary."""
+    import shutil
+    from nemo.collections.asr.models import EncDecCTCModelBPE
+    from nemo.core.config import load_config
+    tdir = str(tmp_path / "tok")
+    shutil.copytree(tok_dir, tdir)
+    m = EncDecCTCModelBPE(load_config(CTC_BPE_SMALL, {"model.tokenizer.dir": tdir}).model)
+    path = str(tmp_path / "m.nemo")
+    m.save_to(path)
+    shutil.rmtree(tdir)
+    r = EncDecCTCModelBPE.restore_from(path)
+    assert r.tokenizer.get_vocab() == m.tokenizer.get_vocab()
+    assert str(r.cfg.tokenizer.model_path).startswith("nemo:")              # the archive member
+    assert os.path.isfile(r.artifacts["tokenizer.model_path"])                 # ... extracted for the model
+    a, b = m.state_dict(), r.state_dict()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    # a restored model saves again with its artifacts (round trip of a round trip)
+    path2 = str(tmp_path / "m2.nemo")
+    r.save_to(path2)
+    assert EncDecCTCModelBPE.restore_from(path2).tokenizer.get_vocab() == m.tokenizer.get_vocab()
+
+
+def test_nemo_artifact_paths_stay_inside_the_archive(tok_dir, tmp_path):
+    """`nemo:` paths name plain archive members only: '../x' or a directory part is refused."""
+    import yaml
+    from nemo.collections.asr.models import EncDecCTCModelBPE
+    from nemo.core.config import load_config
+    from nemo.core.connectors import SaveRestoreConnector
+    m = EncDecCTCModelBPE(load_config(CTC_BPE_SMALL, {"model.tokenizer.dir": tok_dir}).model)
+    cfg = m.cfg.to_dict()
+    cfg["tokenizer"]["model_path"] = "nemo:../../etc/passwd"
+    path = str(tmp_path / "bad.nemo")
+    SaveRestoreConnector._make_nemo_file_from_members(path, {
+        "model_config.yaml": yaml.safe_dump(cfg).encode(), "model_weights.ckpt": _state_bytes(m)})
+    with pytest.raises(FileNotFoundError, match="plain archive member"):
+        EncDecCTCModelBPE.restore_from(path)
+
+
 def test_restore_refuses_foreign_targets(tok_dir, tmp_path):
     """A .nemo config is untrusted: a `_target_` outside this package's drop-in modules is refused
     before anything is instantiated (nothing in the file runs)."""
