@@ -24,7 +24,7 @@ STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "UNSUPPORTED", 3: "HIP", 4: "WORKS
 EXPORTED_SYMBOLS = (
     "cfm_last_error", "cfm_version", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
-    "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
+    "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_abs_pos", "cfm_encoder_abs_pos", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
     "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
     "cfm_op_rel_attention", "cfm_bench_gemm", "cfm_encoder_layers_workspace_size", "cfm_encoder_layers_forward",
     "cfm_op_conv_glu_dwconv_ws_size", "cfm_op_conv_glu_dwconv",
@@ -128,6 +128,8 @@ def load() -> ctypes.CDLL:
         "cfm_encoder_max_audio_length": (ci, [vp]),
         "cfm_encoder_set_microbatches": (ci, [vp, ci]),
         "cfm_encoder_set_pad_mask": (ci, [vp, ci]),
+        "cfm_encoder_set_abs_pos": (ci, [vp, ci]),
+        "cfm_encoder_abs_pos": (ci, [vp]),
         "cfm_encoder_workspace_size": (sz, [vp, ci, ci]),
         "cfm_encoder_forward": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp]),
         "cfm_num_stages": (ci, []),

@@ -109,6 +109,15 @@ class NativeEncoder:
         """enable_pad_mask (conformer_encoder.py:301-305): off -> conv module runs with pad_mask=None."""
         _lib.check(self.lib.cfm_encoder_set_pad_mask(self.handle, 1 if on else 0), "set_pad_mask")
 
+    def set_abs_pos(self, on: bool) -> None:
+        """self_attention_model='abs_pos': absolute sinusoids added after the xscale and plain
+        MultiHeadAttention in the layers (cfm_encoder_set_abs_pos).  Clears the weights."""
+        _lib.check(self.lib.cfm_encoder_set_abs_pos(self.handle, 1 if on else 0), "set_abs_pos")
+
+    @property
+    def abs_pos(self) -> bool:
+        return bool(self.lib.cfm_encoder_abs_pos(self.handle))
+
     def set_microbatches(self, n: int) -> None:
         """Split each forward's batch over up to n concurrent streams (bitwise-identical results)."""
         _lib.check(self.lib.cfm_encoder_set_microbatches(self.handle, int(n)), "set_microbatches")

@@ -179,7 +179,7 @@ class LayerRunner:
         self._versions = {}
 
     def forward(self, layer, x: torch.Tensor, lengths: torch.Tensor, pos_emb: Optional[torch.Tensor],
-                ctx: Tuple[int, int], use_pad_mask: bool, compute: str) -> torch.Tensor:
+                ctx: Tuple[int, int], use_pad_mask: bool, compute: str, abs_pos: bool = False) -> torch.Tensor:
         from .runtime import NativeEncoder, make_cfg
         d = layer.norm_out.normalized_shape[0]
         d_ff = layer.feed_forward1.linear1.out_features
@@ -187,7 +187,7 @@ class LayerRunner:
             raise NotImplementedError(f"d_ff={d_ff} is not a multiple of d_model={d} (the native layer's FFN width "
                                       "is d_model * ff_expansion_factor)")
         dev = x.device
-        key = (dev.index, compute, ctx)
+        key = (dev.index, compute, ctx, abs_pos)
         enc = self._handles.get(key)
         norm_type = "batch_norm" if isinstance(layer.conv.batch_norm, torch.nn.BatchNorm1d) else "layer_norm"
         if enc is None:
@@ -196,6 +196,8 @@ class LayerRunner:
                                subsampling_conv_channels=_FRONT_CH, att_context_size=list(ctx),
                                conv_kernel_size=layer.conv.depthwise_conv.kernel_size[0], conv_norm_type=norm_type)
                 enc = NativeEncoder(cfg, device=dev.index, compute=compute)
+                if abs_pos:   # MultiHeadAttention: positional projection and biases packed as zeros
+                    enc.set_abs_pos(True)
             self._handles[key] = enc
         sd = layer.state_dict(keep_vars=True)
         version = tuple((t.data_ptr(), t._version) for t in sd.values())

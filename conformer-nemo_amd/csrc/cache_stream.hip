@@ -595,6 +595,7 @@ cfm_status cfm_cache_stream_create(cfm_encoder* enc, int batch, int chunk, int l
     if (batch < 1 || chunk < 1) fail(CFM_ERR_INVALID_ARG, "batch and chunk must be >= 1");
     if (left_context < 1 || left_context >= enc->max_len || left_context > 2048)
       fail(CFM_ERR_INVALID_ARG, "left_context must be in [1, min(pos_emb_max_len - 1, 2048)]");
+    if (enc->abs_pos) fail(CFM_ERR_UNSUPPORTED, "cache-aware streaming is implemented for rel_pos encoders");
     if (enc->C % 8 != 0) fail(CFM_ERR_INVALID_ARG, "subsampling channels must be a multiple of 8");
     if (enc->dkp % 16 != 0 || enc->dkp > 128) fail(CFM_ERR_INVALID_ARG, "head width must be at most 128");
     std::unique_ptr<cfm_cache_stream> s(new cfm_cache_stream);

@@ -41,6 +41,11 @@ struct cfm_encoder {
   // relative positional table (compute type), rows = 2*max_len - 1
   char* pe = nullptr;
   int max_len = 0;
+  // self_attention_model='abs_pos' (cfm_encoder_set_abs_pos): PositionalEncoding adds pe_abs rows
+  // 0 .. T'-1 (fp32, max_len x d) to the scaled embedding, and the layers' linear_pos / pos_bias_u /
+  // pos_bias_v are packed as zeros, which turns the rel-pos attention into MultiHeadAttention exactly
+  bool abs_pos = false;
+  float* pe_abs = nullptr;
   // micro-batch concurrency: the batch is split into `microbatches` parts run on their own streams
   int microbatches = 1;
   // enable_pad_mask (conformer_encoder.py:301-305): false -> the conv module's GLU output is not

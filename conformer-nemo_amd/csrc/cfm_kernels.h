@@ -223,6 +223,8 @@ void rel_pos_attention_backward(int dtype, const void* qk, long ldqk, const void
                                 float* dv, long ld_dqkv, float* dpos, long ld_dpos, float* du, float* dvb, char* ws,
                                 hipStream_t st, Drop adrop = Drop{0u, 0u, 1.0f});
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st);
+// X (B*T', d fp32) += pe[t] (rows of d fp32), d % 4 == 0
+void add_rows_f32(float* X, const float* pe, int B, int Tp, int d, hipStream_t st);
 
 // Weight gradient on frame-major operands (wgrad_tn.hip, bf16): out[n][k] (fp32, ld ldo) = sum over
 // rows r of A[r][n] * B'[r][k] with B' = B (bfn 0) or dropout(swish(B)) (bfn 1, mask index r*ldb + k),

@@ -316,6 +316,29 @@ void build_pe(cfm_encoder* h, int max_len) {
   HIP_OK(hipMalloc(&h->pe, host.size()));
   HIP_OK(hipMemcpy(h->pe, host.data(), host.size(), hipMemcpyHostToDevice));
   h->max_len = max_len;
+  if (h->pe_abs) (void)hipFree(h->pe_abs);
+  h->pe_abs = nullptr;
+  if (h->abs_pos) {
+    // PositionalEncoding.extend_pe/create_pe (multi_head_attention.py:235-255): positions 0 .. max_len-1,
+    // float32 in every compute mode (it is added to the fp32 residual stream)
+    std::vector<float> abs_host((size_t)max_len * d);
+    for (int p = 0; p < max_len; ++p)
+      for (int c = 0; c < d; ++c) {
+        const float a = (float)p * div[c / 2];
+        abs_host[(size_t)p * d + c] = (c % 2 == 0) ? std::sin(a) : std::cos(a);
+      }
+    HIP_OK(hipMalloc(&h->pe_abs, abs_host.size() * 4));
+    HIP_OK(hipMemcpy(h->pe_abs, abs_host.data(), abs_host.size() * 4, hipMemcpyHostToDevice));
+  }
+}
+
+// names of the positional parameters an abs_pos encoder does not have (packed as zeros)
+bool is_rel_pos_param(const std::string& key) {
+  auto ends = [&](const char* s) {
+    const size_t n = std::strlen(s);
+    return key.size() >= n && key.compare(key.size() - n, n, s) == 0;
+  };
+  return ends(".self_attn.linear_pos.weight") || ends(".self_attn.pos_bias_u") || ends(".self_attn.pos_bias_v");
 }
 
 void ensure_streams(cfm_encoder* h, int n) {
@@ -462,6 +485,7 @@ void cfm_encoder_destroy(cfm_encoder* h) {
   if (!h) return;
   if (h->wbuf) (void)hipFree(h->wbuf);
   if (h->pe) (void)hipFree(h->pe);
+  if (h->pe_abs) (void)hipFree(h->pe_abs);
   if (h->zero_page) (void)hipFree(h->zero_page);
   for (auto st : h->sub_streams) (void)hipStreamDestroy(st);
   for (auto ev : h->sub_events) (void)hipEventDestroy(ev);
@@ -502,6 +526,16 @@ cfm_status cfm_encoder_set_weights(cfm_encoder* h, const cfm_tensor_view* table,
       } else {
         W[key] = table[i].data;
       }
+    }
+    // abs_pos: MultiHeadAttention has no linear_pos / pos_bias_u / pos_bias_v - zeros, whatever is passed
+    std::vector<float> zeros;
+    if (h->abs_pos) {
+      int64_t zmax = 0;
+      for (auto& kv : expect)
+        if (is_rel_pos_param(kv.first)) zmax = std::max(zmax, kv.second);
+      zeros.assign((size_t)zmax, 0.0f);
+      for (auto& kv : expect)
+        if (is_rel_pos_param(kv.first)) W[kv.first] = zeros.data();
     }
     for (auto& kv : expect)
       if (!W.count(kv.first)) fail(CFM_ERR_WEIGHTS, "missing weight: " + kv.first);
@@ -809,6 +843,8 @@ void run_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B
       e.ldx = d;
       gemm(dt, ws + wl.X2, (long)h->F2 * h->C, M, h->F2 * h->C, W(h->sub_w), (int)h->kpad(h->F2 * h->C), d, e,
            h->zero_page, st);
+      // abs_pos: PositionalEncoding.forward adds pe[:, :T'] after the xscale (multi_head_attention.py:265-270)
+      if (h->abs_pos) add_rows_f32(X, h->pe_abs, B, Tp, d, st);
     }
     const char* Pbuf = P_ext ? P_ext : ws + wl.P;
     if (L > 0 && !P_ext) {
@@ -934,6 +970,23 @@ cfm_status cfm_encoder_set_pad_mask(cfm_encoder* h, int on) {
     h->use_pad_mask = on != 0;
   });
 }
+
+cfm_status cfm_encoder_set_abs_pos(cfm_encoder* h, int on) {
+  return guarded([&] {
+    if (!h) fail(CFM_ERR_INVALID_ARG, "null handle");
+    if (h->abs_pos == (on != 0)) return;
+    int prev = 0;
+    HIP_OK(hipGetDevice(&prev));
+    HIP_OK(hipSetDevice(h->device));
+    HIP_OK(hipDeviceSynchronize());
+    h->abs_pos = on != 0;
+    build_pe(h, h->max_len);      // (re)builds pe_abs
+    h->weights_set = false;       // the positional weights are packed differently: set_weights again
+    HIP_OK(hipSetDevice(prev));
+  });
+}
+
+int cfm_encoder_abs_pos(const cfm_encoder* h) { return h && h->abs_pos ? 1 : 0; }
 
 cfm_status cfm_encoder_set_microbatches(cfm_encoder* h, int n) {
   return guarded([&] {

@@ -226,6 +226,19 @@ __global__ void convert_kernel(const float* __restrict__ src, T* __restrict__ ds
     st_f<T>(dst + i, src[i]);
 }
 
+// X (B*T', d) += pe rows 0 .. T'-1 (d % 4 == 0): the absolute positional encoding
+__global__ __launch_bounds__(256) void add_rows_kernel(float4* __restrict__ X, const float4* __restrict__ pe, int Tp,
+                                                       int d4, long n4) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / d4;
+    const int c = (int)(i - row * d4);
+    const float4 p = pe[(long)(row % Tp) * d4 + c];
+    float4 x = X[i];
+    x.x += p.x; x.y += p.y; x.z += p.z; x.w += p.w;
+    X[i] = x;
+  }
+}
+
 }  // namespace
 
 void calc_length(const int32_t* len_in, int32_t* len_out, int B, int T, int repeat, hipStream_t st) {
@@ -294,6 +307,13 @@ void dwconv_norm_swish(int dtype, const void* g, int B, int Tp, int d, int K, co
 void transpose_out(const float* X, int B, int Tp, int d, float* y, hipStream_t st) {
   if (B <= 0 || Tp <= 0) return;
   cfm_launch(transpose_kernel, dim3((Tp + 31) / 32, (d + 31) / 32, B), dim3(256), 0, st, X, Tp, d, y);
+}
+
+void add_rows_f32(float* X, const float* pe, int B, int Tp, int d, hipStream_t st) {
+  const long n4 = (long)B * Tp * (d / 4);
+  if (n4 <= 0) return;
+  const int blocks = (int)std::min<long>((n4 + 255) / 256, 4096);
+  cfm_launch(add_rows_kernel, dim3(blocks), dim3(256), 0, st, (float4*)X, (const float4*)pe, Tp, d / 4, n4);
 }
 
 void convert_f32(int dtype, const float* src, void* dst, long n, hipStream_t st) {

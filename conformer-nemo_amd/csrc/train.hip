@@ -1655,6 +1655,9 @@ void train_forward(Step& S, const float* x_bft, const int32_t* len_b, float* y_b
   float* xcur = g.L > 0 ? S.T_<float>(S.tp.lay[0].x[0]) : S.T_<float>(S.tp.xfin);
   S.gemm_f32out(S.T_(S.tp.X2), (long)g.F2 * g.C, M, g.F2 * g.C, S.W_(S.wl.wsub), d, S.W_<float>(S.wl.bsub), xs, xcur,
                 d, false);
+  // abs_pos: + pe[:, :T'] between the xscale and the embedding dropout (multi_head_attention.py:265-271);
+  // a constant, so the backward is unchanged
+  if (h->abs_pos) add_rows_f32(xcur, h->pe_abs, g.B, g.Tp, d, st);
   {
     const Drop dr = S.drop(0);
     if (dr.thr) cfm_launch(scale_drop_kernel, dim3(ew_grid((long)M * d)), dim3(256), 0, st, (const float*)xcur, 1.0f,

@@ -45,21 +45,23 @@ class ConformerLayer(nn.Module):
         self.norm_out = LayerNorm(d_model)
 
     def forward(self, x, att_mask=None, pos_emb=None, pad_mask=None):
-        """x (B, T, d_model) -> (B, T, d_model) (conformer_modules.py:88-121): macaron FFN, rel-pos MHSA,
-        convolution module, FFN, norm_out, on the native layer stack.  att_mask (B, T, T) / pad_mask (B, T)
-        (True = masked) as ConformerEncoder builds them; pos_emb (1, 2T-1, d_model) from
-        RelPositionalEncoding."""
+        """x (B, T, d_model) -> (B, T, d_model) (conformer_modules.py:88-121): macaron FFN, rel-pos MHSA
+        (or MultiHeadAttention for abs_pos), convolution module, FFN, norm_out, on the native layer stack.
+        att_mask (B, T, T) / pad_mask (B, T) (True = masked) as ConformerEncoder builds them; pos_emb
+        (1, 2T-1, d_model) from RelPositionalEncoding (ignored for abs_pos)."""
         from conformer_amd import submodule_ops as ops
         ops.check_inference(self, x)
-        if self.self_attention_model != "rel_pos":
-            raise NotImplementedError("the native layer stack implements self_attention_model='rel_pos'")
-        if pos_emb is None:
+        abs_pos = self.self_attention_model == "abs_pos"
+        if abs_pos:
+            pos_emb = None   # MultiHeadAttention takes no positional input (conformer_modules.py:106-107)
+        elif pos_emb is None:
             raise ValueError("rel_pos ConformerLayer needs pos_emb (RelPositionalEncoding's output)")
         B, T, _ = x.shape
         lengths, ctx = ops.masks_to_lengths(att_mask, pad_mask, B, T, x.device)
         if not hasattr(self, "_runner"):
             self._runner = ops.LayerRunner()
-        return self._runner.forward(self, x, lengths, pos_emb, ctx, pad_mask is not None, ops.compute_mode(self))
+        return self._runner.forward(self, x, lengths, pos_emb, ctx, pad_mask is not None, ops.compute_mode(self),
+                                    abs_pos=abs_pos)
 
     def set_compute_mode(self, compute: str):
         if compute not in ("bf16", "fp32"):

@@ -83,8 +83,8 @@ const char* cfm_last_error(void);
  *      became active (an older host's shorter struct would leave the callback pointer unset);
  *   3  the *_set_weights of cfm_ctc.h / cfm_joint.h / cfm_rnnt_decode.h are stream-ordered (they no
  *      longer synchronise the stream: a host must keep the sources valid until the stream passes the
- *      call); new entry points cfm_encoder_layers_forward, cfm_op_conv_glu_dwconv, the transducer
- *      training entries of cfm_joint.h / cfm_rnnt_decode.h. */
+ *      call); new entry points cfm_encoder_layers_forward, cfm_op_conv_glu_dwconv, cfm_encoder_set_abs_pos, the
+ *      transducer training entries of cfm_joint.h / cfm_rnnt_decode.h. */
 #define CFM_ABI_VERSION 3
 int cfm_version(void);
 
@@ -111,6 +111,17 @@ int cfm_encoder_max_audio_length(const cfm_encoder* h);
  * the convolution module does not zero padded frames after the GLU (conformer_modules.py:165-166);
  * the attention mask is unchanged.  Default on. */
 cfm_status cfm_encoder_set_pad_mask(cfm_encoder* h, int on);
+
+/* self_attention_model='abs_pos' (conformer_encoder.py:184-189, conformer_modules.py:73-74, 106-107):
+ * on = 1 adds PositionalEncoding's absolute sinusoids (positions 0 .. T'-1, fp32,
+ * multi_head_attention.py:235-271) after the xscale, in the forward and the training step, and the
+ * layers attend with MultiHeadAttention (multi_head_attention.py:94-129): the linear_pos /
+ * pos_bias_u / pos_bias_v entries become optional in set_weights and are packed as zeros whatever
+ * is passed (the rel-pos scores then reduce exactly to q.k / sqrt(d_k)).  Clears the weights: call
+ * set_weights after it.  Not stream-ordered (synchronises the device).  Default off (rel_pos).
+ * cfm_cache_stream_create refuses an abs_pos handle. */
+cfm_status cfm_encoder_set_abs_pos(cfm_encoder* h, int on);
+int cfm_encoder_abs_pos(const cfm_encoder* h);
 
 /* Micro-batch concurrency (default 1, env CFM_MICROBATCH): the batch is split into up to n parts
  * (each >= 4 utterances) that run on library-owned streams forked from / joined into `stream`.

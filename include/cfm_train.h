@@ -84,6 +84,9 @@ cfm_status cfm_op_swish_backward(const float* z, const float* du, float* dz, int
  * updates the batch_norm running_mean / running_var entries in place (momentum, unbiased variance,
  * like nn.BatchNorm1d) when opts->update_running_stats != 0.  grads[i] may be NULL (gradient not
  * wanted); non-NULL entries are overwritten (not accumulated); running-stat rows are ignored.
+ * An abs_pos handle (cfm_encoder_set_abs_pos) adds the absolute sinusoids before the embedding
+ * dropout; its linear_pos / pos_bias_u / pos_bias_v rows must point at zero-filled tensors (pass
+ * NULL grads for them): MultiHeadAttention has no such parameters.
  *
  * The tape (caller-owned, cfm_train_tape_size bytes) carries the activations from the forward to
  * the backward; it must be passed unmodified to cfm_train_backward with the same B, T and opts.

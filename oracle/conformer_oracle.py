@@ -128,6 +128,14 @@ def rel_positional_encoding(x: np.ndarray, pe: np.ndarray, center_pos: int,
     return x, pos_emb
 
 
+def abs_positional_encoding(x: np.ndarray, pe: np.ndarray, xscale: Optional[float]) -> Tuple[np.ndarray, np.ndarray]:
+    """PositionalEncoding.forward (multi_head_attention.py:257-271), eval mode: x * xscale + pe[:, :T]."""
+    if xscale:
+        x = x * x.dtype.type(xscale)
+    pos_emb = pe[:, :x.shape[1]]
+    return x + pos_emb, pos_emb
+
+
 def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float = 1e-5) -> np.ndarray:
     """torch.nn.LayerNorm over the last dim (biased variance, eps inside the sqrt)."""
     mu = x.mean(axis=-1, keepdims=True)
@@ -178,6 +186,25 @@ def rel_pos_mha(x: np.ndarray, mask: Optional[np.ndarray], pos_emb: np.ndarray, 
     bd = q_v @ pp.transpose(0, 1, 3, 2)
     bd = rel_shift(bd)[:, :, :, :ac.shape[-1]]
     scores = (ac + bd) / x.dtype.type(math.sqrt(dk))
+    return _attend(scores, mask, v, sd, p)
+
+
+def mha(x: np.ndarray, mask: Optional[np.ndarray], sd, p: str, n_heads: int) -> np.ndarray:
+    """MultiHeadAttention.forward (multi_head_attention.py:117-129), the abs_pos layers' attention:
+    scores = q.k^T / sqrt(d_k), then forward_attention (94-115)."""
+    B, T, D = x.shape
+    dk = D // n_heads
+    q = linear(x, sd[p + "linear_q.weight"], sd[p + "linear_q.bias"]).reshape(B, T, n_heads, dk).transpose(0, 2, 1, 3)
+    k = linear(x, sd[p + "linear_k.weight"], sd[p + "linear_k.bias"]).reshape(B, T, n_heads, dk).transpose(0, 2, 1, 3)
+    v = linear(x, sd[p + "linear_v.weight"], sd[p + "linear_v.bias"]).reshape(B, T, n_heads, dk).transpose(0, 2, 1, 3)
+    scores = (q @ k.transpose(0, 1, 3, 2)) / x.dtype.type(math.sqrt(dk))
+    return _attend(scores, mask, v, sd, p)
+
+
+def _attend(scores, mask, v, sd, p):
+    """forward_attention (multi_head_attention.py:94-115) + linear_out."""
+    B, _, T, _ = scores.shape
+    x = scores
     if mask is not None:
         m = mask[:, None]
         scores = np.where(m, x.dtype.type(-10000.0), scores)
@@ -187,7 +214,7 @@ def rel_pos_mha(x: np.ndarray, mask: Optional[np.ndarray], pos_emb: np.ndarray, 
     else:
         e = np.exp(scores - scores.max(-1, keepdims=True))
         attn = e / e.sum(-1, keepdims=True)
-    o = (attn @ v).transpose(0, 2, 1, 3).reshape(B, T, D)
+    o = (attn @ v).transpose(0, 2, 1, 3).reshape(B, T, -1)
     return linear(o, sd[p + "linear_out.weight"], sd[p + "linear_out.bias"])
 
 
@@ -223,15 +250,19 @@ def conv_module(x: np.ndarray, pad_mask: Optional[np.ndarray], sd, p: str,
 
 
 def conformer_layer(x, att_mask, pos_emb, pad_mask, sd, p: str, n_heads: int,
-                    norm_type: str = "batch_norm") -> np.ndarray:
-    """ConformerLayer.forward (conformer_modules.py:88-121), eval mode (dropout = identity)."""
+                    norm_type: str = "batch_norm", self_attention_model: str = "rel_pos") -> np.ndarray:
+    """ConformerLayer.forward (conformer_modules.py:88-121), eval mode (dropout = identity);
+    self_attention_model 'abs_pos' attends with MultiHeadAttention (conformer_modules.py:106-107)."""
     half = x.dtype.type(0.5)
     residual = x
     h = feed_forward(layer_norm(x, sd[p + "norm_feed_forward1.weight"], sd[p + "norm_feed_forward1.bias"]),
                      sd, p + "feed_forward1.")
     residual = residual + h * half
     h = layer_norm(residual, sd[p + "norm_self_att.weight"], sd[p + "norm_self_att.bias"])
-    h = rel_pos_mha(h, att_mask, pos_emb, sd, p + "self_attn.", n_heads)
+    if self_attention_model == "abs_pos":
+        h = mha(h, att_mask, sd, p + "self_attn.", n_heads)
+    else:
+        h = rel_pos_mha(h, att_mask, pos_emb, sd, p + "self_attn.", n_heads)
     residual = residual + h
     h = layer_norm(residual, sd[p + "norm_conv.weight"], sd[p + "norm_conv.bias"])
     h = conv_module(h, pad_mask, sd, p + "conv.", norm_type)
@@ -274,16 +305,20 @@ def encoder_forward(x_bft: np.ndarray, lengths: Optional[np.ndarray], sd: Dict[s
         lengths = np.full((B,), T, dtype=np.int32)
     x = x.transpose(0, 2, 1)
     x, lengths = conv_subsampling(x, lengths, sd)
-    pe, center = rel_pe_table(max_len, d, dtype)
     xscale = math.sqrt(d) if cfg.get("xscaling", True) else None
-    x, pos_emb = rel_positional_encoding(x, pe, center, xscale)
+    sam = cfg.get("self_attention_model", "rel_pos")
+    if sam == "abs_pos":
+        x, pos_emb = abs_positional_encoding(x, create_pe(np.arange(max_len), d, dtype), xscale)
+    else:
+        pe, center = rel_pe_table(max_len, d, dtype)
+        x, pos_emb = rel_positional_encoding(x, pe, center, xscale)
     Tp = x.shape[1]
     pad_mask, att_mask = make_masks(Tp, lengths, cfg.get("att_context_size") or (-1, -1))
     if not cfg.get("use_pad_mask", True):   # enable_pad_mask(False): pad_mask = None (conformer_encoder.py:269-272)
         pad_mask = None
     for i in range(cfg["n_layers"]):
         x = conformer_layer(x, att_mask, pos_emb, pad_mask, sd, f"layers.{i}.", cfg["n_heads"],
-                            cfg.get("conv_norm_type", "batch_norm"))
+                            cfg.get("conv_norm_type", "batch_norm"), sam)
     if "out_proj.weight" in sd:
         x = linear(x, sd["out_proj.weight"], sd["out_proj.bias"])
     return x.transpose(0, 2, 1), lengths

@@ -50,6 +50,16 @@ def rel_pe(T: int, d: int, max_len: int = 5000) -> Tensor:
     return pe.unsqueeze(0)
 
 
+def abs_pe(T: int, d: int) -> Tensor:
+    """PositionalEncoding create_pe + forward window (multi_head_attention.py:235-271): positions 0 ... T-1."""
+    positions = torch.arange(0, T, dtype=torch.float32).unsqueeze(1)
+    div_term = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pe = torch.zeros(T, d)
+    pe[:, 0::2] = torch.sin(positions * div_term)
+    pe[:, 1::2] = torch.cos(positions * div_term)
+    return pe.unsqueeze(0)
+
+
 def rel_shift(x: Tensor) -> Tensor:
     """multi_head_attention.py:159-170."""
     b, h, qlen, pos_len = x.size()
@@ -77,12 +87,15 @@ def mhsa(x: Tensor, att_mask: Tensor, pos_emb: Tensor, sd: Dict[str, Tensor], p:
     q = F.linear(x, sd[p + "linear_q.weight"], sd[p + "linear_q.bias"]).view(B, -1, H, dk)
     k = F.linear(x, sd[p + "linear_k.weight"], sd[p + "linear_k.bias"]).view(B, -1, H, dk).transpose(1, 2)
     v = F.linear(x, sd[p + "linear_v.weight"], sd[p + "linear_v.bias"]).view(B, -1, H, dk).transpose(1, 2)
-    pp = F.linear(pos_emb, sd[p + "linear_pos.weight"]).view(pos_emb.size(0), -1, H, dk).transpose(1, 2)
-    q_u = (q + sd[p + "pos_bias_u"]).transpose(1, 2)
-    q_v = (q + sd[p + "pos_bias_v"]).transpose(1, 2)
-    ac = torch.matmul(q_u, k.transpose(-2, -1))
-    bd = rel_shift(torch.matmul(q_v, pp.transpose(-2, -1)))[:, :, :, :ac.size(-1)]
-    scores = (ac + bd) / math.sqrt(dk)
+    if pos_emb is None:   # MultiHeadAttention.forward (multi_head_attention.py:117-129), abs_pos layers
+        scores = torch.matmul(q.transpose(1, 2), k.transpose(-2, -1)) / math.sqrt(dk)
+    else:
+        pp = F.linear(pos_emb, sd[p + "linear_pos.weight"]).view(pos_emb.size(0), -1, H, dk).transpose(1, 2)
+        q_u = (q + sd[p + "pos_bias_u"]).transpose(1, 2)
+        q_v = (q + sd[p + "pos_bias_v"]).transpose(1, 2)
+        ac = torch.matmul(q_u, k.transpose(-2, -1))
+        bd = rel_shift(torch.matmul(q_v, pp.transpose(-2, -1)))[:, :, :, :ac.size(-1)]
+        scores = (ac + bd) / math.sqrt(dk)
     m = att_mask.unsqueeze(1)
     attn = torch.softmax(scores.masked_fill(m, -10000.0), dim=-1).masked_fill(m, 0.0)
     o = torch.matmul(attn, v).transpose(1, 2).reshape(B, -1, D)
@@ -143,7 +156,11 @@ def encoder_forward(x_bft: Tensor, lengths: Optional[Tensor], sd: Dict[str, Tens
     lengths = calc_length(lengths)
     if cfg.get("xscaling", True):
         x = x * math.sqrt(d)
-    pos_emb = rel_pe(x.size(1), d)
+    if cfg.get("self_attention_model", "rel_pos") == "abs_pos":   # PositionalEncoding.forward, :257-271
+        x = x + abs_pe(x.size(1), d)
+        pos_emb = None
+    else:
+        pos_emb = rel_pe(x.size(1), d)
     pad_mask, att_mask = masks(x.size(1), lengths, cfg.get("att_context_size") or (-1, -1))
     if not cfg.get("use_pad_mask", True):
         pad_mask = None

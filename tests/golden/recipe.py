@@ -59,8 +59,9 @@ def encoder_param_shapes(cfg: dict) -> List[Tuple[str, tuple]]:
         out += ln("norm_self_att")
         for n in ("linear_q", "linear_k", "linear_v", "linear_out"):
             out += [(p + f"self_attn.{n}.weight", (d, d)), (p + f"self_attn.{n}.bias", (d,))]
-        out += [(p + "self_attn.linear_pos.weight", (d, d)),
-                (p + "self_attn.pos_bias_u", (H, d // H)), (p + "self_attn.pos_bias_v", (H, d // H))]
+        if cfg.get("self_attention_model", "rel_pos") == "rel_pos":   # abs_pos: MultiHeadAttention, no pos terms
+            out += [(p + "self_attn.linear_pos.weight", (d, d)),
+                    (p + "self_attn.pos_bias_u", (H, d // H)), (p + "self_attn.pos_bias_v", (H, d // H))]
         out += ln("norm_feed_forward2") + ff("feed_forward2") + ln("norm_out")
     fo = cfg.get("feat_out", -1)
     if fo and fo > 0 and fo != d:

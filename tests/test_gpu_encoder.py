@@ -33,6 +33,9 @@ def native(cfg, compute):
                         compute=compute)
     if not cfg.get("use_pad_mask", True):   # enable_pad_mask(False) golden (enc_tiny_nopadmask)
         enc.set_pad_mask(False)
+    if cfg.get("self_attention_model", "rel_pos") == "abs_pos":   # enc_tiny_abspos
+        enc.set_abs_pos(True)
+        assert enc.abs_pos
     return enc
 
 
@@ -179,6 +182,43 @@ def test_dropin_enable_pad_mask():
         y2, _ = enc(audio_signal=x, length=ln)
     yr, _ = O.encoder_forward(z["x"], z["lengths"], sd, dict(cfg, use_pad_mask=True))
     check(y2.cpu().numpy(), yr, "fp32")
+
+
+def test_dropin_abs_pos():
+    """self_attention_model='abs_pos' through the drop-in module: the reference's state_dict (no
+    linear_pos / pos_bias), PositionalEncoding + MultiHeadAttention outputs (enc_tiny_abspos), and a
+    standalone abs_pos ConformerLayer against the oracle's MultiHeadAttention layer."""
+    from nemo.collections.asr.modules import ConformerEncoder
+    z = np.load(os.path.join(GOLDEN, "enc_tiny_abspos.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    enc = ConformerEncoder(feat_in=80, n_layers=cfg["n_layers"], d_model=cfg["d_model"], n_heads=cfg["n_heads"],
+                           self_attention_model="abs_pos")
+    sd = make_state_dict(cfg, int(z["seed"]))
+    ref_sd = enc.state_dict()
+    assert set(ref_sd) == set(sd)
+    enc.load_state_dict({k: torch.from_numpy(np.asarray(v)).reshape(ref_sd[k].shape) for k, v in sd.items()})
+    enc = enc.cuda().eval()
+    for compute in ("fp32", "bf16"):
+        enc.set_compute_mode(compute)
+        x, ln = torch.from_numpy(z["x"]).cuda(), torch.from_numpy(z["lengths"]).cuda()
+        with torch.no_grad():
+            y, yl = enc(audio_signal=x, length=ln)
+        np.testing.assert_array_equal(yl.cpu().numpy(), z["y_len"])
+        check(y.cpu().numpy(), z["y"], compute)
+    with pytest.raises(NotImplementedError):
+        enc.cache_aware_streamer(1, 4, 8)
+    # one layer on its own (conformer_modules.py:106-107): no pos_emb
+    layer = enc.layers[0]
+    layer.set_compute_mode("fp32")
+    rng = np.random.default_rng(3)
+    xl = rng.standard_normal((2, 12, cfg["d_model"])).astype(np.float32)
+    lens = np.array([12, 7])
+    pad, att = O.make_masks(12, lens)
+    with torch.no_grad():
+        yl_ = layer(torch.from_numpy(xl).cuda(), att_mask=torch.from_numpy(att).cuda(),
+                    pad_mask=torch.from_numpy(pad).cuda())
+    ref = O.conformer_layer(xl, att, None, pad, sd, "layers.0.", cfg["n_heads"], "batch_norm", "abs_pos")
+    check(yl_.cpu().numpy(), ref, "fp32")
 
 
 @pytest.mark.parametrize("path", [f for f in ENC_FILES if "large17" in f or "tiny_ctx" in f or "noxscale_ln" in f],

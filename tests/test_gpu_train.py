@@ -18,7 +18,7 @@ import torch
 from conftest import GOLDEN, rel_l2
 
 pytestmark = pytest.mark.gpu
-CASES = ["train_tiny", "train_tiny_dk10", "train_tiny_ctx", "train_tiny_nopad"]
+CASES = ["train_tiny", "train_tiny_dk10", "train_tiny_ctx", "train_tiny_nopad", "train_tiny_abspos"]
 GATE_Y = {"fp32": 1e-3, "bf16": 2e-2}
 GATE_G = {"fp32": 1e-3, "bf16": 6e-2}
 

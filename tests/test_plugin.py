@@ -61,7 +61,26 @@ def test_neural_types_and_input_example():
     assert x.shape[1] == 80 and ln.shape[0] == x.shape[0]
 
 
-@pytest.mark.parametrize("bad", [{"subsampling": "vggnet"}, {"self_attention_model": "abs_pos"},
+def test_abs_pos_module_tree():
+    """self_attention_model='abs_pos' (conformer_encoder.py:184-189): PositionalEncoding, MultiHeadAttention
+    layers and the reference's state_dict keys (no linear_pos / pos_bias), also with untie_biases=False."""
+    from nemo.collections.asr.modules import ConformerEncoder
+    from nemo.collections.asr.parts.submodules.multi_head_attention import (MultiHeadAttention,
+                                                                            RelPositionMultiHeadAttention)
+    from recipe import encoder_param_shapes
+    cfg = dict(feat_in=80, n_layers=2, d_model=64, n_heads=4, self_attention_model="abs_pos")
+    for untie in (True, False):
+        enc = ConformerEncoder(**cfg, untie_biases=untie)
+        assert type(enc.layers[0].self_attn) is MultiHeadAttention
+        assert not isinstance(enc.layers[0].self_attn, RelPositionMultiHeadAttention)
+        shapes = dict(encoder_param_shapes(cfg))
+        sd = enc.state_dict()
+        assert set(sd) == set(shapes)
+        assert all(tuple(sd[k].shape) == tuple(v) for k, v in shapes.items())
+        assert enc._dropout_emb == 0.0
+
+
+@pytest.mark.parametrize("bad", [{"subsampling": "vggnet"}, {"self_attention_model": "bogus_pos"},
                                  {"subsampling_factor": 8}])
 def test_unsupported_configs_raise(bad):
     from nemo.collections.asr.modules import ConformerEncoder
