@@ -3,7 +3,7 @@
 B=32 x T=1000 x 80-mel per GPU, eval mode, through the drop-in
 `nemo.collections.asr.modules.ConformerEncoder` (one C-ABI call per forward).
 
-    python bench.py [--gpus N --steps K --warmup W] [--compute bf16|fp32]
+    python bench.py [--gpus N --steps K --warmup W] [--compute bf16|fp16|fp32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 `--gpus N` is authoritative: started without a torch.distributed environment (no WORLD_SIZE) and
@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
 import torch  # noqa: E402
 
 METRIC = "encoder audio-frames/sec, Conformer-Large B=32 T=1000 @1/2/4/8 MI355X"
-PEAK = {"bf16": 2500.0, "fp32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+PEAK = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}          # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -126,12 +126,14 @@ def cpu_baseline(enc, B, T, budget_s):
 
 def parity_and_fp32(dev, B, T, steps=5):
     """What the bf16 headline hides (rank 0, after the timed loop):
-    * the error of both compute modes at the timed shape against the REFERENCE encoder: the two
+    * the error of every compute mode at the timed shape against the REFERENCE encoder: the two
       reference utterances of tests/golden/enc_large17.npz (Large-17, outputs of the reference
       ConformerEncoder, fp32 CPU) embedded at positions 5 and 30 of a B x T batch, weights from the
-      golden's seed recipe (tests/golden/recipe.py) -> relL2 per compute mode (north-star gate: fp32
+      golden's seed recipe (tests/golden/recipe.py) -> relL2 per compute mode (north-star gate:
       relL2 <= 1e-3);
-    * the fp32 parity mode's own throughput at the same shape (v_mfma_f32_32x32x2_f32 contractions)."""
+    * the throughput of the two modes that meet that gate, at the same shape: fp32
+      (v_mfma_f32_32x32x2_f32 contractions) and fp16 (libcfm_f16.so: the bf16 kernels with fp16
+      operands, same MFMA rate)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from recipe import make_state_dict  # fixture recipe (checker only)
@@ -153,28 +155,33 @@ def parity_and_fp32(dev, B, T, steps=5):
     out = {"reference": "tests/golden/enc_large17.npz: reference ConformerEncoder outputs (fp32, CPU) for 2 "
                         f"utterances embedded in the B={B} x T={T} batch", "gate_fp32_relL2": 1e-3}
     yref = torch.from_numpy(z["y"]).to(dev, torch.float64)
-    for compute in ("bf16", "fp32"):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from conformer_oracle import encoder_flops
+    lines = {}
+    for compute in ("bf16", "fp16", "fp32"):
         enc.set_compute_mode(compute)
         with torch.inference_mode():
             y, yl = enc(audio_signal=x, length=ln)
             y = y[slots].to(torch.float64)
             out[f"{compute}_relL2"] = float((y - yref).norm() / yref.norm())
             out[f"{compute}_max_abs_err_over_max_ref"] = float((y - yref).abs().max() / yref.abs().max())
-            if compute == "fp32":
+            if compute != "bf16":
+                n = steps if compute == "fp32" else 4 * steps
                 for _ in range(2):
                     enc(audio_signal=x, length=ln)
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-                for _ in range(steps):
+                for _ in range(n):
                     enc(audio_signal=x, length=ln)
                 torch.cuda.synchronize(dev)
-                ms = 1000.0 * (time.perf_counter() - t0) / steps
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from conformer_oracle import encoder_flops
-    tf = encoder_flops(B, T, 512, 17) / (ms * 1e-3) / 1e12
-    fp32 = {"ms_per_step": round(ms, 3), "value": round(B * T / (ms * 1e-3), 1), "unit": "audio-frames/s",
-            "TFLOP/s": round(tf, 1), "frac_of_fp32_mfma_peak": round(tf / PEAK["fp32"], 4), "steps": steps}
-    return out, fp32
+                ms = 1000.0 * (time.perf_counter() - t0) / n
+                tf = encoder_flops(B, T, 512, 17) / (ms * 1e-3) / 1e12
+                lines[compute] = {"ms_per_step": round(ms, 3), "value": round(B * T / (ms * 1e-3), 1),
+                                  "unit": "audio-frames/s", "TFLOP/s": round(tf, 1),
+                                  f"frac_of_{compute}_mfma_peak": round(tf / PEAK[compute], 4), "steps": n,
+                                  "relL2": round(out[f"{compute}_relL2"], 7)}
+    enc.set_compute_mode("bf16")
+    return out, lines["fp32"], lines["fp16"]
 
 
 def max_over_ranks(elapsed, dev, dist):
@@ -247,7 +254,7 @@ def main():
                     help="launcher/rendezvous check on CPU (gloo): no GPU, prints the ranks that joined")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--compute", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--compute", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1000)
     ap.add_argument("--layers", type=int, default=17)
@@ -341,7 +348,7 @@ def main():
 
     if rank == 0:
         import conformer_amd
-        es = 2 if args.compute == "bf16" else 4
+        es = 4 if args.compute == "fp32" else 2
         total_flop = None
         roof = None
         breakdown = {}
@@ -387,9 +394,9 @@ def main():
         total_flop = encoder_flops(B, T, d, L)
         # the CPU baseline is a rank-0, N=1 measurement (a multi-GPU job reports the GPU lines only)
         cpu = cpu_baseline(enc, B, T, args.cpu_budget) if (args.cpu_budget > 0 and world == 1) else None
-        parity, fp32_line = (None, None)
+        parity, fp32_line, fp16_line = (None, None, None)
         if not args.no_parity and L == 17 and d == 512:
-            parity, fp32_line = parity_and_fp32(dev, B, T)
+            parity, fp32_line, fp16_line = parity_and_fp32(dev, B, T)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "audio-frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -406,6 +413,7 @@ def main():
             "train": train,
             "parity": parity,
             "fp32_parity_mode": fp32_line,
+            "fp16_mode": fp16_line,
             "breakdown": breakdown,
         }
         print(json.dumps(out), flush=True)
@@ -433,7 +441,7 @@ def train_leg(args, world, rank, dev, dist, barrier, steps, warmup):
                            dropout_att=0.1).to(dev).train()
     dec = ConvASRDecoder(feat_in=d, num_classes=V).to(dev).train()
     for m in (enc, dec):
-        m.set_compute_mode(args.compute)
+        m.set_compute_mode("bf16" if args.compute == "fp16" else args.compute)   # fp16 is inference-only
     if dist:
         cdist.convert_sync_batchnorm(enc)
     loss_fn = CTCLoss(num_classes=V, zero_infinity=True, reduction="mean_batch")

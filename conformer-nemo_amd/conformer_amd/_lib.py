@@ -10,19 +10,23 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Optional
+from typing import Dict, Optional
 
 # CFM_LIB_PATH: load another build of the library (same-process A/B timing in tools/)
 LIB_PATH = os.environ.get("CFM_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcfm.so")
+# the fp16 build (same sources, IEEE fp16 as the 16-bit compute type): compute='fp16'
+LIB16_PATH = os.environ.get("CFM_LIB16_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                              "libcfm_f16.so")
 
 CFM_COMPUTE_FP32 = 0
 CFM_COMPUTE_BF16 = 1
+CFM_COMPUTE_FP16 = 2
 
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "UNSUPPORTED", 3: "HIP", 4: "WORKSPACE", 5: "WEIGHTS", 6: "NOMEM"}
 
 # every symbol include/cfm_encoder.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
-    "cfm_last_error", "cfm_version", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
+    "cfm_last_error", "cfm_version", "cfm_half_mode", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
     "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_abs_pos", "cfm_encoder_abs_pos", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
     "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
@@ -97,26 +101,34 @@ class CfmError(RuntimeError):
     pass
 
 
-_lib: Optional[ctypes.CDLL] = None
+_libs: Dict[str, ctypes.CDLL] = {}
 
 
 ABI_VERSION = 3   # include/cfm_encoder.h CFM_ABI_VERSION: the struct layouts these bindings declare
 
 
-def load() -> ctypes.CDLL:
-    """Load libcfm.so once.  torch must be imported first so the process shares torch's HIP runtime."""
-    global _lib
-    if _lib is not None:
-        return _lib
+def variant_of(compute: str) -> str:
+    """The library build a compute mode runs in: 'fp16' -> libcfm_f16.so, else libcfm.so."""
+    return "fp16" if compute == "fp16" else "bf16"
+
+
+def load(variant: str = "bf16") -> ctypes.CDLL:
+    """Load libcfm.so (variant 'bf16', the default) or libcfm_f16.so ('fp16') once.  torch must be
+    imported first so the process shares torch's HIP runtime."""
+    lib = _libs.get(variant)
+    if lib is not None:
+        return lib
     import torch  # noqa: F401  (HIP runtime first: libcfm resolves libamdhip64.so.7 to torch's copy)
-    if not os.path.exists(LIB_PATH):
-        raise CfmError(f"native library not built: {LIB_PATH} (run `make -C conformer-nemo_amd/csrc` "
+    path = LIB16_PATH if variant == "fp16" else LIB_PATH
+    if not os.path.exists(path):
+        raise CfmError(f"native library not built: {path} (run `make -C conformer-nemo_amd/csrc` "
                        f"or __graft_entry__.build())")
-    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
     vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     sig = {
         "cfm_last_error": (ctypes.c_char_p, []),
         "cfm_version": (ci, []),
+        "cfm_half_mode": (ci, []),
         "cfm_encoded_length": (ci, [ci]),
         "cfm_encoder_create": (ci, [ctypes.POINTER(CfmEncoderCfg), ci, ci, ctypes.POINTER(vp)]),
         "cfm_encoder_destroy": (None, [vp]),
@@ -197,13 +209,18 @@ def load() -> ctypes.CDLL:
         fn.restype = res
         fn.argtypes = args
     if lib.cfm_version() != ABI_VERSION:
-        raise CfmError(f"{LIB_PATH}: ABI version {lib.cfm_version()}, these bindings expect {ABI_VERSION} "
+        raise CfmError(f"{path}: ABI version {lib.cfm_version()}, these bindings expect {ABI_VERSION} "
                        f"(include/cfm_encoder.h CFM_ABI_VERSION): rebuild the library")
-    _lib = lib
+    want = CFM_COMPUTE_FP16 if variant == "fp16" else CFM_COMPUTE_BF16
+    if lib.cfm_half_mode() != want:
+        raise CfmError(f"{path}: 16-bit compute mode {lib.cfm_half_mode()}, expected {want}")
+    _libs[variant] = lib
     return lib
 
 
-def check(status: int, what: str = "") -> None:
+def check(status: int, what: str = "", lib: Optional[ctypes.CDLL] = None) -> None:
+    """Raise CfmError for a non-OK status; the message is the failing library's cfm_last_error (`lib`,
+    default libcfm.so: each build keeps its own)."""
     if status != 0:
-        msg = load().cfm_last_error().decode(errors="replace")
+        msg = (lib or load()).cfm_last_error().decode(errors="replace")
         raise CfmError(f"{what}: {STATUS_NAMES.get(status, status)}: {msg}")

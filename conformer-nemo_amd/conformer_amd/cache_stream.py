@@ -44,7 +44,7 @@ class NativeCacheStream:
     of attention history.  `encoder` is a conformer_amd.NativeEncoder whose weights are set."""
 
     def __init__(self, encoder, batch: int, chunk: int, left_context: int):
-        self.lib = _lib.load()
+        self.lib = encoder.lib            # the encoder handle's own build (bf16 or fp16)
         _bind(self.lib)
         self.encoder = encoder            # keeps the weights alive
         self.device = encoder.device
@@ -54,7 +54,7 @@ class NativeCacheStream:
         self.d_out = int(encoder.cfg.feat_out) if int(encoder.cfg.feat_out) > 0 else d
         h = ctypes.c_void_p()
         _lib.check(self.lib.cfm_cache_stream_create(encoder.handle, self.B, self.c, self.left, ctypes.byref(h)),
-                   "cfm_cache_stream_create")
+                   "cfm_cache_stream_create", lib=self.lib)
         self.handle = h
         ws = int(self.lib.cfm_cache_stream_workspace_size(h))
         self._ws = torch.empty(ws, dtype=torch.uint8, device=f"cuda:{self.device}")
@@ -74,7 +74,7 @@ class NativeCacheStream:
 
     def reset(self) -> None:
         """Zero the caches, restart at frame 0, rebuild the position projections from the weights."""
-        _lib.check(self.lib.cfm_cache_stream_reset(self.handle, self._stream()), "cfm_cache_stream_reset")
+        _lib.check(self.lib.cfm_cache_stream_reset(self.handle, self._stream()), "cfm_cache_stream_reset", lib=self.lib)
 
     @property
     def position(self) -> int:
@@ -90,5 +90,5 @@ class NativeCacheStream:
         elif out.shape != (self.B, self.d_out, self.c) or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError(f"out must be a contiguous fp32 ({self.B}, {self.d_out}, {self.c}) tensor")
         _lib.check(self.lib.cfm_cache_stream_step(self.handle, x.data_ptr(), out.data_ptr(), self._ws.data_ptr(),
-                                                  self._ws.numel(), self._stream()), "cfm_cache_stream_step")
+                                                  self._ws.numel(), self._stream()), "cfm_cache_stream_step", lib=self.lib)
         return out

@@ -13,7 +13,7 @@ import torch
 
 from . import _lib
 
-COMPUTE_MODES = {"fp32": _lib.CFM_COMPUTE_FP32, "bf16": _lib.CFM_COMPUTE_BF16}
+COMPUTE_MODES = {"fp32": _lib.CFM_COMPUTE_FP32, "bf16": _lib.CFM_COMPUTE_BF16, "fp16": _lib.CFM_COMPUTE_FP16}
 
 
 def encoded_length(T: int) -> int:
@@ -46,7 +46,9 @@ class NativeEncoder:
     """One encoder instance on one GPU."""
 
     def __init__(self, cfg: _lib.CfmEncoderCfg, device: Optional[int] = None, compute: str = "bf16"):
-        self.lib = _lib.load()
+        if compute not in COMPUTE_MODES:
+            raise ValueError(f"compute must be one of {list(COMPUTE_MODES)}")
+        self.lib = _lib.load(_lib.variant_of(compute))   # fp16: the libcfm_f16.so build
         if not torch.cuda.is_available():
             raise _lib.CfmError("the native Conformer encoder needs a ROCm GPU (torch.cuda.is_available() is False)")
         if compute not in COMPUTE_MODES:
@@ -56,7 +58,7 @@ class NativeEncoder:
         self.cfg = cfg
         h = ctypes.c_void_p()
         _lib.check(self.lib.cfm_encoder_create(ctypes.byref(cfg), self.device, COMPUTE_MODES[compute], ctypes.byref(h)),
-                   "cfm_encoder_create")
+                   "cfm_encoder_create", lib=self.lib)
         self.handle = h
         self._ws: Optional[torch.Tensor] = None
 
@@ -94,7 +96,7 @@ class NativeEncoder:
         arr = (_lib.CfmTensorView * len(views))(*views)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(self.lib.cfm_encoder_set_weights(self.handle, arr, len(views), ctypes.c_void_p(stream)),
-                   "cfm_encoder_set_weights")
+                   "cfm_encoder_set_weights", lib=self.lib)
         del keep
 
     # ---- forward ------------------------------------------------------------------------------
@@ -103,16 +105,16 @@ class NativeEncoder:
         return int(self.lib.cfm_encoder_max_audio_length(self.handle))
 
     def set_max_audio_length(self, n: int) -> None:
-        _lib.check(self.lib.cfm_encoder_set_max_audio_length(self.handle, int(n)), "set_max_audio_length")
+        _lib.check(self.lib.cfm_encoder_set_max_audio_length(self.handle, int(n)), "set_max_audio_length", lib=self.lib)
 
     def set_pad_mask(self, on: bool) -> None:
         """enable_pad_mask (conformer_encoder.py:301-305): off -> conv module runs with pad_mask=None."""
-        _lib.check(self.lib.cfm_encoder_set_pad_mask(self.handle, 1 if on else 0), "set_pad_mask")
+        _lib.check(self.lib.cfm_encoder_set_pad_mask(self.handle, 1 if on else 0), "set_pad_mask", lib=self.lib)
 
     def set_abs_pos(self, on: bool) -> None:
         """self_attention_model='abs_pos': absolute sinusoids added after the xscale and plain
         MultiHeadAttention in the layers (cfm_encoder_set_abs_pos).  Clears the weights."""
-        _lib.check(self.lib.cfm_encoder_set_abs_pos(self.handle, 1 if on else 0), "set_abs_pos")
+        _lib.check(self.lib.cfm_encoder_set_abs_pos(self.handle, 1 if on else 0), "set_abs_pos", lib=self.lib)
 
     @property
     def abs_pos(self) -> bool:
@@ -120,7 +122,7 @@ class NativeEncoder:
 
     def set_microbatches(self, n: int) -> None:
         """Split each forward's batch over up to n concurrent streams (bitwise-identical results)."""
-        _lib.check(self.lib.cfm_encoder_set_microbatches(self.handle, int(n)), "set_microbatches")
+        _lib.check(self.lib.cfm_encoder_set_microbatches(self.handle, int(n)), "set_microbatches", lib=self.lib)
 
     def workspace_size(self, B: int, T: int) -> int:
         return int(self.lib.cfm_encoder_workspace_size(self.handle, int(B), int(T)))
@@ -160,7 +162,7 @@ class NativeEncoder:
         stream = torch.cuda.current_stream(dev).cuda_stream
         _lib.check(self.lib.cfm_encoder_forward(self.handle, x_bft.data_ptr(), len_ptr, B, T, out.data_ptr(),
                                                 out_len.data_ptr(), ws.data_ptr(), nbytes, ctypes.c_void_p(stream)),
-                   "cfm_encoder_forward")
+                   "cfm_encoder_forward", lib=self.lib)
         return out, out_len
 
     def layers_forward(self, x_btd: torch.Tensor, lengths: Optional[torch.Tensor] = None,
@@ -192,7 +194,7 @@ class NativeEncoder:
         stream = torch.cuda.current_stream(dev).cuda_stream
         _lib.check(self.lib.cfm_encoder_layers_forward(self.handle, x.data_ptr(), len_ptr, B, Tp, pe_ptr, y.data_ptr(),
                                                        ws.data_ptr(), nbytes, ctypes.c_void_p(stream)),
-                   "cfm_encoder_layers_forward")
+                   "cfm_encoder_layers_forward", lib=self.lib)
         return y
 
     def forward_timed(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None):
@@ -216,5 +218,5 @@ class NativeEncoder:
         stream = torch.cuda.current_stream(x_bft.device).cuda_stream
         _lib.check(self.lib.cfm_encoder_forward_timed(self.handle, x_bft.data_ptr(), len_ptr, B, T, out.data_ptr(),
                                                       out_len.data_ptr(), ws.data_ptr(), nbytes, ctypes.c_void_p(stream),
-                                                      ms, cnt), "cfm_encoder_forward_timed")
+                                                      ms, cnt), "cfm_encoder_forward_timed", lib=self.lib)
         return {self.lib.cfm_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(n)}

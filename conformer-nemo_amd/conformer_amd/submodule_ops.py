@@ -25,14 +25,14 @@ import torch
 
 from . import _lib
 
-COMPUTE_DTYPE = {"bf16": torch.bfloat16, "fp32": torch.float32}
-COMPUTE_ID = {"fp32": 0, "bf16": 1}
+COMPUTE_DTYPE = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
+COMPUTE_ID = {"fp32": 0, "bf16": 1, "fp16": 2}
 
 
 def compute_mode(module) -> str:
     c = getattr(module, "compute", None) or os.environ.get("CFM_COMPUTE", "bf16")
     if c not in COMPUTE_ID:
-        raise ValueError("compute must be 'bf16' or 'fp32'")
+        raise ValueError("compute must be 'bf16', 'fp16' or 'fp32'")
     return c
 
 
@@ -106,7 +106,7 @@ def masks_to_lengths(att_mask: Optional[torch.Tensor], pad_mask: Optional[torch.
 # ---- kernel-level ops ------------------------------------------------------------------------------
 def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], act: int, compute: str) -> torch.Tensor:
     """x2d (M, K) in the compute dtype -> (M, N) compute dtype; act 0 none, 1 relu, 2 swish (cfm_op_linear)."""
-    lib = _lib.load()
+    lib = _lib.load(_lib.variant_of(compute))
     dev = x2d.device
     M, K = x2d.shape
     w = weight.detach().reshape(weight.shape[0], -1).to(dev, torch.float32).contiguous()
@@ -120,16 +120,16 @@ def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
     need = ctypes.c_size_t(0)
     mode = COMPUTE_ID[compute]
     _lib.check(lib.cfm_op_linear(mode, x2d.data_ptr(), M, K, w.data_ptr(), None if b is None else b.data_ptr(), N, act,
-                                 y.data_ptr(), None, ctypes.byref(need), _stream(dev)), "cfm_op_linear")
+                                 y.data_ptr(), None, ctypes.byref(need), _stream(dev)), "cfm_op_linear", lib)
     ws = torch.empty(need.value, dtype=torch.uint8, device=dev)
     _lib.check(lib.cfm_op_linear(mode, x2d.data_ptr(), M, K, w.data_ptr(), None if b is None else b.data_ptr(), N, act,
-                                 y.data_ptr(), ws.data_ptr(), ctypes.byref(need), _stream(dev)), "cfm_op_linear")
+                                 y.data_ptr(), ws.data_ptr(), ctypes.byref(need), _stream(dev)), "cfm_op_linear", lib)
     return y
 
 
 def rel_attention(q, k, v, p, pos_u, pos_v, lengths, B, T, H, dk, ctx, compute) -> torch.Tensor:
     """Fused attention core (cfm_op_rel_attention) on projected q, k, v (B*T, H*dk) and p (2T-1, H*dk)."""
-    lib = _lib.load()
+    lib = _lib.load(_lib.variant_of(compute))
     dev = q.device
     mode = COMPUTE_ID[compute]
     out = torch.empty((B * T, H * dk), dtype=COMPUTE_DTYPE[compute], device=dev)
@@ -138,14 +138,14 @@ def rel_attention(q, k, v, p, pos_u, pos_v, lengths, B, T, H, dk, ctx, compute) 
     vb = pos_v.detach().to(dev, torch.float32).contiguous()
     _lib.check(lib.cfm_op_rel_attention(mode, q.data_ptr(), k.data_ptr(), v.data_ptr(), p.data_ptr(), u.data_ptr(),
                                         vb.data_ptr(), lengths.data_ptr(), B, T, H, dk, int(ctx[0]), int(ctx[1]),
-                                        out.data_ptr(), ws.data_ptr(), _stream(dev)), "cfm_op_rel_attention")
+                                        out.data_ptr(), ws.data_ptr(), _stream(dev)), "cfm_op_rel_attention", lib)
     return out
 
 
 def conv_glu_dwconv(pre, lengths, B, T, d, conv, compute) -> torch.Tensor:
     """GLU + pad mask + depthwise conv + Batch/LayerNorm + Swish (cfm_op_conv_glu_dwconv) on pointwise_conv1's
     output pre (B*T, 2d); `conv` is the ConformerConvolution holding the weights."""
-    lib = _lib.load()
+    lib = _lib.load(_lib.variant_of(compute))
     dev = pre.device
     mode = COMPUTE_ID[compute]
     K = conv.depthwise_conv.kernel_size[0]
@@ -162,7 +162,7 @@ def conv_glu_dwconv(pre, lengths, B, T, d, conv, compute) -> torch.Tensor:
                                           d, K, dw_w.data_ptr(), dw_b.data_ptr(), 0 if is_bn else 1, nw.data_ptr(),
                                           nb.data_ptr(), None if mean is None else mean.data_ptr(),
                                           None if var is None else var.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                                          nbytes, _stream(dev)), "cfm_op_conv_glu_dwconv")
+                                          nbytes, _stream(dev)), "cfm_op_conv_glu_dwconv", lib)
     return out
 
 

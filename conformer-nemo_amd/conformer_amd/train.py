@@ -166,7 +166,7 @@ class EncoderTrainer:
         _lib.check(self.lib.cfm_train_forward(self.native.handle, self._ptrs(params), len(params), x.data_ptr(),
                                               None if ln is None else ln.data_ptr(), B, T, ctypes.byref(o),
                                               y.data_ptr(), ylen.data_ptr(), tape.data_ptr(), tape.numel(),
-                                              ws.data_ptr(), ws.numel(), st), "cfm_train_forward")
+                                              ws.data_ptr(), ws.numel(), st), "cfm_train_forward", lib=self.lib)
         state = dict(tape=tape, B=B, T=T, dropout=dropout, seed=seed, bn_momentum=bn_momentum, x=x, ln=ln,
                      dropout_emb=dropout_emb, dropout_att=dropout_att, use_pad_mask=self.use_pad_mask)
         return y, ylen, state
@@ -204,7 +204,7 @@ class EncoderTrainer:
         _lib.check(self.lib.cfm_train_backward(self.native.handle, self._ptrs(params), len(params), dy.data_ptr(),
                                                state["B"], state["T"], ctypes.byref(o), self._ptrs(out),
                                                tape.data_ptr(), tape.numel(), ws.data_ptr(), ws.numel(), st),
-                   "cfm_train_backward")
+                   "cfm_train_backward", lib=self.lib)
         if gb is not None:
             gb.after_backward()
         return grads

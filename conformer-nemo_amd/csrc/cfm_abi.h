@@ -46,6 +46,22 @@ cfm_status guarded(F&& f) {
 
 inline long round_up(long v, long m) { return (v + m - 1) / m * m; }
 
+// host copies of the 16-bit compute type's conversions (cfm_common.h): bfloat16, or IEEE fp16 in
+// the CFM_HALF_F16 build (round to nearest even, saturated to +-65504)
+#ifdef CFM_HALF_F16
+inline uint16_t host_f2bf(float f) {
+  if (f == f) f = f > 65504.0f ? 65504.0f : (f < -65504.0f ? -65504.0f : f);
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+inline float host_bf2f(uint16_t v) {
+  _Float16 h;
+  std::memcpy(&h, &v, 2);
+  return (float)h;
+}
+#else
 inline uint16_t host_f2bf(float f) {
   uint32_t u;
   std::memcpy(&u, &f, 4);
@@ -59,5 +75,6 @@ inline float host_bf2f(uint16_t v) {
   std::memcpy(&f, &u, 4);
   return f;
 }
+#endif
 
 }  // namespace cfm

@@ -17,16 +17,40 @@
 
 #define CFM_DEV __device__ __forceinline__
 
+// The 16-bit compute type.  `bf16_t` is its 16-bit storage: bfloat16 in libcfm.so, IEEE fp16 in
+// libcfm_f16.so (the same sources built with CFM_HALF_F16: the fp16 compute mode, 3 more mantissa
+// bits at the same MFMA rate).  Only the conversions below, Vec16<bf16_t> and the two MFMA
+// wrappers see the format; every loader, LDS image, swizzle and packing trick is format-agnostic.
 typedef uint16_t bf16_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-
+#ifdef CFM_HALF_F16
+typedef __attribute__((ext_vector_type(8))) _Float16 h16x8;
+CFM_DEV float bf2f(bf16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+CFM_DEV bf16_t f2bf(float f) {
+  // saturate to the fp16 range (v_med3_f32) so that an outlier cannot become inf, then round to nearest even
+  return __builtin_bit_cast(bf16_t, (_Float16)__builtin_amdgcn_fmed3f(f, -65504.0f, 65504.0f));
+}
+CFM_DEV f32x16 mfma16_32x32x16(const uint4& a, const uint4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+}
+CFM_DEV f32x4 mfma16_16x16x32(const uint4& a, const uint4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+}
+#else
+typedef __attribute__((ext_vector_type(8))) __bf16 h16x8;
 CFM_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 CFM_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN-preserving)
   return __builtin_bit_cast(bf16_t, b);
 }
+CFM_DEV f32x16 mfma16_32x32x16(const uint4& a, const uint4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+}
+CFM_DEV f32x4 mfma16_16x16x32(const uint4& a, const uint4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+}
+#endif
 
 // Scalar load / store in the compute type, math in fp32.
 template <typename T> CFM_DEV float ld_f(const T* p);
@@ -39,8 +63,7 @@ template <> CFM_DEV void st_f<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
 // One 32-byte k-slab of a 32x32 output tile: acc += A_slab * B_slab.
 template <typename T> CFM_DEV void mfma_slab(f32x16& acc, const uint4& a, const uint4& b);
 template <> CFM_DEV void mfma_slab<bf16_t>(f32x16& acc, const uint4& a, const uint4& b) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                acc, 0, 0, 0);
+  acc = mfma16_32x32x16(a, b, acc);
 }
 template <> CFM_DEV void mfma_slab<float>(f32x16& acc, const uint4& a, const uint4& b) {
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
@@ -69,7 +92,7 @@ template <> struct Vec16<bf16_t> {
   static CFM_DEV void to_f32(const uint4& u, float* f) {
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { f[2 * i] = __uint_as_float(w[i] << 16); f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+    for (int i = 0; i < 4; ++i) { f[2 * i] = bf2f((bf16_t)(w[i] & 0xffffu)); f[2 * i + 1] = bf2f((bf16_t)(w[i] >> 16)); }
   }
   static CFM_DEV uint4 from_f32(const float* f) {
     uint32_t w[4];

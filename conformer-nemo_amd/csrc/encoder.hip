@@ -425,13 +425,22 @@ extern "C" {
 
 const char* cfm_last_error(void) { return g_last_error.c_str(); }
 int cfm_version(void) { return CFM_ABI_VERSION; }
+#ifdef CFM_HALF_F16
+int cfm_half_mode(void) { return CFM_COMPUTE_FP16; }
+#else
+int cfm_half_mode(void) { return CFM_COMPUTE_BF16; }
+#endif
 int cfm_encoded_length(int len) { return host_calc_length(len, 2); }
 
 cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int compute_mode, cfm_encoder** out) {
   return guarded([&] {
     if (!cfg || !out) fail(CFM_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
-    if (compute_mode != CFM_COMPUTE_FP32 && compute_mode != CFM_COMPUTE_BF16) fail(CFM_ERR_INVALID_ARG, "compute_mode");
+    if (compute_mode != CFM_COMPUTE_FP32 && compute_mode != CFM_COMPUTE_BF16 && compute_mode != CFM_COMPUTE_FP16)
+      fail(CFM_ERR_INVALID_ARG, "compute_mode");
+    if (compute_mode != CFM_COMPUTE_FP32 && compute_mode != cfm_half_mode())
+      fail(CFM_ERR_UNSUPPORTED, compute_mode == CFM_COMPUTE_FP16 ? "fp16 compute is libcfm_f16.so"
+                                                                 : "bf16 compute is libcfm.so");
     if (cfg->subsampling_factor != 4) fail(CFM_ERR_UNSUPPORTED, "only subsampling='striding', factor 4 is implemented");
     if (cfg->d_model <= 0 || cfg->n_heads <= 0 || cfg->d_model % cfg->n_heads) fail(CFM_ERR_INVALID_ARG, "d_model % n_heads");
     if (cfg->d_model % 8) fail(CFM_ERR_UNSUPPORTED, "d_model must be a multiple of 8");
@@ -1246,7 +1255,7 @@ __global__ void fill_rand_kernel(uint16_t* p, long n, uint32_t seed, int as_f32)
     x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
     const float f = ((x & 0xffffff) / 16777216.0f) * 2.0f - 1.0f;
     if (as_f32) ((float*)p)[i] = f;
-    else { uint32_t u = __float_as_uint(f); p[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16); }
+    else p[i] = f2bf(f);
   }
 }
 }  // namespace

@@ -888,8 +888,6 @@ constexpr int G8_BUF = 4 * G8_HALF;     // one K-tile: A0 | B0 | A1 | B1
 static_assert(2 * G8_BUF >= T8::BM / T8::EP * T8::EPS * 4, "epilogue image fits the ring");
 CFM_DEV int g8_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-
 template <int EPI, class ALoad>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
   __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF];
@@ -991,8 +989,7 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[(q & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), acc[(q & 1) * 4 + i][j], 0, 0, 0);
+          acc[(q & 1) * 4 + i][j] = mfma16_16x16x32(af[i], bfr[j], acc[(q & 1) * 4 + i][j]);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 && (q & 1)) wait_vmcnt<8>();
       raw_barrier();
@@ -1245,8 +1242,7 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[(q & 1) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), acc[(q & 1) * 4 + i][j], 0, 0, 0);
+          acc[(q & 1) * 4 + i][j] = mfma16_16x16x32(af[i], bfr[j], acc[(q & 1) * 4 + i][j]);
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 && (q & 1)) wait_vmcnt<4>();
       raw_barrier();

@@ -2263,6 +2263,11 @@ static void make_step(Step& S, cfm_encoder* h, const float* const* params, int n
                       const cfm_train_opts* opts, void* tape, size_t tape_bytes, void* ws, size_t ws_bytes,
                       void* stream) {
   check_common(h, params, n_params, B, T, opts);
+#ifdef CFM_HALF_F16
+  // fp16 gradients would need loss scaling (their range, not their precision, is the limit): the fp16
+  // build is an inference build; train in bf16 (libcfm.so) or fp32
+  if (h->dtype != DT_F32) fail(CFM_ERR_UNSUPPORTED, "training in fp16 is not supported: use the bf16 or fp32 mode");
+#endif
   S.h = h;
   S.g = make_geo(h, B, T);
   S.tp = tape_layout(h, S.g);

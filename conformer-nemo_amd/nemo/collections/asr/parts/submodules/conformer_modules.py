@@ -64,8 +64,8 @@ class ConformerLayer(nn.Module):
                                     abs_pos=abs_pos)
 
     def set_compute_mode(self, compute: str):
-        if compute not in ("bf16", "fp32"):
-            raise ValueError("compute must be 'bf16' or 'fp32'")
+        if compute not in ("bf16", "fp16", "fp32"):
+            raise ValueError("compute must be 'bf16', 'fp16' or 'fp32'")
         self.compute = compute
 
 

@@ -32,8 +32,8 @@ class MultiHeadAttention(nn.Module):
         return self._native_attention(query, key, value, mask, None)
 
     def set_compute_mode(self, compute: str):
-        if compute not in ("bf16", "fp32"):
-            raise ValueError("compute must be 'bf16' or 'fp32'")
+        if compute not in ("bf16", "fp16", "fp32"):
+            raise ValueError("compute must be 'bf16', 'fp16' or 'fp32'")
         self.compute = compute
 
     def _native_attention(self, query, key, value, mask, pos_emb):

@@ -38,12 +38,17 @@ typedef int cfm_status;
 #define CFM_ERR_WEIGHTS 5
 #define CFM_ERR_NOMEM 6
 
-/* Compute modes.  FP32: every contraction on v_mfma_f32_32x32x2_f32 (exact fp32 products) — the
- * parity mode for the north-star 1e-3 relative gate.  BF16: operands in bf16 on
- * v_mfma_f32_32x32x16_bf16 with fp32 accumulation, fp32 residual stream / norms / softmax — the
- * performance mode. */
+/* Compute modes.  FP32: every contraction on v_mfma_f32_32x32x2_f32 (exact fp32 products).
+ * BF16: operands in bf16 on v_mfma_f32_32x32x16_bf16 with fp32 accumulation, fp32 residual stream /
+ * norms / softmax — the performance mode (libcfm.so).  FP16: the same kernels with IEEE fp16
+ * operands on v_mfma_f32_32x32x16_f16 at the same rate (3 more mantissa bits: within the north-star
+ * 1e-3 relative gate where bf16 is not), from libcfm_f16.so — the same sources built with the other
+ * 16-bit format; inference only (its training entries refuse the 16-bit mode).  A library accepts
+ * FP32 and its own 16-bit mode (cfm_half_mode()); every other entry point's `dtype` /
+ * compute-mode argument that is not CFM_COMPUTE_FP32 means that 16-bit mode. */
 #define CFM_COMPUTE_FP32 0
 #define CFM_COMPUTE_BF16 1
+#define CFM_COMPUTE_FP16 2
 
 /* Constructor arguments of ConformerEncoder.__init__ (conformer_encoder.py:111-132).
  * Eval-mode forward only: dropout / dropout_emb / dropout_att are identities and are not passed. */
@@ -83,10 +88,13 @@ const char* cfm_last_error(void);
  *      became active (an older host's shorter struct would leave the callback pointer unset);
  *   3  the *_set_weights of cfm_ctc.h / cfm_joint.h / cfm_rnnt_decode.h are stream-ordered (they no
  *      longer synchronise the stream: a host must keep the sources valid until the stream passes the
- *      call); new entry points cfm_encoder_layers_forward, cfm_op_conv_glu_dwconv, cfm_encoder_set_abs_pos, the
- *      transducer training entries of cfm_joint.h / cfm_rnnt_decode.h. */
+ *      call); new entry points cfm_encoder_layers_forward, cfm_op_conv_glu_dwconv,
+ *      cfm_encoder_set_abs_pos, cfm_half_mode (and the fp16 build libcfm_f16.so), the transducer
+ *      training entries of cfm_joint.h / cfm_rnnt_decode.h. */
 #define CFM_ABI_VERSION 3
 int cfm_version(void);
+/* This library's 16-bit compute mode: CFM_COMPUTE_BF16 (libcfm.so) or CFM_COMPUTE_FP16 (libcfm_f16.so). */
+int cfm_half_mode(void);
 
 /* calc_length (subsampling.py:272-282) on the host: encoder frames for `len` input frames. */
 int cfm_encoded_length(int len);

@@ -55,6 +55,25 @@ def test_library_loads_and_exports_header_symbols():
         assert hasattr(lib, name) and re.search(rf"\bT {name}\b", out), name
 
 
+def test_fp16_build_exports_the_same_abi():
+    """libcfm_f16.so (the fp16 compute mode) is the same sources with the other 16-bit format: the same
+    exported symbols, and each build accepts only its own 16-bit mode (checked before any GPU call)."""
+    from conformer_amd import _lib, make_cfg
+    lib16 = _lib.load("fp16")
+    lib = _lib.load()
+    assert lib.cfm_half_mode() == _lib.CFM_COMPUTE_BF16 and lib16.cfm_half_mode() == _lib.CFM_COMPUTE_FP16
+    out = os.popen(f"nm -D --defined-only {_lib.LIB16_PATH}").read()
+    ref = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
+    syms = lambda t: sorted(set(re.findall(r"\bT (cfm_[a-z0-9_]+)\b", t)))   # noqa: E731
+    assert syms(out) == syms(ref) and len(syms(out)) > 100
+    h = ctypes.c_void_p()
+    cfg = make_cfg(80, 2, 64, n_heads=4)
+    assert lib.cfm_encoder_create(ctypes.byref(cfg), 0, _lib.CFM_COMPUTE_FP16, ctypes.byref(h)) == 2
+    assert b"libcfm_f16" in lib.cfm_last_error()
+    assert lib16.cfm_encoder_create(ctypes.byref(cfg), 0, _lib.CFM_COMPUTE_BF16, ctypes.byref(h)) == 2
+    assert b"libcfm.so" in lib16.cfm_last_error()
+
+
 def test_encoded_length_matches_oracle():
     from conformer_amd import _lib
     lib = _lib.load()

@@ -20,7 +20,8 @@ from recipe import make_inputs, make_state_dict
 pytestmark = pytest.mark.gpu
 
 ENC_FILES = sorted(glob.glob(os.path.join(GOLDEN, "enc_*.npz")))
-GATES = {"fp32": (1e-3, 1e-3), "bf16": (2e-2, None)}
+# fp16 (libcfm_f16.so): the north-star 1e-3 relative gate, which bf16 operands miss by ~4x at Large-17
+GATES = {"fp32": (1e-3, 1e-3), "bf16": (2e-2, None), "fp16": (1e-3, None)}
 
 _CFG_KEYS = ("feat_out", "subsampling_conv_channels", "ff_expansion_factor", "att_context_size", "xscaling",
              "conv_kernel_size", "conv_norm_type")
@@ -57,7 +58,7 @@ def check(y, ref, compute):
     return e
 
 
-@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("compute", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("path", ENC_FILES, ids=[os.path.basename(f)[4:-4] for f in ENC_FILES])
 def test_encoder_matches_reference(path, compute):
     z = np.load(path)
@@ -95,7 +96,7 @@ def test_edge_lengths(compute):
     check(y, yr, compute)
 
 
-@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("compute", ["fp32", "bf16", "fp16"])
 def test_batch_invariance_full_size(compute):
     """BASELINE cfg2 shape (Large-17, B=32, T=1000): each utterance's output is bitwise independent
     of its batch neighbours, and the two reference utterances of enc_large17 embedded in the batch
@@ -104,7 +105,7 @@ def test_batch_invariance_full_size(compute):
     cfg = json.loads(str(z["cfg_json"]))
     sd = make_state_dict(cfg, int(z["seed"]))
     x, lens = make_inputs(32, 1000, seed=11)
-    lens = np.full(32, 1000) if compute == "bf16" else lens
+    lens = np.full(32, 1000) if compute != "fp32" else lens
     x[5], lens[5] = z["x"][0], z["lengths"][0]
     x[30], lens[30] = z["x"][1], z["lengths"][1]
     enc = native(cfg, compute)
