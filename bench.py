@@ -56,6 +56,7 @@ def stage_work(B, T, d, L, H, C=None, F=80, K=31, dff=None, es=2):
         "ffn_down_gemm": ("flop", 2 * M * dff * d),
         "qkv_gemm": ("flop", 2 * M * d * 3 * d),
         "rel_attention": ("flop", 2 * B * Tp * d * (4 * Tp - 1)),
+        "qkv_attention": ("flop", 2 * M * d * 3 * d + 2 * B * Tp * d * (4 * Tp - 1)),   # fused: both above
         "out_proj_gemm": ("flop", 2 * M * d * d),
         "pw1_glu_gemm": ("flop", 2 * M * d * 2 * d),
         "dwconv_bn_swish": ("byte", 2 * M * d * es),

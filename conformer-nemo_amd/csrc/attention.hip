@@ -354,8 +354,138 @@ CFM_DEV_HOST_INLINE LdsGeom lds_geom(int Tp, int dkp, int vt_rows, int nw) {
   return g;
 }
 
+// One wave's 32-query tile [i0, i0 + 32) against the LDS-resident K (Ks) / Vt (Vs) of its (b, h):
+// qu / qv are the (q + u)*c / (q + v)*c B-operand slabs of the wave's queries (lane = query).
+// bd_s / row_s: the wave's private BD image and row table.  Writes the tile's output rows.
 // PF: prefetch the next key tile's P rows into registers (8*NS VGPRs; with NW = 8, two waves per
 // SIMD must fit 256 registers: on for dk <= 64).
+template <int NS, int ND, bool PF>
+CFM_DEV void attn_query_tile(const AttnParams& p, const LdsGeom& g, const char* Ks, const char* Vs, float* bd_s,
+                             float* row_s, const uint4 (&qu)[NS], const uint4 (&qv)[NS], int i0, int len, long rowbase,
+                             int h, int bh, int lane) {
+  using T = bf16_t;
+  constexpr int SE = 16;
+  const int hsel = lane >> 5, col = lane & 31;
+  const int Tp = p.Tp;
+  f32x16 o[ND];
+#pragma unroll
+  for (int n = 0; n < ND; ++n) o[n] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.0f;
+  const int iq = i0 + col;
+  int jbeg = 0, jend = len;
+  if (p.ctx_left >= 0) jbeg = max(0, (i0 - p.ctx_left) & ~31);
+  if (p.ctx_right >= 0) jend = min(jend, i0 + 31 + p.ctx_right + 1);
+
+  // BD window of key tile k = positions [j0 - i0 + T' - 32, j0 - i0 + T' + 32): its upper half is
+  // the lower half of tile k+1, so each tile computes one new 32-position block (P rows loaded
+  // one tile ahead) into the ring slot the block before last used.
+  auto load_p = [&](int prow0, uint4 (&pr)[NS]) {
+    const int ra = min(max(prow0 + col, 0), 2 * Tp - 2);
+    const T* prow = (const T*)p.P + (long)ra * p.ldp + (long)h * p.dkp;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) pr[s] = *(const uint4*)(prow + s * SE + hsel * (SE / 2));
+  };
+  auto bd_block = [&](const uint4 (&pr)[NS], int slot) {
+    f32x16 bd = f32x16{};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mfma_slab<T>(bd, pr[s], qv[s]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bd_s[(acc_row(r, lane) + 32 * slot) * BDS + col] = bd[r];
+  };
+  // P row of position block start for key tile j0: lower = Tp - 1 - (i0 + 31) + j0, upper = +32
+  uint4 pu[NS], pn[PF ? NS : 1];
+  if (jbeg < jend) {
+    uint4 pl[NS];
+    load_p(Tp - 1 - (i0 + 31) + jbeg, pl);
+    load_p(Tp - 1 - (i0 + 31) + jbeg + 32, pu);
+    bd_block(pl, 0);
+  }
+  int k = 0;
+  for (int j0 = jbeg; j0 < jend; j0 += 32, ++k) {
+    const bool more = j0 + 32 < jend;
+    if constexpr (PF) {
+      if (more) load_p(Tp - 1 - (i0 + 31) + j0 + 64, (uint4(&)[NS])pn);
+    }
+    f32x16 st = f32x16{};
+    const char* krow = Ks + (j0 + col) * g.ks + hsel * 16;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint4 kf = *(const uint4*)(krow + s * 32);
+      mfma_slab<T>(st, kf, qu[s]);
+    }
+    bd_block(pu, (k + 1) & 1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
+    __builtin_amdgcn_wave_barrier();
+    const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane, (k & 1) << 5);
+    softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
+    drop_tile(st, p.adrop, bh, Tp, iq, j0, lane);
+    uint2 v[ND][4];
+#pragma unroll
+    for (int n = 0; n < ND; ++n)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        v[n][q] = *(const uint2*)(Vs + (n * 32 + col) * g.vs + (j0 + 8 * q + 4 * hsel) * 2);
+    PV<T, ND>::run(o, st, v);
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // bd_s / row_s reads done before the next tile rewrites them
+    __builtin_amdgcn_wave_barrier();
+    if (more) {
+      if constexpr (PF) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) pu[s] = pn[s];
+      } else {
+        load_p(Tp - 1 - (i0 + 31) + j0 + 64, pu);
+      }
+    }
+  }
+  if (hsel == 0) row_s[col] = l_run;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  T* out = (T*)p.out;
+  if (ND <= 2 && p.vec_out && p.dk == ND * 32 && p.ldo % 8 == 0) {
+    // the wave's 32 x dk output tile goes through its (now free) BD image as fp32, then leaves as
+    // 16-byte rows of 8 bf16 (4 stores per lane instead of 16 * ND two-byte stores)
+    constexpr int OW = ND * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, lane);
+      const float l = row_s[i];
+      const bool valid = i0 + i < len && l > 0.0f;
+      const float inv = valid ? 1.0f / l : 0.0f;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) bd_s[i * OW + n * 32 + col] = valid ? o[n][r] * inv : 0.0f;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CH = OW / 8;   // 16-byte chunks per row
+#pragma unroll
+    for (int q = 0; q < 32 * CH / 64; ++q) {
+      const int j = lane + 64 * q, i = j / CH, c8 = j - i * CH;
+      if (i0 + i >= Tp) continue;
+      const float4 a = *(const float4*)(bd_s + i * OW + c8 * 8);
+      const float4 b2 = *(const float4*)(bd_s + i * OW + c8 * 8 + 4);
+      const float f[8] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w};
+      *(uint4*)(out + (rowbase + i0 + i) * p.ldo + (long)h * p.dk + c8 * 8) = Vec16<bf16_t>::from_f32(f);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = acc_row(r, lane);
+      const int ig = i0 + i;
+      const float l = row_s[i];
+      const bool valid = ig < len && l > 0.0f;
+      const float inv = valid ? 1.0f / l : 0.0f;
+      if (ig >= Tp) continue;
+#pragma unroll
+      for (int n = 0; n < ND; ++n) {
+        const int d = n * 32 + col;
+        if (d < p.dk) st_f<T>(out + (rowbase + ig) * p.ldo + (long)h * p.dk + d, valid ? o[n][r] * inv : 0.0f);
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int NS, int ND, int NW, bool PF, bool QN>
 __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   using T = bf16_t;
@@ -495,123 +625,234 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
         }
       }
     }
-    f32x16 o[ND];
-#pragma unroll
-    for (int n = 0; n < ND; ++n) o[n] = f32x16{};
-    float m_run = -INFINITY, l_run = 0.0f;
-    const int iq = i0 + col;
-    int jbeg = 0, jend = len;
-    if (p.ctx_left >= 0) jbeg = max(0, (i0 - p.ctx_left) & ~31);
-    if (p.ctx_right >= 0) jend = min(jend, i0 + 31 + p.ctx_right + 1);
+    attn_query_tile<NS, ND, PF>(p, g, Ks, Vs, bd_s, row_s, qu, qv, i0, len, rowbase, h, bh, lane);
+  }
+}
 
-    // BD window of key tile k = positions [j0 - i0 + T' - 32, j0 - i0 + T' + 32): its upper half is
-    // the lower half of tile k+1, so each tile computes one new 32-position block (P rows loaded
-    // one tile ahead) into the ring slot the block before last used.
-    auto load_p = [&](int prow0, uint4 (&pr)[NS]) {
-      const int ra = min(max(prow0 + col, 0), 2 * Tp - 2);
-      const T* prow = (const T*)p.P + (long)ra * p.ldp + (long)h * p.dkp;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) pr[s] = *(const uint4*)(prow + s * SE + hsel * (SE / 2));
-    };
-    auto bd_block = [&](const uint4 (&pr)[NS], int slot) {
-      f32x16 bd = f32x16{};
-#pragma unroll
-      for (int s = 0; s < NS; ++s) mfma_slab<T>(bd, pr[s], qv[s]);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) bd_s[(acc_row(r, lane) + 32 * slot) * BDS + col] = bd[r];
-    };
-    // P row of position block start for key tile j0: lower = Tp - 1 - (i0 + 31) + j0, upper = +32
-    uint4 pu[NS], pn[PF ? NS : 1];
-    if (jbeg < jend) {
-      uint4 pl[NS];
-      load_p(Tp - 1 - (i0 + 31) + jbeg, pl);
-      load_p(Tp - 1 - (i0 + 31) + jbeg + 32, pu);
-      bd_block(pl, 0);
+// ---------------------------------------------------------------------------------------------
+// QKV projection + rel-pos attention in one launch (bf16 eval forward with the LayerNorm fold,
+// dkp = 64, T' <= 256; conformer_modules.py:104-105, multi_head_attention.py:172-210).
+// Block = (utterance b, head h), 8 waves; wave w owns frames [32w, 32w + 32).
+// Phase 1, this head's slice of the QKV GEMM: the 192 folded weight rows (q | k | v of head h) stream
+// through a 3-stage LDS ring (glds, 24 KiB per 64-element K-step, XOR-swizzled as gemm_kernel's
+// images); each wave's 32 normalised-input rows (xb, the residual producer's compute-type copy) come
+// straight from global memory as MFMA operands.  Q and K are computed transposed (weights as A:
+// rows = channels, lane = frame), V as rows = frames, so after the folded-LayerNorm epilogue
+// y = rstd (acc - mean c) + d:
+//   * Q stays in registers: (y + u)c / (y + v)c become the attention's B-operand slabs after one
+//     v_permlane32_swap per 4 values (lane = query, 8 consecutive channels per slab half);
+//   * K goes to the LDS K image as 8-byte rows of 4 channels, V to the Vt image as 8-byte runs of
+//     4 frames of one channel; frames >= T' are zero in both.
+// Phase 2: attn_query_tile on the LDS-resident K / Vt, as rel_attn_lds_kernel.
+// Gone against the two-kernel path: the QKV GEMM launch and its M x 3*H*dkp output written to and
+// re-read from HBM.  The heads of one utterance are placed on one XCD (its xb rows stay in that L2).
+// ---------------------------------------------------------------------------------------------
+struct QkvFold {
+  const char* xb; long ldx_b;          // normalised-input rows (compute type), bytes per row
+  const float2* ln_in; int ln_parts, ln_width;   // producer granule partials (GemmEpi::ln_out)
+  const char* W; long ldw_b;           // folded q | k | v weight [3*H*dkp][Kpad] (compute type)
+  const float* lc; const float* ld;    // fold column terms [3*H*dkp]
+  const char* zero;                    // >= 1 KiB of zeros
+  int probe;                           // timing probes only (env CFM_QA_PROBE): 1 no attention phase, 2 no K loop
+};
+constexpr int QA_NS = 3;               // weight ring stages
+constexpr int QA_STAGE = 192 * 128;    // 192 weight rows x 128 bytes of K
+constexpr int QA_TAB_BYTES = (256 + 192 + 64) * 8;   // rs (per frame), cd (per channel), uv (per q channel)
+
+CFM_DEV_HOST_INLINE int qkv_attn_lds_bytes(int Tp) { return lds_geom(Tp, 64, 64, 8).bytes + QA_TAB_BYTES; }
+
+template <int NK>
+__global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold f) {
+  using T = bf16_t;
+  constexpr int NS = 4, ND = 2, DKP = 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hsel = lane >> 5, col = lane & 31;
+  const int nblocks = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+  const int bh = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int b = bh / p.H, h = bh - b * p.H;
+  const int Tp = p.Tp;
+  const int len = min(p.lens[b], Tp);
+  const LdsGeom g = lds_geom(Tp, DKP, DKP, 8);
+  const long rowbase = (long)b * Tp;
+  char* Ks = smem + g.k_off;
+  char* Vs = smem + g.v_off;
+  float2* rs_tab = (float2*)(smem + g.bytes);
+  float2* cd_tab = rs_tab + 256;
+  float2* uv_tab = cd_tab + 192;
+
+  // ---- phase 0: per-frame (mean, rstd) from the granule partials (the same expressions as the GEMM
+  // epilogue's fold), per-channel (c, d), per-q-channel (u, v) ----
+  if (tid < 256) {
+    const float2* pp = f.ln_in + (rowbase + min(tid, Tp - 1)) * f.ln_parts;
+    const int W = f.ln_width, np = f.ln_parts;
+    float sm = 0.0f;
+    for (int gi = 0; gi < np; ++gi) sm += (float)min(LN_GRANULE, W - gi * LN_GRANULE) * pp[gi].x;
+    const float mean = sm / (float)W;
+    float m2 = 0.0f;
+    for (int gi = 0; gi < np; ++gi) {
+      const float2 pg = pp[gi];
+      const float dm = pg.x - mean;
+      m2 += pg.y + (float)min(LN_GRANULE, W - gi * LN_GRANULE) * dm * dm;
     }
-    int k = 0;
-    for (int j0 = jbeg; j0 < jend; j0 += 32, ++k) {
-      const bool more = j0 + 32 < jend;
-      if constexpr (PF) {
-        if (more) load_p(Tp - 1 - (i0 + 31) + j0 + 64, (uint4(&)[NS])pn);
+    rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
+  } else if (tid < 448) {
+    const int c = tid - 256, part = c / DKP;
+    const long n = (long)part * p.H * DKP + h * DKP + (c - part * DKP);
+    cd_tab[c] = make_float2(f.lc[n], f.ld[n]);
+  } else {
+    const int c = tid - 448;
+    uv_tab[c] = make_float2(p.uv[h * DKP + c], p.uv[(long)p.H * DKP + h * DKP + c]);
+  }
+
+  // ---- phase 1: the head's QKV GEMM ----
+  // ring chunk c (0..23) of a stage = weight rows 8c .. 8c+7 (1 KiB); wave w fills chunks w, w+8, w+16
+  const char* wsrc[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int row = (i * 8 + wave) * 8 + lane / 8, part = row / DKP;
+    const long n = (long)part * p.H * DKP + h * DKP + (row - part * DKP);
+    wsrc[i] = f.W + n * f.ldw_b + (((lane & 7) ^ ((row >> 1) & 7)) * 16);
+  }
+  const uint32_t sbase = lds_addr(smem);
+  auto stage = [&](int kt) {   // past the last K-step: the zero page (uniform vmcnt counts)
+    const uint32_t base = sbase + (kt % QA_NS) * QA_STAGE;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      glds16_asm(kt < NK ? (const void*)(wsrc[i] + kt * 128) : (const void*)(f.zero + lane * 16),
+                 base + (i * 8 + wave) * 1024);
+  };
+  const char* xrow = f.xb + (rowbase + min(32 * wave + col, Tp - 1)) * f.ldx_b + hsel * 16;
+  auto load_x = [&](int kt, uint4 (&x)[4]) {
+    const int k = kt < NK ? kt : 0;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) x[kk] = *(const uint4*)(xrow + (k * 4 + kk) * 32);
+  };
+  const int sw = (col >> 1) & 7;
+  auto read_w = [&](int slot, int kk, uint4 (&w)[6]) {
+    const char* Sb = smem + slot * QA_STAGE;
+    const int so = ((2 * kk + hsel) ^ sw) * 16;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) w[j] = *(const uint4*)(Sb + (32 * j + col) * 128 + so);
+  };
+
+  f32x16 acc[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) acc[j] = f32x16{};
+  uint4 x[2][4], wc[6], wn[6];
+  load_x(0, x[0]);
+  stage(0);
+  stage(1);
+  wait_vmcnt<3>();      // stage 0 has landed (hipcc waits for the x rows itself at their first use)
+  wait_lgkm0();
+  raw_barrier();        // ... and the tables are written
+  read_w(0, 0, wc);
+  if (!(f.probe & 2))
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    // order matters for the counted waits: x rows of K-step kt+1, then weight stage kt+2
+    load_x(kt + 1, x[(kt + 1) & 1]);
+    stage(kt + 2);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < 3) {
+        read_w(kt % QA_NS, kk + 1, wn);
+      } else if (kt + 1 < NK) {
+        wait_vmcnt<7>();   // weight stage kt+1 (younger: x of kt+1, stage kt+2)
+        wait_lgkm0();
+        raw_barrier();
+        read_w((kt + 1) % QA_NS, 0, wn);
       }
-      f32x16 st = f32x16{};
-      const char* krow = Ks + (j0 + col) * g.ks + hsel * 16;
+      const uint4 xf = x[kt & 1][kk];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const uint4 kf = *(const uint4*)(krow + s * 32);
-        mfma_slab<T>(st, kf, qu[s]);
+      for (int j = 0; j < 4; ++j) acc[j] = mfma16_32x32x16(wc[j], xf, acc[j]);   // Q^T, K^T
+#pragma unroll
+      for (int j = 4; j < 6; ++j) acc[j] = mfma16_32x32x16(xf, wc[j], acc[j]);   // V
+#pragma unroll
+      for (int j = 0; j < 6; ++j) wc[j] = wn[j];
+    }
+  }
+  wait_vmcnt<0>();
+  wait_lgkm0();
+  raw_barrier();        // every wave is done with the ring: the K / Vt images may overwrite it
+
+  // ---- phase 1 epilogue ----
+  const int tq = 32 * wave + col;                  // this lane's frame in the Q / K products
+  const float2 rsq = rs_tab[tq];
+  uint4 qu[NS], qv[NS];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int sm = 0; sm < 2; ++sm) {
+      // slab 2j + sm = channels 32j + 16sm + [0, 16): rows m = 2sm (this half's channels +0..3, the other
+      // half's +4..7) and m = 2sm + 1 (+8..11 / +12..15) swap across the lane halves
+      float au[8], av[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = 8 * sm + i, rb = ra + 4;
+        const int ca = 32 * j + acc_row(ra, lane), cb = 32 * j + acc_row(rb, lane);
+        const float2 fa = cd_tab[ca], fb = cd_tab[cb];
+        const float ya = rsq.y * (acc[j][ra] - rsq.x * fa.x) + fa.y;
+        const float yb = rsq.y * (acc[j][rb] - rsq.x * fb.x) + fb.y;
+        const float2 pa = uv_tab[ca], pb = uv_tab[cb];
+        const auto su = __builtin_amdgcn_permlane32_swap(__float_as_uint((ya + pa.x) * p.qscale),
+                                                         __float_as_uint((yb + pb.x) * p.qscale), false, false);
+        const auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint((ya + pa.y) * p.qscale),
+                                                         __float_as_uint((yb + pb.y) * p.qscale), false, false);
+        au[i] = __uint_as_float(su[0]);
+        au[4 + i] = __uint_as_float(su[1]);
+        av[i] = __uint_as_float(sv[0]);
+        av[4 + i] = __uint_as_float(sv[1]);
       }
-      bd_block(pu, (k + 1) & 1);
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
-      __builtin_amdgcn_wave_barrier();
-      const float mloc = tile_scores(st, bd_s, p, j0, len, iq, lane, (k & 1) << 5);
-      softmax_tile<ND>(st, mloc, m_run, l_run, o, row_s, lane);
-      drop_tile(st, p.adrop, bh, Tp, iq, j0, lane);
-      uint2 v[ND][4];
+      qu[2 * j + sm] = Vec16<bf16_t>::from_f32(au);
+      qv[2 * j + sm] = Vec16<bf16_t>::from_f32(av);
+    }
+  // K rows: frame tq, channels 32(j-2) + 8m + 4*hsel + [0, 4)
+  if (tq < g.tp32) {
 #pragma unroll
-      for (int n = 0; n < ND; ++n)
+    for (int j = 2; j < 4; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          v[n][q] = *(const uint2*)(Vs + (n * 32 + col) * g.vs + (j0 + 8 * q + 4 * hsel) * 2);
-      PV<T, ND>::run(o, st, v);
-      __builtin_amdgcn_s_waitcnt(0xc07f);   // bd_s / row_s reads done before the next tile rewrites them
-      __builtin_amdgcn_wave_barrier();
-      if (more) {
-        if constexpr (PF) {
+      for (int m = 0; m < 4; ++m) {
+        const int c0 = 32 * (j - 2) + 8 * m + 4 * hsel;
+        float y[4];
 #pragma unroll
-          for (int s = 0; s < NS; ++s) pu[s] = pn[s];
-        } else {
-          load_p(Tp - 1 - (i0 + 31) + j0 + 64, pu);
+        for (int i = 0; i < 4; ++i) {
+          const float2 fc = cd_tab[64 + c0 + i];
+          y[i] = tq < Tp ? rsq.y * (acc[j][4 * m + i] - rsq.x * fc.x) + fc.y : 0.0f;
         }
+        *(uint2*)(Ks + tq * g.ks + c0 * 2) =
+            make_uint2((uint32_t)f2bf(y[0]) | ((uint32_t)f2bf(y[1]) << 16), (uint32_t)f2bf(y[2]) | ((uint32_t)f2bf(y[3]) << 16));
       }
+  }
+  // Vt: channel 32(j-4) + col, frames 32w + 8m + 4*hsel + [0, 4)
+#pragma unroll
+  for (int j = 4; j < 6; ++j) {
+    const int c = 32 * (j - 4) + col;
+    const float2 fc = cd_tab[128 + c];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int t0 = 32 * wave + 8 * m + 4 * hsel;
+      if (t0 >= g.tp32) continue;
+      float y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 rs = rs_tab[t0 + i];
+        y[i] = t0 + i < Tp ? rs.y * (acc[j][4 * m + i] - rs.x * fc.x) + fc.y : 0.0f;
+      }
+      *(uint2*)(Vs + c * g.vs + t0 * 2) =
+          make_uint2((uint32_t)f2bf(y[0]) | ((uint32_t)f2bf(y[1]) << 16), (uint32_t)f2bf(y[2]) | ((uint32_t)f2bf(y[3]) << 16));
     }
-    if (hsel == 0) row_s[col] = l_run;
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    T* out = (T*)p.out;
-    if (ND <= 2 && p.vec_out && p.dk == ND * 32 && p.ldo % 8 == 0) {
-      // the wave's 32 x dk output tile goes through its (now free) BD image as fp32, then leaves as
-      // 16-byte rows of 8 bf16 (4 stores per lane instead of 16 * ND two-byte stores)
-      constexpr int OW = ND * 32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = acc_row(r, lane);
-        const float l = row_s[i];
-        const bool valid = i0 + i < len && l > 0.0f;
-        const float inv = valid ? 1.0f / l : 0.0f;
-#pragma unroll
-        for (int n = 0; n < ND; ++n) bd_s[i * OW + n * 32 + col] = valid ? o[n][r] * inv : 0.0f;
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-      constexpr int CH = OW / 8;   // 16-byte chunks per row
-#pragma unroll
-      for (int q = 0; q < 32 * CH / 64; ++q) {
-        const int j = lane + 64 * q, i = j / CH, c8 = j - i * CH;
-        if (i0 + i >= Tp) continue;
-        const float4 a = *(const float4*)(bd_s + i * OW + c8 * 8);
-        const float4 b2 = *(const float4*)(bd_s + i * OW + c8 * 8 + 4);
-        const float f[8] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w};
-        *(uint4*)(out + (rowbase + i0 + i) * p.ldo + (long)h * p.dk + c8 * 8) = Vec16<bf16_t>::from_f32(f);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = acc_row(r, lane);
-        const int ig = i0 + i;
-        const float l = row_s[i];
-        const bool valid = ig < len && l > 0.0f;
-        const float inv = valid ? 1.0f / l : 0.0f;
-        if (ig >= Tp) continue;
-#pragma unroll
-        for (int n = 0; n < ND; ++n) {
-          const int d = n * 32 + col;
-          if (d < p.dk) st_f<T>(out + (rowbase + ig) * p.ldo + (long)h * p.dk + d, valid ? o[n][r] * inv : 0.0f);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+  }
+  wait_lgkm0();
+  __syncthreads();
+
+  // ---- phase 2: attention of the wave's query tile ----
+  const int i0 = 32 * wave;
+  if (i0 < Tp && !(f.probe & 1)) {
+    float* bd_s = (float*)(smem + g.bd_off + wave * (64 * BDS * 4 + 32 * 4));
+    attn_query_tile<NS, ND, true>(p, g, Ks, Vs, bd_s, bd_s + 64 * BDS, qu, qv, i0, len, rowbase, h, bh, lane);
   }
 }
 
@@ -718,6 +959,48 @@ void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, flo
     default: break;
   }
   if (!done) throw std::runtime_error("rel_pos_attention_natural: shape does not fit the LDS kernel");
+}
+
+bool qkv_attention_fused_supported(int dtype, int Tp, int dkp, int d) {
+  if (dtype != DT_BF16 || dkp != 64 || Tp < 1 || Tp > 256 || (d != 256 && d != 512)) return false;
+  return qkv_attn_lds_bytes(Tp) <= 160 * 1024;
+}
+
+void qkv_rel_attention_fused(const void* xb, int d, const float2* ln_in, int ln_parts, const void* Wqkv, int Kpad,
+                             const float* lc, const float* ld, const float* uv, float qscale, const void* P, long ldp,
+                             const int32_t* lens, int B, int Tp, int H, int dk, int ctx_left, int ctx_right, void* out,
+                             long ldo, const void* zero_page, hipStream_t st) {
+  if (B <= 0 || Tp <= 0) return;
+  if (!qkv_attention_fused_supported(DT_BF16, Tp, 64, d) || Kpad != d || dk > 64 || (dk + 15) / 16 * 16 != 64)
+    throw std::runtime_error("qkv_rel_attention_fused: bf16, dkp = 64, d in {256, 512}, T' <= 256 only");
+  AttnParams p;
+  p.qk = nullptr; p.ldqk = 0;
+  p.Vt = nullptr; p.vt_rows = 64; p.Tpad = 0;
+  p.P = (const char*)P; p.ldp = ldp;
+  p.lens = lens;
+  p.Tp = Tp; p.H = H; p.dk = dk; p.dkp = 64;
+  p.ctx_left = ctx_left; p.ctx_right = ctx_right;
+  p.out = (char*)out; p.ldo = ldo;
+  p.uv = uv; p.qscale = qscale;
+  p.adrop = Drop{0u, 0u, 1.0f};
+  p.vec_out = 1;
+  QkvFold f;
+  f.xb = (const char*)xb; f.ldx_b = (long)d * 2;
+  f.ln_in = ln_in; f.ln_parts = ln_parts; f.ln_width = d;
+  f.W = (const char*)Wqkv; f.ldw_b = (long)Kpad * 2;
+  f.lc = lc; f.ld = ld;
+  f.zero = (const char*)zero_page;
+  static const int probe = [] { const char* e = getenv("CFM_QA_PROBE"); return e ? atoi(e) : 0; }();
+  f.probe = probe;
+  const int bytes = qkv_attn_lds_bytes(Tp);
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)qkv_rel_attn_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qkv_rel_attn_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  if (d == 512) cfm_launch(qkv_rel_attn_kernel<8>, dim3(B * H), dim3(512), bytes, st, p, f);
+  else cfm_launch(qkv_rel_attn_kernel<4>, dim3(B * H), dim3(512), bytes, st, p, f);
 }
 
 void rel_pos_attention(int dtype, const void* qk, long ldqk, const void* Vt, int vt_rows, int Tpad, const void* P,

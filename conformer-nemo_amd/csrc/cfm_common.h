@@ -129,4 +129,25 @@ CFM_DEV void store16_wt(const void* base, long byte_off, uint4 v) {
   u32x4 d = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)byte_off, 0, 16);
 }
+// LDS-DMA issued from inline asm (hipcc's waitcnt pass does not see it, so it does not put a
+// vmcnt(0) in front of every ds_read), counted waits, a raw barrier and LDS byte addresses.
+CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+template <int N> CFM_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+CFM_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+CFM_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+CFM_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 }  // namespace cfm

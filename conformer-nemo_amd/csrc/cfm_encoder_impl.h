@@ -62,6 +62,10 @@ struct cfm_encoder {
   // 5.60 against 4.96 ms per forward (its 9 fp32 FMAs per X1 value overflow the MFMA ping-pong's VALU slots,
   // DESIGN.md section 4); env CFM_CONV12=1 turns it on
   bool fuse_conv12 = false;
+  // bf16 eval forward with the LayerNorm fold, dkp = 64, T' <= 256: each head's q | k | v projection
+  // and its attention in one launch (qkv_rel_attention_fused); CFM_QKV_ATTN=0 keeps the QKV GEMM +
+  // attention pair (A/B)
+  bool fuse_qkv_attn = true;
   std::vector<hipStream_t> sub_streams;
   std::vector<hipEvent_t> sub_events;   // [0] fork, [1 + i] join of part i
   void* zero_page = nullptr;

@@ -208,6 +208,16 @@ bool attn_natural_layout(int dtype, int Tp, int dkp);
 void rel_pos_attention_natural(const void* qkv, long ldqkv, const float* uv, float qscale, const void* P, long ldp,
                                const int32_t* lens, int B, int Tp, int H, int dk, int dkp, int ctx_left,
                                int ctx_right, void* out, long ldo, hipStream_t st);
+// QKV projection + attention in one launch (bf16 eval forward with the LayerNorm fold, dkp = 64,
+// T' <= 256, d in {256, 512}): xb = the normalised-input rows' compute-type copy (M x d), ln_in their
+// granule partials, Wqkv the folded q | k | v weight ([3*H*64][Kpad], Kpad = d) with column terms
+// lc / ld; uv, qscale, P, out as rel_pos_attention_natural.  Replaces gemm(EPI_STORE) into qkv +
+// rel_pos_attention_natural (no qkv buffer).
+bool qkv_attention_fused_supported(int dtype, int Tp, int dkp, int d);
+void qkv_rel_attention_fused(const void* xb, int d, const float2* ln_in, int ln_parts, const void* Wqkv, int Kpad,
+                             const float* lc, const float* ld, const float* uv, float qscale, const void* P, long ldp,
+                             const int32_t* lens, int B, int Tp, int H, int dk, int ctx_left, int ctx_right, void* out,
+                             long ldo, const void* zero_page, hipStream_t st);
 // q, k, v (M, H*dk), p (2T'-1, H*dk) in the compute type -> the qk / Vt / P layouts above, at ws,
 // ws + qk_bytes, ws + qk_bytes + vt_bytes (what the QKV and pos GEMM epilogues write in the encoder).
 void attn_relayout(int dt, const void* q, const void* k, const void* v, const void* p, const float* pos_u,

@@ -484,6 +484,7 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     if (const char* lf = getenv("CFM_LN_FOLD")) h->ln_fold = atoi(lf) != 0 && h->d % 4 == 0;
     if (const char* gd = getenv("CFM_GLU_DW")) h->fuse_glu_dw = atoi(gd) != 0;
     if (const char* cc = getenv("CFM_CONV12")) h->fuse_conv12 = atoi(cc) != 0;
+    if (const char* qa = getenv("CFM_QKV_ATTN")) h->fuse_qkv_attn = atoi(qa) != 0;
     ensure_streams(h.get(), 8);
     HIP_OK(hipSetDevice(prev));
     *out = h.release();
@@ -587,10 +588,10 @@ size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T) {
 namespace {
 
 enum Stage { ST_LEN, ST_CONV1, ST_CONV2, ST_SUBOUT, ST_POS, ST_LN, ST_FFN_UP, ST_FFN_DOWN, ST_QKV, ST_ATTN,
-             ST_OUTPROJ, ST_PW1, ST_DWCONV, ST_PW2, ST_OUT, ST_COUNT };
+             ST_OUTPROJ, ST_PW1, ST_DWCONV, ST_PW2, ST_OUT, ST_QKV_ATTN, ST_COUNT };
 const char* kStageNames[ST_COUNT] = {"lengths", "conv1", "conv2_gemm", "subsample_linear", "pos_gemm", "layernorm",
                                      "ffn_up_gemm", "ffn_down_gemm", "qkv_gemm", "rel_attention", "out_proj_gemm",
-                                     "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output"};
+                                     "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output", "qkv_attention"};
 
 // Stage timer (timed entry point only), installed as the thread's KernelClock.
 //   chain (default): one stop event per kernel, in the dispatch packet; per-kernel time = stop(k) -
@@ -704,7 +705,13 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
         layernorm(dt, X, M, d, Wf(Lw.ln_w[1]), Wf(Lw.ln_b[1]), nullptr, nullptr, nullptr, Hn, 0, st);
       }
       const long qkv_w = fold ? Lw.qkv_wf : Lw.qkv_w;
-      if (attn_natural_layout(dt, Tp, dkp)) {
+      if (fold && h->fuse_qkv_attn && qkv_attention_fused_supported(dt, Tp, dkp, d) && (int)h->kpad(d) == d) {
+        // the head's q | k | v projection and its attention in one launch (no qkv buffer)
+        TM(ST_QKV_ATTN);
+        qkv_rel_attention_fused(Hn, d, lns, lnp, W(qkv_w), (int)h->kpad(d), Wf(Lw.qkv_lc), Wf(Lw.qkv_ld), Wf(Lw.uv),
+                                attn_qscale(h->dk), Pbuf + (long)l * H * dkp * es, ldp, lens, B, Tp, H, h->dk,
+                                h->cfg.att_context_left, h->cfg.att_context_right, ws + wl.O, d, h->zero_page, st);
+      } else if (attn_natural_layout(dt, Tp, dkp)) {
         // plain bias GEMM into [q | k | v]; the attention kernel adds u / v, scales and transposes V
         TM(ST_QKV);
         GemmEpi e = epi_of(EPI_STORE, Wf(Lw.qkv_b));

@@ -90,16 +90,7 @@ using T128x256k = Tile<128, 256, 2, 2, 3, 1, 128, 2>;  // 8 waves = 2 K-groups x
 using T64x128k = Tile<64, 128, 2, 2, 3, 1, 128, 2>;    // 8 waves = 2 K-groups x 4, 3 x 24 KiB, wave tile 32 x 64
 using T128x128q = Tile<128, 128, 2, 2, 4, 1, 128, 4>;  // 16 waves = 4 K-groups x 4, 4 x 32 KiB, wave tile 64 x 64
 
-// ---- LDS-DMA and counted waits in inline asm ------------------------------------------------
-CFM_DEV void glds16_asm(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-template <int N> CFM_DEV void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 63, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+// LDS-DMA (glds16_asm) and counted waits: cfm_common.h
 // wait until at most `ahead` stages of G loads each are still in flight (ahead in [0, MAXA])
 template <int G, int MAXA> CFM_DEV void wait_stages(int ahead) {
   if constexpr (MAXA <= 0) {
@@ -108,15 +99,6 @@ template <int G, int MAXA> CFM_DEV void wait_stages(int ahead) {
     if (ahead >= MAXA) wait_vmcnt<G * MAXA>();
     else wait_stages<G, MAXA - 1>(ahead);
   }
-}
-CFM_DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-CFM_DEV void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-CFM_DEV uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
 // ---- A-operand loaders -----------------------------------------------------------------------

@@ -264,6 +264,58 @@ def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
     assert d <= 1e-2, f"fused vs unfused relL2 {d:.3e}"
 
 
+# (cfg, B, T, lengths) cases that take the fused QKV + attention launch (dkp = 64, d in {256, 512},
+# T' <= 256): ragged lengths incl. T' = 1, the T' = 256 edge, a context window, abs_pos, d = 256
+QKV_ATTN_CASES = {
+    "d512_ragged": (dict(d_model=512, n_heads=8, n_layers=2), 4, 411, [411, 300, 5, 1]),
+    "d512_tp256": (dict(d_model=512, n_heads=8, n_layers=1), 2, 1024, [1024, 997]),
+    "d256_ctx": (dict(d_model=256, n_heads=4, n_layers=2, att_context_size=[24, 9]), 3, 333, [333, 250, 120]),
+    "d256_abspos": (dict(d_model=256, n_heads=4, n_layers=2, self_attention_model="abs_pos"), 2, 301, [301, 177]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(QKV_ATTN_CASES))
+def test_bf16_fused_qkv_attention_matches_two_kernels(case, monkeypatch):
+    """bf16 with the LayerNorm fold: each head's q | k | v projection runs inside its attention launch
+    (qkv_rel_attention_fused); CFM_QKV_ATTN=0 keeps the QKV GEMM + attention pair.  Both
+    meet the bf16 gate against the oracle and agree to bf16 rounding (the fused kernel feeds the
+    unrounded q to the score operands)."""
+    cfg, B, T, lens = QKV_ATTN_CASES[case]
+    sd = make_state_dict(cfg, 7)
+    x, lens = make_inputs(B, T, seed=17, lengths=lens)
+    yr, ylr = O.encoder_forward(x, lens, sd, cfg)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_QKV_ATTN", flag)
+        y, yl = run(native(cfg, "bf16"), sd, x, lens)
+        np.testing.assert_array_equal(yl, ylr)
+        out[flag] = (y, check(y, yr, "bf16"))
+    d = rel_l2(out["1"][0], out["0"][0])
+    print(f"{case}: bf16 relL2 vs oracle: fused {out['1'][1]:.3e}, two kernels {out['0'][1]:.3e}; between {d:.3e}")
+    assert d <= 1e-2, f"fused vs two-kernel relL2 {d:.3e}"
+    assert out["1"][1] <= 1.1 * out["0"][1] + 1e-4
+
+
+def test_bf16_fused_qkv_attention_full_size(monkeypatch):
+    """The north-star shape (Large-17, B=32, T=1000, ragged lengths) through the fused QKV + attention
+    launch against the two-kernel path, with the enc_large17 reference utterances embedded."""
+    z = np.load(os.path.join(GOLDEN, "enc_large17.npz"))
+    cfg = json.loads(str(z["cfg_json"]))
+    sd = make_state_dict(cfg, int(z["seed"]))
+    x, lens = make_inputs(32, 1000, seed=11)
+    x[5], lens[5] = z["x"][0], z["lengths"][0]
+    x[30], lens[30] = z["x"][1], z["lengths"][1]
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_QKV_ATTN", flag)
+        y, yl = run(native(cfg, "bf16"), sd, x, lens)
+        np.testing.assert_array_equal(yl[[5, 30]], z["y_len"])
+        out[flag] = (y, check(y[[5, 30]], z["y"], "bf16"))
+    d = rel_l2(out["1"][0], out["0"][0])
+    print(f"full size: fused {out['1'][1]:.3e}, two kernels {out['0'][1]:.3e} vs reference; between {d:.3e}")
+    assert d <= 1e-2
+
+
 @pytest.mark.parametrize("B,T", [(2, 333), (32, 1000)])
 def test_bf16_fused_conv12_matches_two_kernels(B, T, monkeypatch):
     """ConvSubsampling's conv.0 recomputed inside conv.2's implicit GEMM (conv12_fused, CFM_CONV12=1)
