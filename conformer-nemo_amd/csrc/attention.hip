@@ -20,6 +20,7 @@
 // in the reference, whose probabilities are then zeroed (:107) -> their output is exactly 0.
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "cfm_common.h"
 #include "cfm_kernels.h"
@@ -683,30 +684,6 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
   float2* cd_tab = rs_tab + 256;
   float2* uv_tab = cd_tab + 192;
 
-  // ---- phase 0: per-frame (mean, rstd) from the granule partials (the same expressions as the GEMM
-  // epilogue's fold), per-channel (c, d), per-q-channel (u, v) ----
-  if (tid < 256) {
-    const float2* pp = f.ln_in + (rowbase + min(tid, Tp - 1)) * f.ln_parts;
-    const int W = f.ln_width, np = f.ln_parts;
-    float sm = 0.0f;
-    for (int gi = 0; gi < np; ++gi) sm += (float)min(LN_GRANULE, W - gi * LN_GRANULE) * pp[gi].x;
-    const float mean = sm / (float)W;
-    float m2 = 0.0f;
-    for (int gi = 0; gi < np; ++gi) {
-      const float2 pg = pp[gi];
-      const float dm = pg.x - mean;
-      m2 += pg.y + (float)min(LN_GRANULE, W - gi * LN_GRANULE) * dm * dm;
-    }
-    rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
-  } else if (tid < 448) {
-    const int c = tid - 256, part = c / DKP;
-    const long n = (long)part * p.H * DKP + h * DKP + (c - part * DKP);
-    cd_tab[c] = make_float2(f.lc[n], f.ld[n]);
-  } else {
-    const int c = tid - 448;
-    uv_tab[c] = make_float2(p.uv[h * DKP + c], p.uv[(long)p.H * DKP + h * DKP + c]);
-  }
-
   // ---- phase 1: the head's QKV GEMM ----
   // ring chunk c (0..23) of a stage = weight rows 8c .. 8c+7 (1 KiB); wave w fills chunks w, w+8, w+16
   const char* wsrc[3];
@@ -725,10 +702,20 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
                  base + (i * 8 + wave) * 1024);
   };
   const char* xrow = f.xb + (rowbase + min(32 * wave + col, Tp - 1)) * f.ldx_b + hsel * 16;
-  auto load_x = [&](int kt, uint4 (&x)[4]) {
-    const int k = kt < NK ? kt : 0;
+  // x fragments by inline-asm loads: hipcc does not count them, so its waits cannot over-wait on the
+  // weight stages issued in between; each group is retired by the counted wait that names it
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  auto load_x = [&](int kt, v4u (&x)[4]) {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) x[kk] = *(const uint4*)(xrow + (k * 4 + kk) * 32);
+    for (int kk = 0; kk < 4; ++kk)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x[kk]) : "v"(xrow + (kt * 4 + kk) * 32) : "memory");
+  };
+  // vmcnt(N) naming the x group it retires (N = the loads issued after it: x group + stage, or the
+  // stage alone past the last x group - no x loads are issued past the end, as an x register the
+  // kernel never reads would be handed to other values while its load is in flight)
+  auto wait_x = [&](auto n, v4u (&x)[4]) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "n"(decltype(n)::value)
+                 : "memory");
   };
   const int sw = (col >> 1) & 7;
   auto read_w = [&](int slot, int kk, uint4 (&w)[6]) {
@@ -741,31 +728,51 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
   f32x16 acc[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) acc[j] = f32x16{};
-  uint4 x[2][4], wc[6], wn[6];
+  // x rows two K-steps ahead, weight stages two ahead; the issue order (x(k), stage(k)) per K-step is
+  // what the counted waits below assume
+  v4u x[3][4];
+  uint4 wc[6], wn[6];
+  // the epilogue's tables: per-frame LayerNorm granule partials, per-channel (c, d), (u, v) - loaded
+  // first (in flight with the first stages), reduced and written to LDS after the loop
+  float2 part[4] = {};
+  float2 tab_a = make_float2(0.f, 0.f), tab_b = make_float2(0.f, 0.f);
+  if (tid < 256) {
+    const float2* pp = f.ln_in + (rowbase + min(tid, Tp - 1)) * f.ln_parts;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) part[gi] = pp[min(gi, f.ln_parts - 1)];
+  } else if (tid < 448) {
+    const int c = tid - 256, part_ = c / DKP;
+    const long n = (long)part_ * p.H * DKP + h * DKP + (c - part_ * DKP);
+    tab_a = make_float2(f.lc[n], f.ld[n]);
+  } else {
+    const int c = tid - 448;
+    tab_b = make_float2(p.uv[h * DKP + c], p.uv[(long)p.H * DKP + h * DKP + c]);
+  }
   load_x(0, x[0]);
   stage(0);
+  load_x(1, x[1]);
   stage(1);
-  wait_vmcnt<3>();      // stage 0 has landed (hipcc waits for the x rows itself at their first use)
-  wait_lgkm0();
-  raw_barrier();        // ... and the tables are written
+  wait_x(std::integral_constant<int, 7>{}, x[0]);   // tables' loads, x(0), stage 0 (younger: x(1), stage(1))
+  raw_barrier();
   read_w(0, 0, wc);
   if (!(f.probe & 2))
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
-    // order matters for the counted waits: x rows of K-step kt+1, then weight stage kt+2
-    load_x(kt + 1, x[(kt + 1) & 1]);
+    if (kt + 2 < NK) load_x(kt + 2, x[(kt + 2) % 3]);
     stage(kt + 2);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       if (kk < 3) {
         read_w(kt % QA_NS, kk + 1, wn);
       } else if (kt + 1 < NK) {
-        wait_vmcnt<7>();   // weight stage kt+1 (younger: x of kt+1, stage kt+2)
+        // x(kt+1) and weight stage kt+1 (younger: x(kt+2) while there is one, stage(kt+2))
+        if (kt + 2 < NK) wait_x(std::integral_constant<int, 7>{}, x[(kt + 1) % 3]);
+        else wait_x(std::integral_constant<int, 3>{}, x[(kt + 1) % 3]);
         wait_lgkm0();
         raw_barrier();
         read_w((kt + 1) % QA_NS, 0, wn);
       }
-      const uint4 xf = x[kt & 1][kk];
+      const uint4 xf = __builtin_bit_cast(uint4, x[kt % 3][kk]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = mfma16_32x32x16(wc[j], xf, acc[j]);   // Q^T, K^T
 #pragma unroll
@@ -775,8 +782,27 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
     }
   }
   wait_vmcnt<0>();
+  // per-frame (mean, rstd) from the granule partials (the GEMM epilogue's fold expressions)
+  if (tid < 256) {
+    const int W = f.ln_width, np = f.ln_parts;
+    float sm = 0.0f;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) sm += gi < np ? (float)min(LN_GRANULE, W - gi * LN_GRANULE) * part[gi].x : 0.0f;
+    const float mean = sm / (float)W;
+    float m2 = 0.0f;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      const float dm = part[gi].x - mean;
+      m2 += gi < np ? part[gi].y + (float)min(LN_GRANULE, W - gi * LN_GRANULE) * dm * dm : 0.0f;
+    }
+    rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
+  } else if (tid < 448) {
+    cd_tab[tid - 256] = tab_a;
+  } else {
+    uv_tab[tid - 448] = tab_b;
+  }
   wait_lgkm0();
-  raw_barrier();        // every wave is done with the ring: the K / Vt images may overwrite it
+  raw_barrier();        // tables written; every wave is done with the ring (the K / Vt images overwrite it)
 
   // ---- phase 1 epilogue ----
   const int tq = 32 * wave + col;                  // this lane's frame in the Q / K products
