@@ -28,6 +28,8 @@ def stage_of(name, state):
         return "conv1"
     if name.startswith("layernorm_kernel"):
         return "layernorm"
+    if "qkv_rel_attn" in name:         # fused QKV projection + attention
+        return "qkv_attention"
     if "rel_attn" in name:
         return "rel_attention"
     if name.startswith("dwconv"):
