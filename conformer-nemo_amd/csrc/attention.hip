@@ -654,13 +654,20 @@ struct QkvFold {
   const char* W; long ldw_b;           // folded q | k | v weight [3*H*dkp][Kpad] (compute type)
   const float* lc; const float* ld;    // fold column terms [3*H*dkp]
   const char* zero;                    // >= 1 KiB of zeros
-  int probe;                           // timing probes only (env CFM_QA_PROBE): 1 no attention phase, 2 no K loop
+  int probe;                           // timing probes only (env CFM_QA_PROBE): 1 no attention phase, 2 no K loop,
+                                       // 4 half the weight-fragment LDS reads, 8 no loads in the K loop
+                                       // (both give wrong results)
 };
-constexpr int QA_NS = 3;               // weight ring stages
+constexpr int QA_NS = 4;               // weight ring stages
 constexpr int QA_STAGE = 192 * 128;    // 192 weight rows x 128 bytes of K
 constexpr int QA_TAB_BYTES = (256 + 192 + 64) * 8;   // rs (per frame), cd (per channel), uv (per q channel)
 
-CFM_DEV_HOST_INLINE int qkv_attn_lds_bytes(int Tp) { return lds_geom(Tp, 64, 64, 8).bytes + QA_TAB_BYTES; }
+// the weight ring (phase 1) aliases the K / Vt / BD images (phase 2); the tables follow both
+CFM_DEV_HOST_INLINE int qkv_attn_tab_off(int Tp) {
+  const int b = lds_geom(Tp, 64, 64, 8).bytes;
+  return b > QA_NS * QA_STAGE ? b : QA_NS * QA_STAGE;
+}
+CFM_DEV_HOST_INLINE int qkv_attn_lds_bytes(int Tp) { return qkv_attn_tab_off(Tp) + QA_TAB_BYTES; }
 
 template <int NK>
 __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold f) {
@@ -680,7 +687,7 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
   const long rowbase = (long)b * Tp;
   char* Ks = smem + g.k_off;
   char* Vs = smem + g.v_off;
-  float2* rs_tab = (float2*)(smem + g.bytes);
+  float2* rs_tab = (float2*)(smem + qkv_attn_tab_off(Tp));
   float2* cd_tab = rs_tab + 256;
   float2* uv_tab = cd_tab + 192;
 
@@ -722,15 +729,16 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
     const char* Sb = smem + slot * QA_STAGE;
     const int so = ((2 * kk + hsel) ^ sw) * 16;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) w[j] = *(const uint4*)(Sb + (32 * j + col) * 128 + so);
+    for (int j = 0; j < 6; ++j) w[j] = *(const uint4*)(Sb + (32 * ((f.probe & 4) ? j % 3 : j) + col) * 128 + so);
   };
 
   f32x16 acc[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) acc[j] = f32x16{};
-  // x rows two K-steps ahead, weight stages two ahead; the issue order (x(k), stage(k)) per K-step is
-  // what the counted waits below assume
-  v4u x[3][4];
+  // x rows and weight stages three K-steps ahead; the issue order (x(k), stage(k)) per K-step is what
+  // the counted waits assume: x(k) and stage k are retired once only the groups of k+1 .. k+2 (x groups
+  // stop at the last K-step, stages are issued past it from the zero page) may still be in flight
+  v4u x[4][4];
   uint4 wc[6], wn[6];
   // the epilogue's tables: per-frame LayerNorm granule partials, per-channel (c, d), (u, v) - loaded
   // first (in flight with the first stages), reduced and written to LDS after the loop
@@ -748,31 +756,39 @@ __global__ __launch_bounds__(512) void qkv_rel_attn_kernel(AttnParams p, QkvFold
     const int c = tid - 448;
     tab_b = make_float2(p.uv[h * DKP + c], p.uv[(long)p.H * DKP + h * DKP + c]);
   }
-  load_x(0, x[0]);
-  stage(0);
-  load_x(1, x[1]);
-  stage(1);
-  wait_x(std::integral_constant<int, 7>{}, x[0]);   // tables' loads, x(0), stage 0 (younger: x(1), stage(1))
+  auto retire = [&](int k, v4u (&xg)[4]) {   // retire x(k) and stage k
+    const int younger = 3 * 2 + (k + 1 < NK ? 4 : 0) + (k + 2 < NK ? 4 : 0);
+    if (younger == 14) wait_x(std::integral_constant<int, 14>{}, xg);
+    else if (younger == 10) wait_x(std::integral_constant<int, 10>{}, xg);
+    else wait_x(std::integral_constant<int, 6>{}, xg);
+  };
+  static_assert(NK >= 3, "three K-steps in flight");
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    load_x(k, x[k]);
+    stage(k);
+  }
+  retire(0, x[0]);
   raw_barrier();
   read_w(0, 0, wc);
   if (!(f.probe & 2))
 #pragma unroll
   for (int kt = 0; kt < NK; ++kt) {
-    if (kt + 2 < NK) load_x(kt + 2, x[(kt + 2) % 3]);
-    stage(kt + 2);
+    if (!(f.probe & 8)) {
+      if (kt + 3 < NK) load_x(kt + 3, x[(kt + 3) % 4]);
+      stage(kt + 3);
+    }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       if (kk < 3) {
         read_w(kt % QA_NS, kk + 1, wn);
       } else if (kt + 1 < NK) {
-        // x(kt+1) and weight stage kt+1 (younger: x(kt+2) while there is one, stage(kt+2))
-        if (kt + 2 < NK) wait_x(std::integral_constant<int, 7>{}, x[(kt + 1) % 3]);
-        else wait_x(std::integral_constant<int, 3>{}, x[(kt + 1) % 3]);
+        retire(kt + 1, x[(kt + 1) % 4]);
         wait_lgkm0();
         raw_barrier();
         read_w((kt + 1) % QA_NS, 0, wn);
       }
-      const uint4 xf = __builtin_bit_cast(uint4, x[kt % 3][kk]);
+      const uint4 xf = __builtin_bit_cast(uint4, x[kt % 4][kk]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = mfma16_32x32x16(wc[j], xf, acc[j]);   // Q^T, K^T
 #pragma unroll

@@ -265,10 +265,11 @@ def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
 
 
 # (cfg, B, T, lengths) cases that take the fused QKV + attention launch (dkp = 64, d in {256, 512},
-# T' <= 256): ragged lengths incl. T' = 1, the T' = 256 edge, a context window, abs_pos, d = 256
+# T' <= 256): ragged lengths incl. T' = 1, the T' = 256 edge, a short batch, a context window, abs_pos, d = 256
 QKV_ATTN_CASES = {
     "d512_ragged": (dict(d_model=512, n_heads=8, n_layers=2), 4, 411, [411, 300, 5, 1]),
     "d512_tp256": (dict(d_model=512, n_heads=8, n_layers=1), 2, 1024, [1024, 997]),
+    "d512_short": (dict(d_model=512, n_heads=8, n_layers=2), 3, 60, [60, 33, 7]),   # T' = 15: ring > images
     "d256_ctx": (dict(d_model=256, n_heads=4, n_layers=2, att_context_size=[24, 9]), 3, 333, [333, 250, 120]),
     "d256_abspos": (dict(d_model=256, n_heads=4, n_layers=2, self_attention_model="abs_pos"), 2, 301, [301, 177]),
 }
