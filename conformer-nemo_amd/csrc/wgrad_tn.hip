@@ -215,26 +215,40 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
   const bool bias = p.ones && (int)blockIdx.x == (int)(blockIdx.y % gridDim.x) && wn == 0;
   // stage s -> slot s % NST: glds j of wave w moves 1 KB row group (w*G + j) % 8 (4 rows) of image
   // (w*G + j) / 8; lane l fills physical chunk l % 16 of row 4*rg + l / 16, i.e. loads the logical
-  // chunk that the XOR swizzle puts there (LDS-DMA writes are lane-linear)
+  // chunk that the XOR swizzle puts there (LDS-DMA writes are lane-linear).  The per-lane source of
+  // each glds is set up once and advanced by 32 rows per stage (stages are issued in order), so a
+  // stage costs an add, a row check and the DMA per glds.
+  const char* gp[G];
+  long gstep[G];
+  int grow[G];
+  bool gok[G];
+  const void* zp = (const void*)&g_zero16;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int gi = w * G + j, im = gi >> 3, rg = gi & 7;
+    const int row = rg * 4 + (lane >> 4), pc = lane & 15;
+    const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    grow[j] = row;
+    if (im < MI) {
+      const int na = m0 + im * TB + ch * 8;
+      gok[j] = na < p.M;
+      gp[j] = (const char*)(A + (long)row * p.lda + na);
+      gstep[j] = (long)TK * p.lda * 2;
+    } else {
+      const int kb = c0 + (im - MI) * TB + ch * 8;
+      gok[j] = kb < p.N;
+      gp[j] = (const char*)(B + (long)row * p.ldb + kb);
+      gstep[j] = (long)TK * p.ldb * 2;
+    }
+  }
   auto issue = [&](int s) {
     const uint32_t base = sb + (uint32_t)((s % NST) * STG);
     const long r0 = (long)s * TK;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int gi = w * G + j, im = gi >> 3, rg = gi & 7;
-      const int row = rg * 4 + (lane >> 4), pc = lane & 15;
-      const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
-      const long rr = r0 + row;
-      const bool rok = rr < rows;
-      const void* src;
-      if (im < MI) {
-        const int na = m0 + im * TB + ch * 8;
-        src = (rok && na < p.M) ? (const void*)(A + rr * p.lda + na) : (const void*)&g_zero16;
-      } else {
-        const int kb = c0 + (im - MI) * TB + ch * 8;
-        src = (rok && kb < p.N) ? (const void*)(B + rr * p.ldb + kb) : (const void*)&g_zero16;
-      }
-      glds16(src, base + im * (TK * 256) + rg * 1024);
+      glds16((gok[j] && r0 + grow[j] < rows) ? (const void*)gp[j] : zp, base + im * (TK * 256) + rg * 1024);
+      gp[j] += gstep[j];
     }
   };
   f32x16 acc[2][2];
