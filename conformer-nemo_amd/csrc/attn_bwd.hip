@@ -198,6 +198,85 @@ __global__ __launch_bounds__(256) void bgemm2_kernel(BgArgs a) {
   const int wm = w & 1, wn = w >> 1;
   const int aoff = (wm * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
   const int boff = (wn * 32 + (lane & 31)) * RB + 16 * (lane >> 5);
+  // both operands already in the 16-bit compute type: they move as raw 16-bit values (no fp32 round
+  // trip); a row-major (non k-contiguous) operand's 4x4 micro-block is transposed with v_perm_b32
+  constexpr bool RAW = sizeof(T) == 2 && std::is_same<TA, T>::value && std::is_same<TB, T>::value;
+  if constexpr (RAW) {
+    auto loadraw = [&](const bf16_t* P, long sr, long sk, bool kc, int r0, int R, int k0, uint2* v) {
+      const bool full = kc ? (r0 + ((3 * 256 + tid) >> 4) < R && k0 + 4 * (tid & 15) + 3 < KZ)
+                           : (k0 + 4 * (tid >> 4) + 3 < KZ && r0 + 4 * (tid & 15) + 3 < R);
+      if (full) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (kc) {
+            const int idx = q * 256 + tid;
+            v[q] = *(const uint2*)(P + (r0 + (idx >> 4)) * sr + k0 + 4 * (idx & 15));
+          } else {
+            v[q] = *(const uint2*)(P + r0 + 4 * (tid & 15) + (k0 + 4 * (tid >> 4) + q) * sk);
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t e16[4];
+        if (kc) {
+          const int idx = q * 256 + tid;
+          const int r = r0 + (idx >> 4), k = k0 + 4 * (idx & 15);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) e16[e] = (r < R && k + e < KZ) ? (uint32_t)P[r * sr + (k + e)] : 0u;
+        } else {
+          const int r = r0 + 4 * (tid & 15), k = k0 + 4 * (tid >> 4) + q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) e16[e] = (r + e < R && k < KZ) ? (uint32_t)P[(r + e) + k * sk] : 0u;
+        }
+        v[q] = make_uint2(e16[0] | (e16[1] << 16), e16[2] | (e16[3] << 16));
+      }
+    };
+    auto storeraw = [&](char* S, bool kc, const uint2* v) {
+      if (kc) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int idx = q * 256 + tid;
+          *(uint2*)(S + (idx >> 4) * RB + 8 * (idx & 15)) = v[q];
+        }
+      } else {
+        // v[q] = rows r .. r+3 at k + q; row r + e wants (k, k+1 | k+2, k+3) = element e of v[0..3]
+        const int r = 4 * (tid & 15), k = 4 * (tid >> 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t sel = (e & 1) ? 0x07060302u : 0x05040100u;
+          const uint32_t lo0 = (e < 2) ? v[0].x : v[0].y, lo1 = (e < 2) ? v[1].x : v[1].y;
+          const uint32_t hi0 = (e < 2) ? v[2].x : v[2].y, hi1 = (e < 2) ? v[3].x : v[3].y;
+          *(uint2*)(S + (r + e) * RB + 2 * k) =
+              make_uint2(__builtin_amdgcn_perm(lo1, lo0, sel), __builtin_amdgcn_perm(hi1, hi0, sel));
+        }
+      }
+    };
+    uint2 qa[4], qb[4];
+    loadraw((const bf16_t*)A, a.am, a.ak, a_kc, m0, a.M, 0, qa);
+    loadraw((const bf16_t*)Bm, a.bn, a.bk, b_kc, n0, a.N, 0, qb);
+    storeraw(As[0], a_kc, qa);
+    storeraw(Bs[0], b_kc, qb);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < KZ; k0 += KS) {
+      const bool more = k0 + KS < KZ;
+      if (more) {
+        loadraw((const bf16_t*)A, a.am, a.ak, a_kc, m0, a.M, k0 + KS, qa);
+        loadraw((const bf16_t*)Bm, a.bn, a.bk, b_kc, n0, a.N, k0 + KS, qb);
+      }
+#pragma unroll
+      for (int s = 0; s < KS * 2 / 32; ++s)
+        mfma_slab<T>(acc, *(const uint4*)(As[buf] + aoff + 32 * s), *(const uint4*)(Bs[buf] + boff + 32 * s));
+      if (more) {
+        storeraw(As[buf ^ 1], a_kc, qa);
+        storeraw(Bs[buf ^ 1], b_kc, qb);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
   loadop(A, a.am, a.ak, a_kc, m0, a.M, 0, ra);
   loadop(Bm, a.bn, a.bk, b_kc, n0, a.N, 0, rb);
   store(As[0], a_kc, ra);
@@ -219,6 +298,7 @@ __global__ __launch_bounds__(256) void bgemm2_kernel(BgArgs a) {
     }
     __syncthreads();
     buf ^= 1;
+  }
   }
   float* C = a.C + z1 * a.cz1 + z2 * a.cz2;
   const int n = n0 + wn * 32 + (lane & 31);
