@@ -552,7 +552,12 @@ __global__ __launch_bounds__(256) void colred_final2_kernel(const float* __restr
 //   pw[blk][c] = sum over the block's rows of dy * xhat,  pb[blk][c] = sum of dy
 // pk (bf16, optional): the next consumer's GEMM operand, pk[row][c] = bf16(dx * pscale * dropout'(row*d + c))
 // - what tpack2 would make of dx for that consumer, written here instead of re-read in another pass
-constexpr int kLnRowsPerWave = 4;
+// rows per wave (one in flight): 2 measured best (same-box training A/B: 30.66-30.84 ms/step against
+// 30.94-31.08 at 4 and 30.57-30.73 against 30.44-30.56 at 1) - more blocks keep more rows in flight
+#ifndef CFM_LN_ROWS
+#define CFM_LN_ROWS 2
+#endif
+constexpr int kLnRowsPerWave = CFM_LN_ROWS;
 template <int E4>
 __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                            const float* __restrict__ dy, int M, int d,
@@ -1282,7 +1287,7 @@ Ws ws_layout(const cfm_encoder* h, const Geo& g) {
   w.gA = a.take(M * d * 4);
   w.gB = a.take(M * d * 4);
   w.dbr = a.take(M * d * 4);
-  w.lnp = a.take(5L * 2 * ((M + 15) / 16) * d * 4);   // the layer's five LayerNorm backward column partials
+  w.lnp = a.take(5L * 2 * ((M + 4 * kLnRowsPerWave - 1) / (4 * kLnRowsPerWave)) * d * 4);   // the layer's five LayerNorm backward column partials
   w.dU = a.take(M * std::max(dff, 3 * d) * 4);
   w.pa = a.take(M * kp(Kmax) * es);                                   // dgrad A operand [M][N]
   const long NT = std::max({dff, 3 * d, 2 * d, (long)g.C});
