@@ -125,6 +125,51 @@ def cpu_baseline(enc, B, T, budget_s):
                       f"Large-17, B={Bs} x T={T} per forward, min of 2 after a B=2 warm-up, {total:.1f} s in all"}
 
 
+def stage_breakdown(args, enc, dev, x, lengths, B, T, d, L, H, es):
+    """Per-stage kernel durations of the forward (cfm_encoder_forward_timed: a start and a stop event in
+    every kernel's dispatch packet, the durations rocprofv3's kernel trace reports; mean of 3 forwards),
+    and the dominant stage's roofline entry."""
+    breakdown = {}
+    roof = None
+    native = enc._native_for(dev)
+    agg = {}
+    reps = 3
+    with torch.inference_mode():
+        for _ in range(reps):
+            for k, (ms, n) in native.forward_timed(x, lengths.to(torch.int32)).items():
+                a = agg.setdefault(k, [0.0, 0])
+                a[0] += ms / reps
+                a[1] = n
+    work = stage_work(B, T, d, L, H, es=es)
+    for k, (ms, n) in agg.items():
+        if n == 0:
+            continue
+        kind, amt = work.get(k, ("byte", 0))
+        per = ms / n
+        rate = amt / (per * 1e-3) / (1e12 if kind == "flop" else 1e9)
+        breakdown[k] = {"ms_total": round(ms, 4), "launches": n, "ms_per_launch": round(per, 5),
+                        ("TFLOP/s" if kind == "flop" else "GB/s"): round(rate, 1)}
+    dom = max((k for k in agg if agg[k][1]), key=lambda k: agg[k][0])
+    kind, amt = work[dom]
+    per_ms = agg[dom][0] / agg[dom][1]
+    tr = pmc_traffic(dom, B, T, L, args.compute)
+    traffic = None if tr is None else tr["bytes_per_launch"]
+    if kind == "flop":
+        ach = amt / (per_ms * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK[args.compute],
+                "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": traffic,
+                "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (start + stop event in each kernel's dispatch packet, {agg[dom][1]} launches per forward)"}
+    else:
+        ach = amt / (per_ms * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "per_launch": f"{amt / 1e6:.2f} MB in {per_ms:.4f} ms"}
+    roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
+    if tr is not None:
+        roof["traffic_source"] = tr["file"]
+    return roof, breakdown
+
+
 def parity_and_fp32(dev, B, T, steps=5):
     """What the bf16 headline hides (rank 0, after the timed loop):
     * the error of every compute mode at the timed shape against the REFERENCE encoder: the two
@@ -343,53 +388,17 @@ def main():
     t_max = max_over_ranks(elapsed, dev, dist)
     value = job_throughput(t_max, world, B, T, args.steps)
     ms_step = 1000.0 * t_max / args.steps
+    es = 4 if args.compute == "fp32" else 2
+    roof, breakdown = None, {}
+    if rank == 0 and not args.no_breakdown:
+        # per-kernel stage clock, right after the timed loop (same clock / thermal state as ms_per_step)
+        roof, breakdown = stage_breakdown(args, enc, dev, x, lengths, B, T, d, L, H, es)
     # BASELINE config 3 (training step, DP over the same ranks, RCCL gradient buckets): every rank runs it
     train = None if args.no_train else train_leg(args, world, rank, dev, dist, barrier, args.train_steps,
                                                    args.train_warmup)
 
     if rank == 0:
-        import conformer_amd
-        es = 4 if args.compute == "fp32" else 2
         total_flop = None
-        roof = None
-        breakdown = {}
-        if not args.no_breakdown:
-            native = enc._native_for(dev)
-            agg = {}
-            reps = 3
-            with torch.inference_mode():
-                for _ in range(reps):
-                    for k, (ms, n) in native.forward_timed(x, lengths.to(torch.int32)).items():
-                        a = agg.setdefault(k, [0.0, 0])
-                        a[0] += ms / reps
-                        a[1] = n
-            work = stage_work(B, T, d, L, H, es=es)
-            for k, (ms, n) in agg.items():
-                if n == 0:
-                    continue
-                kind, amt = work.get(k, ("byte", 0))
-                per = ms / n
-                rate = amt / (per * 1e-3) / (1e12 if kind == "flop" else 1e9)
-                breakdown[k] = {"ms_total": round(ms, 4), "launches": n, "ms_per_launch": round(per, 5),
-                                ("TFLOP/s" if kind == "flop" else "GB/s"): round(rate, 1)}
-            dom = max((k for k in agg if agg[k][1]), key=lambda k: agg[k][0])
-            kind, amt = work[dom]
-            per_ms = agg[dom][0] / agg[dom][1]
-            tr = pmc_traffic(dom, B, T, L, args.compute)
-            traffic = None if tr is None else tr["bytes_per_launch"]
-            if kind == "flop":
-                ach = amt / (per_ms * 1e-3) / 1e12
-                roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK[args.compute],
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK[args.compute], 4), "traffic": traffic,
-                        "per_launch": f"{amt / 1e9:.2f} GFLOP in {per_ms:.4f} ms (stop events in each dispatch packet, chained, {agg[dom][1]} launches per forward)"}
-            else:
-                ach = amt / (per_ms * 1e-3) / 1e9
-                roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "per_launch": f"{amt / 1e6:.2f} MB in {per_ms:.4f} ms"}
-            roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
-            if tr is not None:
-                roof["traffic_source"] = tr["file"]
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         from conformer_oracle import encoder_flops
         total_flop = encoder_flops(B, T, d, L)
@@ -417,6 +426,11 @@ def main():
             "fp16_mode": fp16_line,
             "breakdown": breakdown,
         }
+        if breakdown:
+            # kernel durations only: the rest of ms_per_step is dispatch gaps between the kernels
+            bsum = sum(v["ms_total"] for v in breakdown.values())
+            out["breakdown_sum"] = {"ms": round(bsum, 4), "of_ms_per_step": round(bsum / ms_step, 4),
+                                    "clock": os.environ.get("CFM_STAGE_CLOCK", "packet")}
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -141,7 +141,19 @@ class GradBuckets:
     # all-reduces overlapped.  Any later native backward of the same step writes into a scratch buffer
     # that is then added into the views, and its exchange is one all-reduce of the whole buffer at the
     # end of the backward.  All-reducing the accumulated sum is exact: the part already reduced is equal
-    # on every rank, so sum_r(avg(g1) + g2_r) / W = avg(g1) + avg(g2).
+    # on every rank, so sum_r(avg(g1) + g2_r) / W = avg(g1) + avg(g2).  Without averaging the reduced
+    # part R = sum(g1) would come back W times, so the buffer is scaled by 1/W before the next backward
+    # of the step writes into it: sum_r(R / W + g2_r) = sum(g1) + sum(g2).
+    # A new step is recognised by a member's .grad being None or not its view: use
+    # zero_grad(set_to_none=True) (the default) or call begin_step(); after zero_grad(set_to_none=False)
+    # the next backward is taken for an accumulation (still exact, but without the per-layer overlap).
+    def begin_step(self) -> None:
+        """Start a new optimizer step explicitly: zero the buffer, the next backward overlaps per layer."""
+        self.flat.zero_()
+        self._fresh, self._pending, self._finished = True, 0, False
+        for p, v in zip(self.members, self.views):
+            p.grad = v
+
     def attach(self) -> None:
         """Point every member's .grad at its view; zero the buffer when a new step starts (a member's
         .grad is None or not the view).  Called by every train-mode encoder forward."""
@@ -150,6 +162,12 @@ class GradBuckets:
             self.flat.zero_()
             self._fresh = True
             self._pending = 0
+            self._finished = False
+        elif getattr(self, "_finished", False):
+            # a later backward of the same step: the buffer holds reduced gradients
+            if not self.average and self.world > 1:
+                self.flat.mul_(1.0 / self.world)
+            self._finished = False
         for p, v in zip(self.members, self.views):
             if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                 p.grad = v
@@ -218,6 +236,7 @@ class GradBuckets:
         """End of the backward: reduce whatever no grad_ready covered, wait, average."""
         try:
             self._finish_impl()
+            self._finished = True
         finally:
             self._finish_queued = False
             self._pending = 0

@@ -198,9 +198,11 @@ class NativeEncoder:
         return y
 
     def forward_timed(self, x_bft: torch.Tensor, lengths: Optional[torch.Tensor] = None):
-        """Per-stage kernel timing (cfm_encoder_forward_timed: every launch replayed in a burst of 8
-        between HIP events).  Returns {stage: (device ms per forward, launches per forward)}.
-        Timing only: the outputs of this call are not the forward's."""
+        """Per-stage kernel timing (cfm_encoder_forward_timed): one production forward in which every
+        kernel carries a start and a stop event in its own dispatch packet, so a kernel's time is its
+        packet's begin -> end, the duration rocprofv3's kernel trace reports (CFM_STAGE_CLOCK=chain:
+        stop events only, chained; =burst: each launch replayed 8x between stream events).
+        Returns {stage: (device ms per forward, launches per forward)}."""
         B, F, T = x_bft.shape
         Tp = encoded_length(T)
         dout = self.cfg.feat_out if (self.cfg.feat_out > 0 and self.cfg.feat_out != self.cfg.d_model) else self.cfg.d_model

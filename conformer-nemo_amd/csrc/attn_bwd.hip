@@ -116,8 +116,8 @@ template <> struct Quad<float> {
 template <> struct Quad<bf16_t> {
   static CFM_DEV void ld(const bf16_t* p, float* v) {
     const uint2 q = *(const uint2*)p;
-    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    v[0] = bf2f((bf16_t)(q.x & 0xffffu)); v[1] = bf2f((bf16_t)(q.x >> 16));
+    v[2] = bf2f((bf16_t)(q.y & 0xffffu)); v[3] = bf2f((bf16_t)(q.y >> 16));
   }
 };
 
@@ -853,6 +853,7 @@ cfm_status cfm_op_rel_attention_backward(int dtype, const void* q, const void* k
   return guarded([&] {
     if (B <= 0 || Tp <= 0 || H <= 0 || dk <= 0) fail(CFM_ERR_INVALID_ARG, "bad shape");
     if (dk > 128) fail(CFM_ERR_UNSUPPORTED, "head dim > 128");
+    refuse_half_training(dtype == CFM_COMPUTE_FP32, "cfm_op_rel_attention_backward");
     if (!q || !k || !v || !p || !pos_u || !pos_v || !dctx || !dq || !dk_ || !dv || !ws)
       fail(CFM_ERR_INVALID_ARG, "null pointer");
     if (ws_bytes < cfm_op_rel_attention_backward_ws_size(dtype, B, Tp, H, dk))

@@ -538,6 +538,7 @@ cfm_status cfm_op_linear_backward(int dtype, const float* x, int M, int K, const
   return guarded([&] {
     if (!x || !w || !dy) fail(CFM_ERR_INVALID_ARG, "null argument");
     if (M <= 0 || K <= 0 || N <= 0 || K % 4) fail(CFM_ERR_INVALID_ARG, "bad sizes (K % 4 == 0 required)");
+    refuse_half_training(dtype == CFM_COMPUTE_FP32, "cfm_op_linear_backward");
     const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16;
     const LinBwdWs l = lin_bwd_ws(dt, M, K, N);
     if (!ws || ws_bytes < (size_t)l.total) fail(CFM_ERR_WORKSPACE, "workspace too small");

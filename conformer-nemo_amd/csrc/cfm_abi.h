@@ -44,6 +44,18 @@ cfm_status guarded(F&& f) {
   }
 }
 
+// The fp16 build (libcfm_f16.so, CFM_HALF_F16) is an inference build: its training and backward
+// entry points refuse the 16-bit mode (fp16 gradients would need loss scaling, and several backward
+// kernels - the weight-gradient TN kernel's bias sums, the attention-backward staging - decode their
+// 16-bit operands as bf16).  fp32 mode stays available in either library; bf16 training: libcfm.so.
+inline void refuse_half_training(bool is_f32, const char* what) {
+#ifdef CFM_HALF_F16
+  if (!is_f32) fail(CFM_ERR_UNSUPPORTED, std::string(what) + ": the fp16 library is inference-only; train in bf16 (libcfm.so) or fp32");
+#else
+  (void)is_f32; (void)what;
+#endif
+}
+
 inline long round_up(long v, long m) { return (v + m - 1) / m * m; }
 
 // host copies of the 16-bit compute type's conversions (cfm_common.h): bfloat16, or IEEE fp16 in

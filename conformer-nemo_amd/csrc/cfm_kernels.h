@@ -9,15 +9,18 @@ namespace cfm {
 
 // Kernel clock for cfm_encoder_forward_timed.  When installed on the calling thread, every launch
 // goes through it:
-//   * chain mode: each kernel carries a stop event in its own dispatch packet
-//     (hipExtLaunchKernel); a kernel's time is the gap between its stop and the previous kernel's
-//     stop on the stream (its execution + the dispatch gap), measured inside a normal forward;
+//   * packet mode (default): each kernel carries a start AND a stop event in its own dispatch packet
+//     (hipExtLaunchKernel); a kernel's time is the packet's begin -> end timestamps, the duration
+//     rocprofv3's kernel trace reports (no dispatch gap), measured inside a normal forward;
+//   * chain mode: a stop event only; a kernel's time is the gap between its stop and the previous
+//     kernel's stop on the stream (its execution + the dispatch gap + the event's own overhead);
 //   * burst mode: each launch is replayed reps() times back-to-back between two stream events
 //     (steady state, warm caches); the timed call's outputs are then not the forward's.
 struct KernelClock {
   virtual int reps() = 0;
   virtual void begin(hipStream_t st) = 0;
   virtual hipEvent_t stop_event() = 0;
+  virtual hipEvent_t start_event() { return nullptr; }
   virtual void end(hipStream_t st) = 0;
   virtual ~KernelClock() = default;
 };
@@ -33,7 +36,9 @@ inline void cfm_launch(F kernel, dim3 grid, dim3 block, uint32_t lds_bytes, hipS
   c->begin(st);
   for (int r = 1; r < c->reps(); ++r)
     hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, nullptr, nullptr, 0, args...);
-  hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, nullptr, c->stop_event(), 0, args...);
+  hipEvent_t e0 = c->start_event();
+  hipEvent_t e1 = c->stop_event();
+  hipExtLaunchKernelGGL(kernel, grid, block, lds_bytes, st, e0, e1, 0, args...);
   c->end(st);
 }
 

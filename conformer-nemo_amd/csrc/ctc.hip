@@ -539,6 +539,7 @@ cfm_status cfm_ctc_head_backward(cfm_ctc_head* h, const float* enc_bdt, int B, i
                                  void* workspace, size_t workspace_bytes, void* stream) {
   return guarded([&] {
     if (!h || !enc_bdt || !logprobs_btc || !grad_lp_btc) fail(CFM_ERR_INVALID_ARG, "null argument");
+    refuse_half_training(h->dtype == DT_F32, "cfm_ctc_head_backward");
     if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
     if (B <= 0 || T <= 0) fail(CFM_ERR_INVALID_ARG, "B and T must be positive");
     const HeadWs w = head_ws(h, B, T);

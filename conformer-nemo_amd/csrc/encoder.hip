@@ -594,15 +594,23 @@ const char* kStageNames[ST_COUNT] = {"lengths", "conv1", "conv2_gemm", "subsampl
                                      "pw1_glu_gemm", "dwconv_bn_swish", "pw2_gemm", "output", "qkv_attention"};
 
 // Stage timer (timed entry point only), installed as the thread's KernelClock.
-//   chain (default): one stop event per kernel, in the dispatch packet; per-kernel time = stop(k) -
-//     stop(k-1) (a start marker precedes the first kernel); outputs are the forward's.
+//   packet (default): a start and a stop event in each kernel's own dispatch packet; per-kernel time =
+//     the packet's begin -> end (what rocprofv3's kernel trace reports); outputs are the forward's.
+//   chain (env CFM_STAGE_CLOCK=chain): one stop event per kernel; per-kernel time = stop(k) - stop(k-1)
+//     (includes the dispatch gap and the event's own overhead: ~2.5 us per launch more than packet).
 //   burst (env CFM_STAGE_CLOCK=burst): kBurst back-to-back replays between two stream events.
 // A stage's time is the sum over its kernels; its launch count the number of kernels per forward.
 struct StageTimer final : KernelClock {
   static constexpr int kBurst = 8;
-  const bool burst = [] { const char* s = getenv("CFM_STAGE_CLOCK"); return s && std::string(s) == "burst"; }();
+  enum Mode { PACKET, CHAIN, BURST };
+  const Mode mode = [] {
+    const char* s = getenv("CFM_STAGE_CLOCK");
+    if (s && std::string(s) == "burst") return BURST;
+    if (s && std::string(s) == "chain") return CHAIN;
+    return PACKET;
+  }();
   int cur = -1;
-  std::vector<hipEvent_t> ev;   // burst: (start, stop) per kernel; chain: marker, then stop per kernel
+  std::vector<hipEvent_t> ev;   // burst / packet: (start, stop) per kernel; chain: marker, then stop per kernel
   std::vector<int> ids;
   hipEvent_t make() {
     hipEvent_t e;
@@ -611,24 +619,25 @@ struct StageTimer final : KernelClock {
     return e;
   }
   void mark(int id) { cur = id; }
-  int reps() override { return burst ? kBurst : 1; }
+  int reps() override { return mode == BURST ? kBurst : 1; }
   void begin(hipStream_t st) override {
     ids.push_back(cur);
-    if (burst || ev.empty()) HIP_OK(hipEventRecord(make(), st));
+    if (mode == BURST || (mode == CHAIN && ev.empty())) HIP_OK(hipEventRecord(make(), st));
   }
-  hipEvent_t stop_event() override { return burst ? nullptr : make(); }
+  hipEvent_t start_event() override { return mode == PACKET ? make() : nullptr; }
+  hipEvent_t stop_event() override { return mode == BURST ? nullptr : make(); }
   void end(hipStream_t st) override {
-    if (burst) HIP_OK(hipEventRecord(make(), st));
+    if (mode == BURST) HIP_OK(hipEventRecord(make(), st));
   }
   void finish(float* ms, int* launches) {
     if (!ev.empty()) HIP_OK(hipEventSynchronize(ev.back()));
     for (size_t i = 0; i < ids.size(); ++i) {
       float t = 0.f;
-      if (burst) {
-        HIP_OK(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
-        t /= kBurst;
-      } else {
+      if (mode == CHAIN) {
         HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      } else {
+        HIP_OK(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+        if (mode == BURST) t /= kBurst;
       }
       if (ids[i] >= 0 && ids[i] < ST_COUNT) { ms[ids[i]] += t; launches[ids[i]] += 1; }
     }

@@ -399,6 +399,7 @@ cfm_status cfm_rnnt_joint_forward_train(cfm_rnnt_joint* h, const float* enc_bdt,
                                         int U, float dropout, uint64_t seed, float* out, void* workspace,
                                         size_t workspace_bytes, void* stream) {
   return guarded([&] {
+    if (h) refuse_half_training(h->dtype == DT_F32, "cfm_rnnt_joint_forward_train");
     joint_forward(h, enc_bdt, dec_bdu, B, T, U, 0, out, workspace, workspace_bytes, (hipStream_t)stream,
                   make_drop(dropout, seed, 1));
   });
@@ -416,6 +417,7 @@ cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, cons
                                    float* db_out, void* workspace, size_t workspace_bytes, void* stream) {
   return guarded([&] {
     if (!h || !enc_bdt || !dec_bdu || !dlogits || !w_enc || !w_pred || !w_out) fail(CFM_ERR_INVALID_ARG, "null argument");
+    refuse_half_training(h->dtype == DT_F32, "cfm_rnnt_joint_backward");
     if (!h->weights_set) fail(CFM_ERR_WEIGHTS, "weights not set");
     if (B <= 0 || T <= 0 || U <= 0) fail(CFM_ERR_INVALID_ARG, "B, T and U must be positive");
     const long rows = (long)B * T * U;

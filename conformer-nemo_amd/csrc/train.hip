@@ -72,8 +72,8 @@ CFM_DEV void tpack_tile(float (*tile)[65], int bx, int by, const Tin* __restrict
 #pragma unroll
         for (int h = 0; h < VI / 4; ++h) {
           const uint2 t = *(const uint2*)(sp + 4 * h);
-          v[4 * h] = __uint_as_float(t.x << 16); v[4 * h + 1] = __uint_as_float(t.x & 0xffff0000u);
-          v[4 * h + 2] = __uint_as_float(t.y << 16); v[4 * h + 3] = __uint_as_float(t.y & 0xffff0000u);
+          v[4 * h] = bf2f((bf16_t)(t.x & 0xffffu)); v[4 * h + 1] = bf2f((bf16_t)(t.x >> 16));
+          v[4 * h + 2] = bf2f((bf16_t)(t.y & 0xffffu)); v[4 * h + 3] = bf2f((bf16_t)(t.y >> 16));
         }
       } else {
 #pragma unroll
@@ -2268,11 +2268,7 @@ static void make_step(Step& S, cfm_encoder* h, const float* const* params, int n
                       const cfm_train_opts* opts, void* tape, size_t tape_bytes, void* ws, size_t ws_bytes,
                       void* stream) {
   check_common(h, params, n_params, B, T, opts);
-#ifdef CFM_HALF_F16
-  // fp16 gradients would need loss scaling (their range, not their precision, is the limit): the fp16
-  // build is an inference build; train in bf16 (libcfm.so) or fp32
-  if (h->dtype != DT_F32) fail(CFM_ERR_UNSUPPORTED, "training in fp16 is not supported: use the bf16 or fp32 mode");
-#endif
+  refuse_half_training(h->dtype == DT_F32, "cfm_train_forward / cfm_train_backward");
   S.h = h;
   S.g = make_geo(h, B, T);
   S.tp = tape_layout(h, S.g);

@@ -45,6 +45,12 @@ __device__ __forceinline__ uint4 tr_frag(const char* img, int cb, int kb, int la
   return make_uint4(ua.x, ua.y, ub.x, ub.y);
 }
 
+// 1.0 in the 16-bit compute type (bf16, or IEEE fp16 in the CFM_HALF_F16 build)
+#ifdef CFM_HALF_F16
+constexpr uint32_t kOne16 = 0x3c00u;
+#else
+constexpr uint32_t kOne16 = 0x3f80u;
+#endif
 template <int BFN>
 __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16_t* __restrict__ A, long lda, int N,
                                                        const bf16_t* __restrict__ B, long ldb, int K, int ones,
@@ -80,7 +86,7 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16_t* __restrict_
         }
         rb[j] = v;
       } else {
-        rb[j] = make_uint4((rok && ones && kb == K) ? 0x3f80u : 0u, 0, 0, 0);   // bf16 1.0 in column K
+        rb[j] = make_uint4((rok && ones && kb == K) ? kOne16 : 0u, 0, 0, 0);   // 16-bit 1.0 in column K
       }
     }
   };
@@ -142,7 +148,7 @@ __global__ __launch_bounds__(256) void wgrad_tn_kernel(const bf16_t* __restrict_
 
 // ---- LDS-DMA variant (bfn = 0): NST-stage ring filled by global_load_lds_dwordx4, counted waits ----
 __device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};
-__device__ uint4 g_one16 = {0x3f80u, 0u, 0u, 0u};   // bf16 1.0 then zeros: the bias column's chunk
+__device__ uint4 g_one16 = {kOne16, 0u, 0u, 0u};   // 16-bit 1.0 then zeros: the bias column's chunk
 
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
   uint32_t keep;
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
           const uint32_t u[4] = {fa[i].x, fa[i].y, fa[i].z, fa[i].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            bsum[i] += __uint_as_float(u[e] << 16) + __uint_as_float(u[e] & 0xffff0000u);
+            bsum[i] += bf2f((bf16_t)(u[e] & 0xffffu)) + bf2f((bf16_t)(u[e] >> 16));
         }
       }
     }

@@ -46,7 +46,11 @@ int cfm_comm_allreduce_cb(void* user, float* buf, int64_t n, void* stream);
  * (numel 0 = no gradient), then any further gradients up to flat_numel (e.g. a CTC head).
  * Pass cfm_grad_buckets_ready_cb / the bucket handle as cfm_train_opts.grad_ready / grad_ready_user:
  * each reported range is all-reduced immediately (ordered after the backward's stream); then
- * cfm_grad_buckets_finish reduces everything not reported yet and scales the whole buffer. */
+ * cfm_grad_buckets_finish reduces everything not reported yet and scales the whole buffer.
+ * One backward per finish writes the buffer from zero.  Gradient accumulation (a second backward of
+ * the same step adding into the reduced buffer) is exact with average = 1; with average = 0 scale the
+ * buffer by 1/world (cfm_allreduce_grads-free: any device scale) before the second backward, or the
+ * already-reduced part comes back world times (conformer_amd/dist.py GradBuckets.attach does this). */
 cfm_status cfm_grad_buckets_create(cfm_comm* comm, float* flat, int64_t flat_numel, int n_rows,
                                    const int64_t* row_offset, const int64_t* row_numel, int average,
                                    cfm_grad_buckets** out);

@@ -148,11 +148,6 @@ size_t cfm_encoder_workspace_size(const cfm_encoder* h, int B, int T);
 cfm_status cfm_encoder_forward(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T, float* y_bdt,
                                int32_t* out_len_b, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Per-stage kernel timing on `stream` (single stream, no micro-batch split): every kernel launch
- * of the forward is replayed 8 times back-to-back between two HIP events, and the per-launch
- * average is ADDED into stage_ms[stage]; stage_launches[stage] += kernels per forward.
- * Synchronises.  The outputs of this call are NOT the forward's (replayed residual adds) — timing
- * only.  Not graph-capturable; used for the per-kernel roofline in bench.py. */
 /* The ConformerLayer stack alone (ConformerLayer.forward, conformer_modules.py:88-121, applied for
  * every layer of the handle as ConformerEncoder.forward_for_export :262-271 does): x_btd (B, T', d) fp32
  * is layer 0's input (after the positional encoding's xscale), y_btd (B, T', d) fp32 the last layer's
@@ -165,6 +160,13 @@ cfm_status cfm_encoder_layers_forward(cfm_encoder* h, const float* x_btd, const 
                                       const float* pos_emb, float* y_btd, void* workspace, size_t workspace_bytes,
                                       void* stream);
 
+/* Per-stage kernel timing on `stream` (single stream, no micro-batch split): one production forward
+ * in which every kernel carries a start and a stop event in its own dispatch packet; each kernel's
+ * begin -> end time (what rocprofv3's kernel trace reports) is ADDED into stage_ms[stage] and
+ * stage_launches[stage] += kernels per forward.  The outputs are the forward's.  Synchronises; not
+ * graph-capturable; used for the per-kernel roofline in bench.py.  CFM_STAGE_CLOCK=chain: stop events
+ * only, a kernel's time = its stop - the previous stop (adds the dispatch gap and the event overhead);
+ * =burst: every launch replayed 8x between two stream events (outputs then not the forward's). */
 int cfm_num_stages(void);
 const char* cfm_stage_name(int i);
 cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,

@@ -156,7 +156,7 @@ def test_bucketed_overlapped_allreduce_equals_flat_gloo_ws2():
         assert issued == [(12, 24), (0, 12), (24, 30)]
 
 
-def _accum_worker(rank, world, port, q):
+def _accum_worker(rank, world, port, q, average=True):
     """Two micro-batches per optimizer step through GradBuckets (accumulation): the first
     native backward writes into the views with overlapped per-layer all-reduces, the second writes into
     the scratch and is added in; the result must equal the flat all-reduce of the summed plain grads."""
@@ -167,7 +167,7 @@ def _accum_worker(rank, world, port, q):
         g = torch.Generator().manual_seed(5 + rank)
         P = [torch.nn.Parameter(torch.zeros(s)) for s in ((4, 3), (7,), (5,))]
         head = torch.nn.Parameter(torch.zeros(6))
-        gb = cdist.GradBuckets(P, [head], average=True)
+        gb = cdist.GradBuckets(P, [head], average=average)
         want = [True, True, True]
         micro = [({i: torch.randn(P[i].shape, generator=g) for i in range(3)}, torch.randn(6, generator=g))
                  for _ in range(2)]
@@ -189,23 +189,32 @@ def _accum_worker(rank, world, port, q):
         Q = [torch.nn.Parameter(torch.zeros(t.shape)) for t in P + [head]]
         for j, qp in enumerate(Q):
             qp.grad = sum((micro[k][0][j] if j < 3 else micro[k][1]) for k in range(2)).clone()
-        cdist.allreduce_gradients(Q)
+        cdist.allreduce_gradients(Q, average=average)
         close = all(torch.allclose(a, qp.grad, rtol=1e-6, atol=1e-6) for a, qp in zip(got, Q))
         # a new step (grads set to None) starts from zero again
         for p in P + [head]:
             p.grad = None
         gb.attach()
         fresh_zero = bool((gb.flat == 0).all()) and gb.overlap
+        # zero_grad(set_to_none=False) keeps the views: begin_step() marks the new step explicitly
+        gb.finish()
+        gb.flat.fill_(3.0)
+        gb.begin_step()
+        gb.attach()
+        fresh_zero = fresh_zero and bool((gb.flat == 0).all()) and gb.overlap
         q.put((rank, overlaps, close, fresh_zero))
     finally:
         dist.destroy_process_group()
 
 
-def test_gradient_accumulation_through_buckets_gloo_ws2():
+@pytest.mark.parametrize("average", [True, False])
+def test_gradient_accumulation_through_buckets_gloo_ws2(average):
+    """with average=False the reduced part of the first backward must not come back
+    world times after the second backward's all-reduce."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q, average)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
