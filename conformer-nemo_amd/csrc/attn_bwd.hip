@@ -621,23 +621,25 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
   __syncthreads();
   const long img = (long)bh * Tp * sld;
   bf16_t* Gb = G + ((long)h * B + b) * Tp * gld;
-  const int cps = (int)(sld / 4), cpg = (int)(gld / 4);
+  // 16-byte runs (sld, gld and the LDS row pitch are multiples of 8 elements)
+  const int cps = (int)(sld / 8), cpg = (int)(gld / 8);
   for (int il = w; il < 32 && i0 + il < Tp; il += nw) {
     const int i = i0 + il, sh = Tp - 1 - i;
     const bf16_t* pr = Ps + il * SP;
     const bf16_t* dr = dSs + il * SP;
     for (int c = lane; c < cps; c += 64) {
-      *(uint2*)(Pg + img + (long)i * sld + 4 * c) = *(const uint2*)(pr + 4 * c);
-      *(uint2*)(dSg + img + (long)i * sld + 4 * c) = *(const uint2*)(dr + 4 * c);
+      *(uint4*)(Pg + img + (long)i * sld + 8 * c) = *(const uint4*)(pr + 8 * c);
+      *(uint4*)(dSg + img + (long)i * sld + 8 * c) = *(const uint4*)(dr + 8 * c);
     }
     for (int c = lane; c < cpg; c += 64) {
-      uint32_t v[4];
+      uint32_t v[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = 4 * c + e - sh;
+      for (int e = 0; e < 8; ++e) {
+        const int j = 8 * c + e - sh;
         v[e] = (j >= 0 && j < Tp) ? (uint32_t)dr[j] : 0u;
       }
-      *(uint2*)(Gb + (long)i * gld + 4 * c) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+      *(uint4*)(Gb + (long)i * gld + 8 * c) =
+          make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
     }
   }
 }

@@ -282,6 +282,33 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     const int n = n0 + cc * 4;
     const int nc = min(n, p.N - 4);
     const bool colok = n < p.N;
+    if constexpr (EPI == EPI_SCALE_F32) {
+      if (e.out_scalar) {
+        // fp32 rows whose stride is not a multiple of 4 (e.g. the RNN-T joint's V + 1 = 1025 logits): each
+        // tile row is re-cut at the 16-byte boundaries of ITS global address - float4 stores for the
+        // aligned body, scalar stores for the < 4 leading and trailing elements (one thread per row)
+        const int ncols = min(TL::BN, p.N - n0);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const int r = r0 + q * RPP;
+          const int m = m0 + r;
+          if (m >= p.M || ncols <= 0) continue;
+          const long g0 = xoff + (long)m * e.ldx + n0;
+          const int lead = min((int)(((16 - ((uintptr_t)(e.X + g0) & 15)) & 15) >> 2), ncols);   // fp32 base: 4-B aligned
+          const int nfull = (ncols - lead) / 4;
+          const float* ir = img + r * TL::EPS;
+          if (cc < nfull) {
+            const int j = lead + 4 * cc;
+            *(float4*)(e.X + g0 + j) = make_float4(ir[j] * e.alpha, ir[j + 1] * e.alpha, ir[j + 2] * e.alpha,
+                                                   ir[j + 3] * e.alpha);
+          } else if (cc == CPR - 1) {
+            for (int j = 0; j < lead; ++j) e.X[g0 + j] = ir[j] * e.alpha;
+            for (int j = lead + 4 * nfull; j < ncols; ++j) e.X[g0 + j] = ir[j] * e.alpha;
+          }
+        }
+        return;
+      }
+    }
     float4 xv[NP];
     if constexpr (EPI == EPI_RESID) {
       const float* XI = e.Xin ? e.Xin : e.X;
@@ -613,7 +640,192 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
   }
 }
 
-template <typename T, int EPI, class TL, class ALoad>
+// ---- direct epilogue: accumulators -> global from registers (no LDS image, no passes) ----------
+// With DIRECT the main loop multiplies W-fragments by A-fragments (C^T per 32x32 block), so lane l of
+// a block holds token m = (l & 31) and the 16 channels acc_row(r, l) = (r & 3) + 8 (r >> 2) + 4 (l >> 5):
+// four runs of 4 consecutive channels.  fp32 outputs (EPI_RESID, EPI_SCALE_F32) go out as one float4
+// per run; compute-type outputs are packed to bf16 pairs and regrouped by four v_permlane32_swap into
+// two 16-byte chunks of 8 consecutive channels per lane (lanes < 32: channels 0-7 / 16-23 of the block,
+// lanes >= 32: 8-15 / 24-31).  Every wave stores its own blocks as soon as they are final: no image
+// write, no barrier between passes, all waves storing at once.
+// K-groups (KG = 2): group g finalises the blocks with (i * NR + j) % 2 == g (ownership by block), the
+// other group's partial sums come through LDS once (owner + partner: the same fp32 sum as the image path).
+template <class TL> struct DirectGeo {
+  static constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;   // wave tile
+  static constexpr int XB = TL::MR * TL::NR * 64 * 64;                  // exchange bytes per wave (all blocks)
+  static CFM_DEV bool owned(int i, int j, int kg) { return TL::KG == 1 || ((i * TL::NR + j) % TL::KG) == kg; }
+};
+
+// bf16 pairs of 16 accumulator values (4 runs of 4 channels) -> two 16-byte chunks of 8 channels
+CFM_DEV void pack_chunks16(const float* v, uint4& c0, uint4& c1) {
+  uint32_t d[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) d[q] = (uint32_t)f2bf(v[2 * q]) | ((uint32_t)f2bf(v[2 * q + 1]) << 16);
+  const auto s0 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+  const auto s1 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+  const auto s2 = __builtin_amdgcn_permlane32_swap(d[4], d[6], false, false);
+  const auto s3 = __builtin_amdgcn_permlane32_swap(d[5], d[7], false, false);
+  c0 = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  c1 = make_uint4(s2[0], s3[0], s2[1], s3[1]);
+}
+
+template <typename T, int EPI, class TL, bool FOLD>
+CFM_DEV void epilogue_direct(const GemmParams& p, f32x16 (&acc)[TL::MR][TL::NR], char* smem, int m0, int n0,
+                             int wm, int wn, int kg, int lane, const float2* rs, const float2* cd, long xoff) {
+  using G = DirectGeo<TL>;
+  const GemmEpi& e = p.epi;
+  const int hi = lane >> 5;
+  constexpr bool kF32 = EPI == EPI_RESID || EPI == EPI_SCALE_F32;
+  constexpr bool kStats = EPI == EPI_RESID && FOLD;           // LayerNorm-fold producer
+  constexpr int NBJ = TL::BN / 32;                              // 32-column blocks per tile row
+  // per (token, 32-column block) (mean, M2) partials of the producer, combined per 128-column granule
+  float2* st_tab = (float2*)(smem + TL::RS_OFF - TL::BM * NBJ * 8);
+#pragma unroll
+  for (int i = 0; i < TL::MR; ++i) {
+    const int tl = wm * G::WTM + i * 32 + (lane & 31);        // tile-local token
+    const int m = m0 + tl;
+    const int mc = min(m, p.M - 1);
+    float2 rsv = make_float2(0.0f, 1.0f);
+    if constexpr (FOLD && !kStats) rsv = rs[tl];
+#pragma unroll
+    for (int j = 0; j < TL::NR; ++j) {
+      if (!G::owned(i, j, kg)) continue;
+      const int cl = wn * G::WTN + j * 32;                      // tile-local first channel of the block
+      float v[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c4 = cl + 8 * g + 4 * hi;                     // this lane's run of 4 channels
+        const float4 bb = *(const float4*)(cd + c4) ;           // (c, d) or (bias, 0) of 2 channels...
+        const float4 bb2 = *(const float4*)(cd + c4 + 2);
+        const float2 t[4] = {make_float2(bb.x, bb.y), make_float2(bb.z, bb.w), make_float2(bb2.x, bb2.y),
+                             make_float2(bb2.z, bb2.w)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a = acc[i][j][4 * g + q];
+          float x;
+          if constexpr (FOLD && !kStats) x = rsv.y * (a - rsv.x * t[q].x) + t[q].y;
+          else x = a + t[q].x;
+          if constexpr (EPI == EPI_RELU) x = fmaxf(x, 0.0f);
+          if constexpr (EPI == EPI_SWISH) x = swishf(x);
+          v[4 * g + q] = x;
+        }
+      }
+      if constexpr (kF32) {
+        float o[16];
+        if constexpr (EPI == EPI_RESID) {
+          const float* XI = e.Xin ? e.Xin : e.X;
+          float4 xv[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = min(n0 + cl + 8 * g + 4 * hi, p.N - 4);
+            xv[g] = *(const float4*)(XI + xoff + (long)mc * e.ldx + n);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float xs[4] = {xv[g].x, xv[g].y, xv[g].z, xv[g].w};
+            const uint64_t i0 = (uint64_t)m * e.ldx + (n0 + cl + 8 * g + 4 * hi);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              o[4 * g + q] = e.drop.thr ? xs[q] + (e.alpha * v[4 * g + q]) * drop_mul(e.drop, i0 + q)
+                                        : xs[q] + v[4 * g + q] * e.alpha;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) o[q] = v[q] * e.alpha;
+        }
+        if (m < p.M) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + cl + 8 * g + 4 * hi;
+            if (n < p.N) {
+              const long off = xoff + (long)m * e.ldx + n;
+              const uint4 u = make_uint4(__float_as_uint(o[4 * g]), __float_as_uint(o[4 * g + 1]),
+                                         __float_as_uint(o[4 * g + 2]), __float_as_uint(o[4 * g + 3]));
+              if (e.wt) store16_wt(e.X, off * 4, u);
+              else *(uint4*)(e.X + off) = u;
+            }
+          }
+        }
+        if constexpr (kStats) {
+          // the compute-type copy of the new rows (the folded consumer's A operand) ...
+          uint4 c0, c1;
+          pack_chunks16(o, c0, c1);
+          const int nb = n0 + cl + 8 * hi;
+          if (m < p.M) {
+            if (nb < p.N) *(uint4*)((T*)e.xb + (long)m * e.ldx + nb) = c0;
+            if (nb + 16 < p.N) *(uint4*)((T*)e.xb + (long)m * e.ldx + nb + 16) = c1;
+          }
+          // ... and this token's (mean, M2) over the block's valid channels (two passes, no cancellation)
+          const int nv = max(0, min(32, p.N - (n0 + cl)));
+          float sm = 0.0f;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sm += (cl + 8 * g + 4 * hi + q < cl + nv) ? o[4 * g + q] : 0.0f;
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(sm), __float_as_uint(sm), false, false);
+          const float mean = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) / (float)max(nv, 1);
+          float q2 = 0.0f;
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float dv = o[4 * g + q] - mean;
+              q2 += (cl + 8 * g + 4 * hi + q < cl + nv) ? dv * dv : 0.0f;
+            }
+          const auto sq = __builtin_amdgcn_permlane32_swap(__float_as_uint(q2), __float_as_uint(q2), false, false);
+          if (hi == 0) st_tab[tl * NBJ + cl / 32] = make_float2(mean, __uint_as_float(sq[0]) + __uint_as_float(sq[1]));
+        }
+      } else {
+        uint4 c0, c1;
+        pack_chunks16(v, c0, c1);
+        const int nb = n0 + cl + 8 * hi;
+        if (m < p.M) {
+          T* row = (T*)e.C + (long)m * e.ldc;
+          const uint4 cs[2] = {c0, c1};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int n = nb + 16 * h;
+            if (n + 8 <= p.N) {
+              if (e.wt) store16_wt(e.C, ((long)m * e.ldc + n) * (long)sizeof(T), cs[h]);
+              else *(uint4*)(row + n) = cs[h];
+            } else if (n < p.N) {
+              const uint32_t w[4] = {cs[h].x, cs[h].y, cs[h].z, cs[h].w};
+              for (int q = 0; q < 8 && n + q < p.N; ++q) row[n + q] = (T)(q & 1 ? w[q >> 1] >> 16 : w[q >> 1] & 0xffffu);
+            }
+          }
+        }
+      }
+    }
+  }
+  if constexpr (kStats) {
+    // per 128-column granule: Chan's combination of the four 32-column block partials, one thread
+    // per (token, granule) of the tile
+    __syncthreads();
+    constexpr int GPT = TL::BN / LN_GRANULE;
+    static_assert(TL::BN % LN_GRANULE == 0, "tile width: whole LayerNorm granules");
+    for (int t = threadIdx.x; t < TL::BM * GPT; t += TL::NT) {
+      const int tl = t / GPT, gl = t - tl * GPT;
+      const int m = m0 + tl;
+      const int g = n0 / LN_GRANULE + gl;
+      const int cnt = min(LN_GRANULE, p.N - g * LN_GRANULE);
+      if (m >= p.M || cnt <= 0) continue;
+      float n_a = 0.0f, mean = 0.0f, m2 = 0.0f;
+#pragma unroll
+      for (int b = 0; b < LN_GRANULE / 32; ++b) {
+        const float n_b = (float)max(0, min(32, cnt - 32 * b));
+        if (n_b <= 0.0f) continue;
+        const float2 pb = st_tab[tl * NBJ + gl * (LN_GRANULE / 32) + b];
+        const float n = n_a + n_b, dm = pb.x - mean;
+        mean += dm * (n_b / n);
+        m2 += pb.y + dm * dm * (n_a * n_b / n);
+        n_a = n;
+      }
+      e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, m2);
+    }
+  }
+}
+
+template <typename T, int EPI, class TL, class ALoad, bool DIRECT = false>
 __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload) {
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -660,6 +872,8 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
     const int nc = n0 + min(tid, TL::BN - 1);
     cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
+  } else if (DIRECT && p.epi.bias) {   // the direct epilogue reads the bias from the same LDS table
+    cd_pre = make_float2(p.epi.bias[n0 + min(tid, TL::BN - 1)], 0.0f);
   }
 
   auto stage = [&](int kt, int slot) {
@@ -725,7 +939,10 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
+        for (int j = 0; j < TL::NR; ++j) {
+          if constexpr (DIRECT) mfma_slab<T>(acc[i][j], bfc[j], afc[i]);   // C^T blocks: lane = token
+          else mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
+        }
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
 #pragma unroll
@@ -746,9 +963,47 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   // ---- epilogue through LDS, BM/EP rows per pass ----
   wait_lgkm0();
   raw_barrier();                         // every wave is done reading the ring
+  if constexpr (DIRECT) {
+    if constexpr (TL::KG > 1) {
+      // the blocks this wave does not finalise go to their owner group once: slot [block][lane][16]
+      // of this wave's region (lane-linear 16-byte accesses: conflict-free)
+      static_assert(TL::KG == 2, "direct epilogue: two K-groups");
+      float4* xr = (float4*)smem;
+      constexpr int WG = TL::WM * TL::WN;                      // waves per K-group
+      const int wq = wave % WG;
+      // block b = i * NR + j is owned by group b % 2: each group hands over the other half, b / 2 indexes it
+      auto slot = [&](int g, int i, int j) { return ((g * WG + wq) * (TL::MR * TL::NR / 2) + (i * TL::NR + j) / 2) * 64 * 4; };
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j)
+          if (!DirectGeo<TL>::owned(i, j, kg)) {
+            float4* d4 = xr + slot(kg, i, j) + lane * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              d4[q] = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+          }
+      static_assert((TL::MR * TL::NR) % 2 == 0, "K-group ownership halves");
+      static_assert(TL::WM * TL::WN * TL::MR * TL::NR * 64 * 64 <= TL::RS_OFF - TL::BM * (TL::BN / 32) * 8,
+                    "exchange image fits below the tables");
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j)
+          if (DirectGeo<TL>::owned(i, j, kg)) {
+            const float4* s4 = xr + slot(1 - kg, i, j) + lane * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 o = s4[q];
+              acc[i][j][4 * q] += o.x; acc[i][j][4 * q + 1] += o.y; acc[i][j][4 * q + 2] += o.z; acc[i][j][4 * q + 3] += o.w;
+            }
+          }
+    }
+  }
   float* img = (float*)smem;
   const int col = lane & 31;
-  if constexpr (TL::KG > 1) {
+  if constexpr (TL::KG > 1 && !DIRECT) {
     // the other K-groups hand their partial sums to K-group 0 through the image, in a fixed order
     // (img = p1; img += p2; ...; acc0 += img): bitwise reproducible, the same for every tile with
     // the same K-grouping
@@ -815,6 +1070,15 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     }
     if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
     if (tid < TL::BN) cd_tab[tid] = cd_pre;
+  }
+  if constexpr (DIRECT) {
+    if (!p.epi.ln_in && tid < TL::BN) cd_tab[tid] = cd_pre;   // (bias, 0), or zeros without a bias
+    __syncthreads();
+    if (p.epi.ln_in || p.epi.ln_out)
+      epilogue_direct<T, EPI, TL, true>(p, acc, smem, m0, n0, wm, wn, kg, lane, rs_tab, cd_tab, (long)blockIdx.y * p.split_x);
+    else
+      epilogue_direct<T, EPI, TL, false>(p, acc, smem, m0, n0, wm, wn, kg, lane, rs_tab, cd_tab, (long)blockIdx.y * p.split_x);
+    return;
   }
   constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
@@ -1015,41 +1279,51 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
 
 // ---------------------------------------------------------------------------------------------
 // conv1 -> conv2 fused (ConvSubsampling conv.0 + ReLU + conv.2 + ReLU, subsampling.py:105-116, 173):
-// the 8-phase implicit GEMM above with its A operand COMPUTED instead of loaded.  A[m][tap*C + c] =
-// X1[b][t1][f1][c] = ReLU(b1[c] + sum_k W1[c][k] * x[b][2f1-1+e][2t1-1+a]), k = 3a + e, at the conv2 input
-// pixel (t1, f1) = (2t2-1+kt, 2f2-1+kf) of output row m = (b, t2, f2) (zero outside the X1 image), so the
-// 655 MB X1 image of the two-kernel path is never written nor re-read.
-//   * A pre-pass (conv12_patch_kernel) writes every conv2-input pixel's 3x3 input patch (36 B + flag) and
-//     conv1's weights as [k][c] rows; a chunk's weights are wave-uniform, so they come in by scalar loads.
-//   * Wave w computes the A chunks of rows (w>>1)*64 + lane for the 16 channels (w & 1)*16 .. +15 of
-//     every K-half (two 8-channel chunks); each lane keeps the 3x3 input patch of its row for the current
-//     conv2 tap in registers, reloaded when the schedule reaches the next tap (x is L1 / L2 resident).
-//   * Schedule (per K-tile kt, R phases): R_0 chunk 1 of half (kt+1, 0), R_1 / R_2 chunks 0 / 1 of half
-//     (kt+1, 1), R_3 chunk 0 of half (kt+2, 0) - the same slots the DMA version fills, so every write
-//     lands >= 2 barriers after the last read of its region and >= 4 phases before its first read.
-//     The B operand (W2) keeps its LDS-DMA loads (2 per thread per K-half).
-//   * The X1 values are computed with conv1_kernel's exact fma order and rounding, so the output is
-//     bitwise the two-kernel path's (tests/test_gpu_encoder.py).
+// the 8-phase implicit GEMM above (gemm8_kernel) with its A operand COMPUTED on the matrix cores instead
+// of loaded.  A[m][tap*C + c] = X1[b][t1][f1][c] = ReLU(b1[c] + sum_k W1[c][k] * x[b][2f1-1+e][2t1-1+a]),
+// k = 3a + e, at the conv2 input pixel (t1, f1) = (2t2-1+kt, 2f2-1+kf) of output row m = (b, t2, f2)
+// (zero outside the X1 image), so the 655 MB X1 image of the two-kernel path (and conv.2's 2.5x
+// over-fetch of it) is never written nor read.
+//   * conv.0 is itself a K = 16 contraction: [9 taps | in-image flag | 0 x 6] . [W1[c][0..8] | b1[c] | 0].
+//     A pre-pass (conv12_patch_kernel) writes every conv2-input pixel's 16-element fp16 patch (taps
+//     zero-padded as conv.0 pads; all zero on conv.2's padding ring, so X1 = ReLU(0) = 0 there) and W1 as
+//     [c][16] fp16.  The products run on v_mfma_f32_32x32x16_f16 (fp16 operands, fp32 sums; the patch and
+//     W1 in fp16 round to 11 bits, finer than the 8-bit bf16 rounding of X1 that follows).
+//   * Per K-half (32 channels of one tap) wave w computes X1 for tile rows 32w .. 32w+31: ONE MFMA
+//     (W1 rows = channels as the A operand, the patch as B: lane l holds row 32w + (l & 31) and four runs of
+//     4 consecutive channels), ReLU, bf16 pairs regrouped into 16-byte chunks of 8 channels by four
+//     v_permlane32_swap, two ds_write_b128 into the XOR-swizzled A half-image - in the R-phase slots where
+//     gemm8_kernel issues the A half's LDS-DMA, so every write lands >= 2 barriers after the region's last
+//     read and before its first.
+//   * LDS: the 8-phase ring (128 KiB: A images computed, B = W2 by LDS-DMA as before), W1 as [C][16] fp16
+//     (C * 32 B, loaded once per block) and the patch fragments [tap & 1][wave][lane] (2 x 8 KiB).
+//     Wave w's patch rows for tap(kt + 4) are fetched by ONE 1-KiB LDS-DMA per K-tile (R_3, next to the
+//     B half), four K-tiles ahead of their first use; a tap's rows are re-fetched into the same buffer
+//     until the next tap's begin (identical bytes), which keeps the vmcnt counts uniform:
+//     R_1 issues 2 DMAs (B), R_3 issues 3 (B + patch), so "two items younger" is vmcnt(5).
 // ---------------------------------------------------------------------------------------------
 struct Conv12Args {
-  const float4* patch;  // conv12_patch_kernel's (B, T1+2, F1+2) x 12 floats: 3x3 input patch + in-image flag
-  const float* w1t;     // conv.0.weight as [k][c] (k < 9) + conv.0.bias as row 9, fp32
-  const char* zero;     // zero page: B loads past the last K-tile
+  const uint4* patch;   // conv12_patch_kernel: (B, T1+2, F1+2) x 32 B fp16 patches (conv.2's padding ring included)
+  const uint4* w1h;     // conv.0 weight + bias as [c][16] fp16
+  const char* zero;     // zero page
   int T1, F1, T2, F2, C;
 };
+constexpr int C12_MAXC = 512;
 
-// Per conv2-input pixel (b, t1, f1), t1 in [-1, T1], f1 in [-1, F1] (conv2's zero-padding ring
-// included): the 3x3 conv1 input patch x[b][2f1-1+e][2t1-1+a] at [3a + e] (zero where conv1 pads),
-// [9] = 1 inside the X1 image, 0 on the ring; 12 floats (3 x 16 B) per pixel.
 __global__ __launch_bounds__(256) void conv12_patch_kernel(const float* __restrict__ x, int B, int F, int T, int T1,
-                                                           int F1, float4* __restrict__ patch, const float* __restrict__ w1,
-                                                           const float* __restrict__ b1, int C, float* __restrict__ w1t) {
+                                                           int F1, uint4* __restrict__ patch, const float* __restrict__ w1,
+                                                           const float* __restrict__ b1, int C, uint4* __restrict__ w1h) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+  auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, h2{(_Float16)a, (_Float16)b}); };
   const int W = F1 + 2, Hh = T1 + 2;
   const long n = (long)B * Hh * W;
-  if (blockIdx.x == 0)   // conv1 weights as [k][c] rows (+ the bias row): wave-uniform scalar loads in conv12_kernel
-    for (int i = threadIdx.x; i < 10 * C; i += 256) {
-      const int k = i / C, c = i - k * C;
-      w1t[i] = k < 9 ? w1[(long)c * 9 + k] : b1[c];
+  if (blockIdx.x == 0)   // conv.0 weights as [c][16] fp16 rows: W1[c][0..8], b1[c], zeros
+    for (int c = threadIdx.x; c < C; c += 256) {
+      float v[16] = {};
+      for (int k = 0; k < 9; ++k) v[k] = w1[(long)c * 9 + k];
+      v[9] = b1[c];
+      w1h[2 * c] = make_uint4(pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7]));
+      w1h[2 * c + 1] = make_uint4(pk(v[8], v[9]), 0u, 0u, 0u);
     }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const int fi = (int)(i % W);
@@ -1057,7 +1331,7 @@ __global__ __launch_bounds__(256) void conv12_patch_kernel(const float* __restri
     const int ti = (int)(r % Hh), b = (int)(r / Hh);
     const int t1 = ti - 1, f1 = fi - 1;
     const bool ok = t1 >= 0 && t1 < T1 && f1 >= 0 && f1 < F1;
-    float v[12];
+    float v[10];
 #pragma unroll
     for (int a = 0; a < 3; ++a)
 #pragma unroll
@@ -1066,16 +1340,18 @@ __global__ __launch_bounds__(256) void conv12_patch_kernel(const float* __restri
         v[3 * a + e] = (ok && t >= 0 && t < T && f >= 0 && f < F) ? x[((long)b * F + f) * T + t] : 0.0f;
       }
     v[9] = ok ? 1.0f : 0.0f;
-    v[10] = v[11] = 0.0f;
-    patch[3 * i] = make_float4(v[0], v[1], v[2], v[3]);
-    patch[3 * i + 1] = make_float4(v[4], v[5], v[6], v[7]);
-    patch[3 * i + 2] = make_float4(v[8], v[9], v[10], v[11]);
+    patch[2 * i] = make_uint4(pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7]));
+    patch[2 * i + 1] = make_uint4(pk(v[8], v[9]), 0u, 0u, 0u);
   }
 }
-constexpr int C12_MAXC = 1024;
+
+constexpr int C12_PATCH = 2 * 8 * 1024;               // [tap & 1][wave][64 lanes x 16 B]
+constexpr int C12_LDS = 2 * G8_BUF + C12_PATCH + C12_MAXC * 32;
+static_assert(C12_LDS <= 160 * 1024, "conv12 LDS");
 
 __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF];
+  __shared__ __attribute__((aligned(16))) char smem[C12_LDS];
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1087,7 +1363,6 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
   const int m0 = mt * 256, n0 = ntl * 256;
-
 
   // B staging (W2 rows): as gemm8_kernel
   int rows[2], lo[2];
@@ -1102,70 +1377,60 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   const char* zsrc = ca.zero + lane * 16;
   const uint32_t sbase = lds_addr(smem);
   const int nk = p.kb / 128;
+  const int ktap = C / 64;                       // K-tiles per conv.2 tap
 
-  // A computation: this lane's row and its 16-channel group (two 8-channel chunks)
-  const int arow = (wave >> 1) * 64 + lane;
-  const int cgrp = (wave & 1) * 16;
-  const int am = m0 + arow;
+  // this lane's X1 row (tile row 32 * wave + (lane & 31)) and its conv2-input pixel base (ring grid)
+  const int xrow = 32 * wave + (lane & 31);
+  const int am = m0 + xrow;
   const bool arow_ok = am < p.M;
   const int amc = min(am, p.M - 1);
   const int af2 = amc % ca.F2, bt = amc / ca.F2;
   const int at2 = bt % ca.T2, ab = bt / ca.T2;
-  // this row's conv2-input pixel (2t2-1, 2f2-1) = padded-grid entry (2t2, 2f2); a tap adds (kt, kf)
-  const float4* prow = ca.patch + 3 * (((long)ab * (ca.T1 + 2) + 2 * at2) * (ca.F1 + 2) + 2 * af2);
-  float pcur[9];
-  int ptap = 0;
-  bool pok = false;
-  auto load_patch = [&](int tap) {
-    const int kt2 = tap / 3, kf2 = tap - 3 * (tap / 3);
-    const float4* q = prow + 3 * (kt2 * (ca.F1 + 2) + kf2);
-    const float4 u0 = q[0], u1 = q[1], u2 = q[2];
-    pcur[0] = u0.x; pcur[1] = u0.y; pcur[2] = u0.z; pcur[3] = u0.w;
-    pcur[4] = u1.x; pcur[5] = u1.y; pcur[6] = u1.z; pcur[7] = u1.w;
-    pcur[8] = u2.x;
-    pok = arow_ok && u2.y != 0.0f;
-  };
-  load_patch(0);
+  const uint4* prow = ca.patch + 2 * (((long)ab * (ca.T1 + 2) + 2 * at2) * (ca.F1 + 2) + 2 * af2) + (lane >> 5);
+  const uint32_t pbase = sbase + 2 * G8_BUF;     // patch fragments
+  const char* w1img = smem + 2 * G8_BUF + C12_PATCH;
 
-  // K-half (kt, h): K elements [kt*64 + 32h, +32) = tap (kt*64 + 32h) / C, channels c0 .. c0+31
-  auto compute_chunk = [&](int kt, int h, int j) {
-    __builtin_amdgcn_sched_barrier(0);   // keep the chunk's arithmetic inside its R phase
-    const int kel = kt * 64 + 32 * h;
-    const int c0 = kel - ptap * C + cgrp + 8 * j;   // this chunk's first channel (C % 64 == 0: one tap per K-tile)
-    // the chunk's 8 channels are the same for every lane of the wave: weights by scalar loads (SGPRs)
-    typedef const __attribute__((address_space(4))) f32x4 cfloat4;   // constant address space: s_load_dwordx4
-    cfloat4* wk = (cfloat4*)(ca.w1t + __builtin_amdgcn_readfirstlane(c0));   // c0 % 8 == 0: 32-byte aligned
-    const int C4 = C / 4;
-    uint32_t packed[4];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {   // 4 channels at a time
-      float acc4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const f32x4 w = wk[k * C4 + half];
-        acc4[0] = fmaf(w[0], pcur[k], acc4[0]); acc4[1] = fmaf(w[1], pcur[k], acc4[1]);
-        acc4[2] = fmaf(w[2], pcur[k], acc4[2]); acc4[3] = fmaf(w[3], pcur[k], acc4[3]);
-      }
-      const f32x4 bv = wk[9 * C4 + half];
-      const bool live = pok && kt < nk;
-      const float o0 = live ? fmaxf(acc4[0] + bv[0], 0.0f) : 0.0f, o1 = live ? fmaxf(acc4[1] + bv[1], 0.0f) : 0.0f;
-      const float o2 = live ? fmaxf(acc4[2] + bv[2], 0.0f) : 0.0f, o3 = live ? fmaxf(acc4[3] + bv[3], 0.0f) : 0.0f;
-      packed[2 * half] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
-      packed[2 * half + 1] = (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16);
-    }
-    // 16-byte slot (cgrp / 8 + j) of row arow in the K-half image, XOR-swizzled as the DMA fills it
-    char* img = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
-    const int slot = (cgrp / 8 + j) ^ g8_swz(arow);
-    *(uint4*)(img + arow * 64 + slot * 16) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
-    __builtin_amdgcn_sched_barrier(0);
+  // LDS-DMA of this wave's patch rows for conv.2 tap `tap` (clamped) into buffer tap & 1
+  auto issue_patch = [&](int tap) {
+    tap = min(tap, 8);
+    const int kt2 = tap / 3, kf2 = tap - 3 * kt2;
+    const void* src = arow_ok ? (const void*)(prow + 2 * (kt2 * (ca.F1 + 2) + kf2)) : (const void*)zsrc;
+    glds16_asm(src, pbase + (tap & 1) * 8192 + wave * 1024);
   };
-  auto issue_b = [&](int kt, int h) {   // K-half h of K-tile kt of W2: 2 glds
+  auto issue_b = [&](int kt, int h) {   // K-half h of K-tile kt of W2: 2 LDS-DMA
     const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
     const bool live = kt < nk;
     const int kb0 = kt * 128 + h * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
   };
+  // X1 for K-half (kt, h): 32 channels of tap kt / ktap, rows 32 * wave + (lane & 31)
+  auto compute_x1 = [&](int kt, int h) {
+    if (kt >= nk) return;
+    __builtin_amdgcn_sched_barrier(0);
+    const int tap = kt / ktap;
+    const int c0 = (kt - tap * ktap) * 64 + 32 * h;
+    const uint4 wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
+    const uint4 pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+    const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
+                                                            f32x16{}, 0, 0, 0);
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = fmaxf(d[q], 0.0f);
+    uint4 c0v, c1v;
+    pack_chunks16(v, c0v, c1v);   // lanes < 32: channels 0-7 / 16-23, lanes >= 32: 8-15 / 24-31
+    char* img = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const int hi = lane >> 5, sw = g8_swz(xrow);
+    *(uint4*)(img + xrow * 64 + ((hi) ^ sw) * 16) = c0v;
+    *(uint4*)(img + xrow * 64 + ((2 + hi) ^ sw) * 16) = c1v;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // conv.0's weights into LDS (C x 32 B), once per block, before any LDS-DMA is in flight (plain loads:
+  // hipcc waits for them here); visible to every wave after the raw barrier
+  for (int i = tid; i < 2 * C; i += 512) ((uint4*)w1img)[i] = ca.w1h[i];
+  wait_lgkm0();
+  raw_barrier();
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1188,14 +1453,18 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
     }
   };
 
-  // prologue: halves (0,0), (0,1), (1,0) of A computed, of B loaded
+  // prologue: tap 0's patch, B halves (0,0), (0,1), (1,0) (+ the patch of tap(4), as R_3 does), then the
+  // A halves (0,0), (0,1), (1,0) computed
+  issue_patch(0);
   issue_b(0, 0);
   issue_b(0, 1);
   issue_b(1, 0);
-  compute_chunk(0, 0, 0); compute_chunk(0, 0, 1);
-  compute_chunk(0, 1, 0); compute_chunk(0, 1, 1);
-  compute_chunk(1, 0, 0);
-  wait_vmcnt<4>();
+  issue_patch(4 / ktap);
+  wait_vmcnt<7>();            // tap 0's patch has landed (this wave's own rows: no barrier needed)
+  compute_x1(0, 0);
+  compute_x1(0, 1);
+  compute_x1(1, 0);
+  wait_vmcnt<5>();            // B (0,0) complete; (0,1) and (1,0) + patch in flight
   wait_lgkm0();
   raw_barrier();
   if (wm == 1) raw_barrier();
@@ -1204,18 +1473,9 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
     for (int q = 0; q < 4; ++q) {
       // R_q
       read_frags(kt, q);
-      if (q == 0) compute_chunk(kt + 1, 0, 1);
-      if (q == 1) { issue_b(kt + 1, 1); compute_chunk(kt + 1, 1, 0); }
-      if (q == 2) compute_chunk(kt + 1, 1, 1);
-      if (q == 3) {
-        issue_b(kt + 2, 0);
-        if (((kt + 2) * 64) % C == 0) {   // K-tile kt+2 starts the next conv2 tap: its input patch
-          ptap = (kt + 2) * 64 / C;
-          if (ptap < 9) load_patch(ptap);
-        }
-        compute_chunk(kt + 2, 0, 0);
-      }
-      if (wm == 1 && (q & 1)) wait_vmcnt<4>();
+      if (q == 1) { issue_b(kt + 1, 1); compute_x1(kt + 1, 1); }
+      if (q == 3) { issue_b(kt + 2, 0); issue_patch((kt + 4) / ktap); compute_x1(kt + 2, 0); }
+      if (wm == 1 && (q & 1)) wait_vmcnt<5>();   // before the barrier preceding row 0's R_{q+1}
       raw_barrier();
       // M_q
       wait_lgkm0();
@@ -1226,11 +1486,11 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
         for (int j = 0; j < 4; ++j)
           acc[(q & 1) * 4 + i][j] = mfma16_16x16x32(af[i], bfr[j], acc[(q & 1) * 4 + i][j]);
       __builtin_amdgcn_s_setprio(0);
-      if (wm == 0 && (q & 1)) wait_vmcnt<4>();
+      if (wm == 0 && (q & 1)) wait_vmcnt<5>();
       raw_barrier();
     }
   }
-  if (wm == 0) raw_barrier();
+  if (wm == 0) raw_barrier();   // re-align the barrier counts of the two wave rows
   wait_vmcnt<0>();
   wait_lgkm0();
   raw_barrier();
@@ -1256,6 +1516,35 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   }
 }
 
+// the direct (register) epilogue (CFM_GEMM_DIRECT=0: the LDS-image epilogue, A/B measurements)
+int g_gemm_direct = [] { const char* s = getenv("CFM_GEMM_DIRECT"); return s ? atoi(s) : 0; }();
+
+// Tiles the direct epilogue is instantiated for: bf16, one or two K-groups, whole LayerNorm granules.
+template <class TL> constexpr bool direct_tile() {
+  // only the tiles pick_tile chooses for these epilogues (compile time)
+  constexpr bool used = std::is_same<TL, T256x256w>::value || std::is_same<TL, T128x128k4>::value ||
+                        std::is_same<TL, T64x128k>::value || std::is_same<TL, T128x128k>::value ||
+                        std::is_same<TL, T64x128s2>::value;
+  return used && (TL::KG == 1 || (TL::KG == 2 && (TL::MR * TL::NR) % 2 == 0 &&
+                          TL::WM * TL::WN * TL::MR * TL::NR * 64 * 64 <= TL::RS_OFF - TL::BM * (TL::BN / 32) * 8)) &&
+         TL::BN % LN_GRANULE == 0 && TL::BM * (TL::BN / 32) * 8 <= TL::RS_OFF;
+}
+// Shapes / epilogues the direct path covers (everything else keeps the LDS-image epilogue).
+bool direct_ok(const GemmParams& p, int es) {
+  const GemmEpi& e = p.epi;
+  if (!g_gemm_direct || es != 2 || e.out_scalar || e.utt_tp > 0) return false;
+  switch (e.mode) {
+    case EPI_STORE: case EPI_RELU: case EPI_SWISH:
+      return (e.ldc * 2) % 16 == 0 && ((uintptr_t)e.C % 16) == 0;
+    case EPI_RESID: case EPI_SCALE_F32:
+      if (e.ldx % 4 || p.N % 4 || ((uintptr_t)e.X % 16)) return false;
+      if (e.mode == EPI_RESID && e.Xin && ((uintptr_t)e.Xin % 16)) return false;
+      if (e.ln_out && (e.ldx % 8 || p.N % 8 || ((uintptr_t)e.xb % 16))) return false;
+      return true;
+    default: return false;
+  }
+}
+
 template <typename T, class TL, template <int> class AL, class ALArgs>
 void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   using ALoad = AL<TL::GA>;
@@ -1265,6 +1554,18 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   if constexpr (ALoad::kConv) {
     cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al);
     return;
+  }
+  if constexpr (!ALoad::kConv && std::is_same<T, bf16_t>::value && direct_tile<TL>()) {
+    if (direct_ok(p, 2)) {
+      switch (p.epi.mode) {
+        case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_RELU: cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_SWISH: cfm_launch((gemm_kernel<T, EPI_SWISH, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_RESID: cfm_launch((gemm_kernel<T, EPI_RESID, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_SCALE_F32: cfm_launch((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        default: break;
+      }
+    }
   }
   switch (p.epi.mode) {
     case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
@@ -1539,25 +1840,26 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
 }
 
 bool conv12_supported(int dtype, int C) {
-  return dtype == DT_BF16 && C > 0 && C <= C12_MAXC && C % 128 == 0 && g_tile_override < 0;
+  return dtype == DT_BF16 && C >= 256 && C <= C12_MAXC && C % 64 == 0 && g_tile_override < 0;
 }
 
 size_t conv12_patch_bytes(int B, int T1, int F1, int C) {
-  return (size_t)B * (T1 + 2) * (F1 + 2) * 48 + 256 + (size_t)10 * C * 4;
+  return (size_t)B * (T1 + 2) * (F1 + 2) * 32 + 256 + (size_t)C * 32;
 }
 
 // conv.0 + ReLU + conv.2 + ReLU: x (B, F, T) fp32 -> X2 (B, T2, F2, C) bf16; `patch` is scratch of
-// conv12_patch_bytes(B, T1, F1) bytes
+// conv12_patch_bytes(B, T1, F1, C) bytes
 void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T2, int F2, const float* w1,
                   const float* b1, int C, const void* Wp, int Kpad, const float* b2, void* X2, void* patch,
                   const void* zero_page, hipStream_t st) {
   const int M = B * T2 * F2;
   if (M <= 0) return;
-  if (!conv12_supported(DT_BF16, C)) fail(CFM_ERR_UNSUPPORTED, "conv12_fused: bf16, C % 128 == 0, C <= 1024");
+  if (!conv12_supported(DT_BF16, C)) fail(CFM_ERR_UNSUPPORTED, "conv12_fused: 16-bit, C % 64 == 0, 256 <= C <= 512");
+  if ((long)Kpad != 9L * C) fail(CFM_ERR_UNSUPPORTED, "conv12_fused: conv.2 weight K must be 9 * C");
   const long npix = (long)B * (T1 + 2) * (F1 + 2);
-  float* w1t = (float*)((char*)patch + ((npix * 48 + 255) / 256) * 256);
+  uint4* w1h = (uint4*)((char*)patch + ((npix * 32 + 255) / 256) * 256);
   cfm_launch(conv12_patch_kernel, dim3((unsigned)std::min<long>((npix + 255) / 256, 4096)), dim3(256), 0, st, x_bft, B,
-             F, T, T1, F1, (float4*)patch, w1, b1, C, w1t);
+             F, T, T1, F1, (uint4*)patch, w1, b1, C, w1h);
   GemmEpi e;
   std::memset(&e, 0, sizeof(e));
   e.mode = EPI_RELU;
@@ -1569,7 +1871,7 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   p.probe = 0;
   p.Mtiles = (M + 255) / 256;
   p.Ntiles = (C + 255) / 256;
-  Conv12Args a{(const float4*)patch, w1t, (const char*)zero_page, T1, F1, T2, F2, C};
+  Conv12Args a{(const uint4*)patch, w1h, (const char*)zero_page, T1, F1, T2, F2, C};
   cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
 }
 
