@@ -61,7 +61,7 @@ struct cfm_encoder {
   // conv.0 recomputed inside conv.2 (conv12_fused) - off by default: bitwise equal to the two-kernel path but
   // 5.60 against 4.96 ms per forward (its 9 fp32 FMAs per X1 value overflow the MFMA ping-pong's VALU slots,
   // DESIGN.md section 4); env CFM_CONV12=1 turns it on
-  bool fuse_conv12 = false;
+  bool fuse_conv12 = true;     // conv.0 on the matrix cores inside conv.2's implicit GEMM (CFM_CONV12=0: two kernels)
   // bf16 eval forward with the LayerNorm fold, dkp = 64, T' <= 256: each head's q | k | v projection
   // and its attention in one launch (qkv_rel_attention_fused); CFM_QKV_ATTN=0 keeps the QKV GEMM +
   // attention pair (A/B)

@@ -61,8 +61,9 @@ struct Tile {
   static constexpr int CD_OFF = RS_OFF + BM * 8;
   static constexpr int LDS_BYTES = CD_OFF + BN * 8;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
-  static_assert(BKB == 64 || BKB == 128, "stage depth");
-  static_assert(GEMM_BK_BYTES % BKB == 0, "packed K granule");
+  static_assert(BKB == 64 || BKB == 128 || BKB == 256, "stage depth");
+  // 256-byte K-steps run only where the host checked p.kb % 256 == 0 (dispatch)
+  static_assert(GEMM_BK_BYTES % BKB == 0 || BKB == 256, "packed K granule");
   static_assert(WM % EP == 0, "epilogue passes split the wave rows");
   static_assert(KG == 1 || (EP == 1 && (BKB / 32) % KG == 0), "K-groups");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -89,6 +90,8 @@ using T128x128k4 = Tile<128, 128, 2, 2, 4, 1, 128, 2>; // as above, 4 x 32 KiB
 using T128x256k = Tile<128, 256, 2, 2, 3, 1, 128, 2>;  // 8 waves = 2 K-groups x 4, 3 x 48 KiB, wave tile 64 x 128
 using T64x128k = Tile<64, 128, 2, 2, 3, 1, 128, 2>;    // 8 waves = 2 K-groups x 4, 3 x 24 KiB, wave tile 32 x 64
 using T128x128q = Tile<128, 128, 2, 2, 4, 1, 128, 4>;  // 16 waves = 4 K-groups x 4, 4 x 32 KiB, wave tile 64 x 64
+using T128x128w = Tile<128, 128, 2, 2, 2, 1, 256, 2>;  // 8 waves = 2 K-groups x 4, 2 x 64 KiB of 256-byte K-steps:
+                                                       // 16 MFMAs per wave between barriers (K % 128 == 0 only)
 
 // LDS-DMA (glds16_asm) and counted waits: cfm_common.h
 // wait until at most `ahead` stages of G loads each are still in flight (ahead in [0, MAXA])
@@ -640,23 +643,9 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
   }
 }
 
-// ---- direct epilogue: accumulators -> global from registers (no LDS image, no passes) ----------
-// With DIRECT the main loop multiplies W-fragments by A-fragments (C^T per 32x32 block), so lane l of
-// a block holds token m = (l & 31) and the 16 channels acc_row(r, l) = (r & 3) + 8 (r >> 2) + 4 (l >> 5):
-// four runs of 4 consecutive channels.  fp32 outputs (EPI_RESID, EPI_SCALE_F32) go out as one float4
-// per run; compute-type outputs are packed to bf16 pairs and regrouped by four v_permlane32_swap into
-// two 16-byte chunks of 8 consecutive channels per lane (lanes < 32: channels 0-7 / 16-23 of the block,
-// lanes >= 32: 8-15 / 24-31).  Every wave stores its own blocks as soon as they are final: no image
-// write, no barrier between passes, all waves storing at once.
-// K-groups (KG = 2): group g finalises the blocks with (i * NR + j) % 2 == g (ownership by block), the
-// other group's partial sums come through LDS once (owner + partner: the same fp32 sum as the image path).
-template <class TL> struct DirectGeo {
-  static constexpr int WTM = TL::BM / TL::WM, WTN = TL::BN / TL::WN;   // wave tile
-  static constexpr int XB = TL::MR * TL::NR * 64 * 64;                  // exchange bytes per wave (all blocks)
-  static CFM_DEV bool owned(int i, int j, int kg) { return TL::KG == 1 || ((i * TL::NR + j) % TL::KG) == kg; }
-};
-
-// bf16 pairs of 16 accumulator values (4 runs of 4 channels) -> two 16-byte chunks of 8 channels
+// 16 values of a C^T 32x32 MFMA block (lane l: column (l & 31), rows acc_row(r, l) = four runs of 4) ->
+// compute-type pairs regrouped by four v_permlane32_swap into two 16-byte chunks of 8 consecutive rows:
+// lanes < 32 hold rows 0-7 / 16-23, lanes >= 32 rows 8-15 / 24-31 (conv12_kernel's computed A operand)
 CFM_DEV void pack_chunks16(const float* v, uint4& c0, uint4& c1) {
   uint32_t d[8];
 #pragma unroll
@@ -669,163 +658,7 @@ CFM_DEV void pack_chunks16(const float* v, uint4& c0, uint4& c1) {
   c1 = make_uint4(s2[0], s3[0], s2[1], s3[1]);
 }
 
-template <typename T, int EPI, class TL, bool FOLD>
-CFM_DEV void epilogue_direct(const GemmParams& p, f32x16 (&acc)[TL::MR][TL::NR], char* smem, int m0, int n0,
-                             int wm, int wn, int kg, int lane, const float2* rs, const float2* cd, long xoff) {
-  using G = DirectGeo<TL>;
-  const GemmEpi& e = p.epi;
-  const int hi = lane >> 5;
-  constexpr bool kF32 = EPI == EPI_RESID || EPI == EPI_SCALE_F32;
-  constexpr bool kStats = EPI == EPI_RESID && FOLD;           // LayerNorm-fold producer
-  constexpr int NBJ = TL::BN / 32;                              // 32-column blocks per tile row
-  // per (token, 32-column block) (mean, M2) partials of the producer, combined per 128-column granule
-  float2* st_tab = (float2*)(smem + TL::RS_OFF - TL::BM * NBJ * 8);
-#pragma unroll
-  for (int i = 0; i < TL::MR; ++i) {
-    const int tl = wm * G::WTM + i * 32 + (lane & 31);        // tile-local token
-    const int m = m0 + tl;
-    const int mc = min(m, p.M - 1);
-    float2 rsv = make_float2(0.0f, 1.0f);
-    if constexpr (FOLD && !kStats) rsv = rs[tl];
-#pragma unroll
-    for (int j = 0; j < TL::NR; ++j) {
-      if (!G::owned(i, j, kg)) continue;
-      const int cl = wn * G::WTN + j * 32;                      // tile-local first channel of the block
-      float v[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c4 = cl + 8 * g + 4 * hi;                     // this lane's run of 4 channels
-        const float4 bb = *(const float4*)(cd + c4) ;           // (c, d) or (bias, 0) of 2 channels...
-        const float4 bb2 = *(const float4*)(cd + c4 + 2);
-        const float2 t[4] = {make_float2(bb.x, bb.y), make_float2(bb.z, bb.w), make_float2(bb2.x, bb2.y),
-                             make_float2(bb2.z, bb2.w)};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float a = acc[i][j][4 * g + q];
-          float x;
-          if constexpr (FOLD && !kStats) x = rsv.y * (a - rsv.x * t[q].x) + t[q].y;
-          else x = a + t[q].x;
-          if constexpr (EPI == EPI_RELU) x = fmaxf(x, 0.0f);
-          if constexpr (EPI == EPI_SWISH) x = swishf(x);
-          v[4 * g + q] = x;
-        }
-      }
-      if constexpr (kF32) {
-        float o[16];
-        if constexpr (EPI == EPI_RESID) {
-          const float* XI = e.Xin ? e.Xin : e.X;
-          float4 xv[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n = min(n0 + cl + 8 * g + 4 * hi, p.N - 4);
-            xv[g] = *(const float4*)(XI + xoff + (long)mc * e.ldx + n);
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float xs[4] = {xv[g].x, xv[g].y, xv[g].z, xv[g].w};
-            const uint64_t i0 = (uint64_t)m * e.ldx + (n0 + cl + 8 * g + 4 * hi);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              o[4 * g + q] = e.drop.thr ? xs[q] + (e.alpha * v[4 * g + q]) * drop_mul(e.drop, i0 + q)
-                                        : xs[q] + v[4 * g + q] * e.alpha;
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) o[q] = v[q] * e.alpha;
-        }
-        if (m < p.M) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n = n0 + cl + 8 * g + 4 * hi;
-            if (n < p.N) {
-              const long off = xoff + (long)m * e.ldx + n;
-              const uint4 u = make_uint4(__float_as_uint(o[4 * g]), __float_as_uint(o[4 * g + 1]),
-                                         __float_as_uint(o[4 * g + 2]), __float_as_uint(o[4 * g + 3]));
-              if (e.wt) store16_wt(e.X, off * 4, u);
-              else *(uint4*)(e.X + off) = u;
-            }
-          }
-        }
-        if constexpr (kStats) {
-          // the compute-type copy of the new rows (the folded consumer's A operand) ...
-          uint4 c0, c1;
-          pack_chunks16(o, c0, c1);
-          const int nb = n0 + cl + 8 * hi;
-          if (m < p.M) {
-            if (nb < p.N) *(uint4*)((T*)e.xb + (long)m * e.ldx + nb) = c0;
-            if (nb + 16 < p.N) *(uint4*)((T*)e.xb + (long)m * e.ldx + nb + 16) = c1;
-          }
-          // ... and this token's (mean, M2) over the block's valid channels (two passes, no cancellation)
-          const int nv = max(0, min(32, p.N - (n0 + cl)));
-          float sm = 0.0f;
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sm += (cl + 8 * g + 4 * hi + q < cl + nv) ? o[4 * g + q] : 0.0f;
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(sm), __float_as_uint(sm), false, false);
-          const float mean = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) / (float)max(nv, 1);
-          float q2 = 0.0f;
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float dv = o[4 * g + q] - mean;
-              q2 += (cl + 8 * g + 4 * hi + q < cl + nv) ? dv * dv : 0.0f;
-            }
-          const auto sq = __builtin_amdgcn_permlane32_swap(__float_as_uint(q2), __float_as_uint(q2), false, false);
-          if (hi == 0) st_tab[tl * NBJ + cl / 32] = make_float2(mean, __uint_as_float(sq[0]) + __uint_as_float(sq[1]));
-        }
-      } else {
-        uint4 c0, c1;
-        pack_chunks16(v, c0, c1);
-        const int nb = n0 + cl + 8 * hi;
-        if (m < p.M) {
-          T* row = (T*)e.C + (long)m * e.ldc;
-          const uint4 cs[2] = {c0, c1};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int n = nb + 16 * h;
-            if (n + 8 <= p.N) {
-              if (e.wt) store16_wt(e.C, ((long)m * e.ldc + n) * (long)sizeof(T), cs[h]);
-              else *(uint4*)(row + n) = cs[h];
-            } else if (n < p.N) {
-              const uint32_t w[4] = {cs[h].x, cs[h].y, cs[h].z, cs[h].w};
-              for (int q = 0; q < 8 && n + q < p.N; ++q) row[n + q] = (T)(q & 1 ? w[q >> 1] >> 16 : w[q >> 1] & 0xffffu);
-            }
-          }
-        }
-      }
-    }
-  }
-  if constexpr (kStats) {
-    // per 128-column granule: Chan's combination of the four 32-column block partials, one thread
-    // per (token, granule) of the tile
-    __syncthreads();
-    constexpr int GPT = TL::BN / LN_GRANULE;
-    static_assert(TL::BN % LN_GRANULE == 0, "tile width: whole LayerNorm granules");
-    for (int t = threadIdx.x; t < TL::BM * GPT; t += TL::NT) {
-      const int tl = t / GPT, gl = t - tl * GPT;
-      const int m = m0 + tl;
-      const int g = n0 / LN_GRANULE + gl;
-      const int cnt = min(LN_GRANULE, p.N - g * LN_GRANULE);
-      if (m >= p.M || cnt <= 0) continue;
-      float n_a = 0.0f, mean = 0.0f, m2 = 0.0f;
-#pragma unroll
-      for (int b = 0; b < LN_GRANULE / 32; ++b) {
-        const float n_b = (float)max(0, min(32, cnt - 32 * b));
-        if (n_b <= 0.0f) continue;
-        const float2 pb = st_tab[tl * NBJ + gl * (LN_GRANULE / 32) + b];
-        const float n = n_a + n_b, dm = pb.x - mean;
-        mean += dm * (n_b / n);
-        m2 += pb.y + dm * dm * (n_a * n_b / n);
-        n_a = n;
-      }
-      e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, m2);
-    }
-  }
-}
-
-template <typename T, int EPI, class TL, class ALoad, bool DIRECT = false>
+template <typename T, int EPI, class TL, class ALoad>
 __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload) {
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -872,8 +705,6 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
     const int nc = n0 + min(tid, TL::BN - 1);
     cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
-  } else if (DIRECT && p.epi.bias) {   // the direct epilogue reads the bias from the same LDS table
-    cd_pre = make_float2(p.epi.bias[n0 + min(tid, TL::BN - 1)], 0.0f);
   }
 
   auto stage = [&](int kt, int slot) {
@@ -939,10 +770,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < TL::NR; ++j) {
-          if constexpr (DIRECT) mfma_slab<T>(acc[i][j], bfc[j], afc[i]);   // C^T blocks: lane = token
-          else mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
-        }
+        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
 #pragma unroll
       for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
 #pragma unroll
@@ -963,47 +791,9 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   // ---- epilogue through LDS, BM/EP rows per pass ----
   wait_lgkm0();
   raw_barrier();                         // every wave is done reading the ring
-  if constexpr (DIRECT) {
-    if constexpr (TL::KG > 1) {
-      // the blocks this wave does not finalise go to their owner group once: slot [block][lane][16]
-      // of this wave's region (lane-linear 16-byte accesses: conflict-free)
-      static_assert(TL::KG == 2, "direct epilogue: two K-groups");
-      float4* xr = (float4*)smem;
-      constexpr int WG = TL::WM * TL::WN;                      // waves per K-group
-      const int wq = wave % WG;
-      // block b = i * NR + j is owned by group b % 2: each group hands over the other half, b / 2 indexes it
-      auto slot = [&](int g, int i, int j) { return ((g * WG + wq) * (TL::MR * TL::NR / 2) + (i * TL::NR + j) / 2) * 64 * 4; };
-#pragma unroll
-      for (int i = 0; i < TL::MR; ++i)
-#pragma unroll
-        for (int j = 0; j < TL::NR; ++j)
-          if (!DirectGeo<TL>::owned(i, j, kg)) {
-            float4* d4 = xr + slot(kg, i, j) + lane * 4;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              d4[q] = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
-          }
-      static_assert((TL::MR * TL::NR) % 2 == 0, "K-group ownership halves");
-      static_assert(TL::WM * TL::WN * TL::MR * TL::NR * 64 * 64 <= TL::RS_OFF - TL::BM * (TL::BN / 32) * 8,
-                    "exchange image fits below the tables");
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < TL::MR; ++i)
-#pragma unroll
-        for (int j = 0; j < TL::NR; ++j)
-          if (DirectGeo<TL>::owned(i, j, kg)) {
-            const float4* s4 = xr + slot(1 - kg, i, j) + lane * 4;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float4 o = s4[q];
-              acc[i][j][4 * q] += o.x; acc[i][j][4 * q + 1] += o.y; acc[i][j][4 * q + 2] += o.z; acc[i][j][4 * q + 3] += o.w;
-            }
-          }
-    }
-  }
   float* img = (float*)smem;
   const int col = lane & 31;
-  if constexpr (TL::KG > 1 && !DIRECT) {
+  if constexpr (TL::KG > 1) {
     // the other K-groups hand their partial sums to K-group 0 through the image, in a fixed order
     // (img = p1; img += p2; ...; acc0 += img): bitwise reproducible, the same for every tile with
     // the same K-grouping
@@ -1070,15 +860,6 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     }
     if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
     if (tid < TL::BN) cd_tab[tid] = cd_pre;
-  }
-  if constexpr (DIRECT) {
-    if (!p.epi.ln_in && tid < TL::BN) cd_tab[tid] = cd_pre;   // (bias, 0), or zeros without a bias
-    __syncthreads();
-    if (p.epi.ln_in || p.epi.ln_out)
-      epilogue_direct<T, EPI, TL, true>(p, acc, smem, m0, n0, wm, wn, kg, lane, rs_tab, cd_tab, (long)blockIdx.y * p.split_x);
-    else
-      epilogue_direct<T, EPI, TL, false>(p, acc, smem, m0, n0, wm, wn, kg, lane, rs_tab, cd_tab, (long)blockIdx.y * p.split_x);
-    return;
   }
   constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
@@ -1350,6 +1131,7 @@ constexpr int C12_LDS = 2 * G8_BUF + C12_PATCH + C12_MAXC * 32;
 static_assert(C12_LDS <= 160 * 1024, "conv12 LDS");
 
 __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca) {
+  auto c12_xcd_cols = [&] { return (p.probe & 8) != 0; };
   __shared__ __attribute__((aligned(16))) char smem[C12_LDS];
   typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1357,11 +1139,21 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   const int wm = wave >> 2, wn = wave & 3;
   const int C = ca.C;
 
+  // Block -> tile: with two 256-column tiles (C = 512) the XCDs of one parity take one column tile, so each
+  // XCD's L2 holds half of W2 (2.4 MB) instead of all of it; otherwise gemm8_kernel's contiguous ranges.
   const int nblocks = p.Mtiles * p.Ntiles;
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
+  int mt, ntl;
+  if (p.Ntiles == 2 && c12_xcd_cols()) {
+    const int full = nblocks >> 3;
+    if (bid < 8 * full) { mt = (bid >> 3) * 4 + ((bid & 7) >> 1); ntl = bid & 1; }
+    else { const int t = bid - 8 * full; mt = 4 * full + (t >> 1); ntl = t & 1; }
+  } else {
+    const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    mt = wg / p.Ntiles;
+    ntl = wg - mt * p.Ntiles;
+  }
   const int m0 = mt * 256, n0 = ntl * 256;
 
   // B staging (W2 rows): as gemm8_kernel
@@ -1404,27 +1196,39 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
 #pragma unroll
     for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
   };
-  // X1 for K-half (kt, h): 32 channels of tap kt / ktap, rows 32 * wave + (lane & 31)
-  auto compute_x1 = [&](int kt, int h) {
-    if (kt >= nk) return;
-    __builtin_amdgcn_sched_barrier(0);
+  // X1 for K-half (kt, h): 32 channels of tap kt / ktap, rows 32 * wave + (lane & 31).  Two halves so
+  // that the MFMA's latency is not waited for inside one R phase: x1_mfma issues the contraction, one
+  // phase later x1_store converts (bf16 pairs, ReLU as a packed int16 max on the bf16 bits: negative
+  // values have the sign bit set, so max(x, 0) as int16 is max(x, +0) as bf16), regroups and writes.
+  auto x1_mfma = [&](int kt, int h) -> f32x16 {
+    if (kt >= nk) return f32x16{};
     const int tap = kt / ktap;
     const int c0 = (kt - tap * ktap) * 64 + 32 * h;
     const uint4 wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
     const uint4 pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
-    const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
-                                                            f32x16{}, 0, 0, 0);
-    float v[16];
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
+                                                 f32x16{}, 0, 0, 0);
+  };
+  auto x1_store = [&](int kt, int h, const f32x16& d) {
+    if (kt >= nk) return;
+    typedef __attribute__((ext_vector_type(2))) short s16x2;
+    uint32_t q[8];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = fmaxf(d[q], 0.0f);
-    uint4 c0v, c1v;
-    pack_chunks16(v, c0v, c1v);   // lanes < 32: channels 0-7 / 16-23, lanes >= 32: 8-15 / 24-31
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t u = (uint32_t)f2bf(d[2 * i]) | ((uint32_t)f2bf(d[2 * i + 1]) << 16);
+      q[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
+    }
+    const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(q[4], q[6], false, false);
+    const auto s3 = __builtin_amdgcn_permlane32_swap(q[5], q[7], false, false);
     char* img = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
     const int hi = lane >> 5, sw = g8_swz(xrow);
-    *(uint4*)(img + xrow * 64 + ((hi) ^ sw) * 16) = c0v;
-    *(uint4*)(img + xrow * 64 + ((2 + hi) ^ sw) * 16) = c1v;
-    __builtin_amdgcn_sched_barrier(0);
+    // lanes < 32: channels 0-7 / 16-23 of the K-half, lanes >= 32: 8-15 / 24-31
+    *(uint4*)(img + xrow * 64 + ((hi) ^ sw) * 16) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    *(uint4*)(img + xrow * 64 + ((2 + hi) ^ sw) * 16) = make_uint4(s2[0], s3[0], s2[1], s3[1]);
   };
+  auto compute_x1 = [&](int kt, int h) { x1_store(kt, h, x1_mfma(kt, h)); };
 
   // conv.0's weights into LDS (C x 32 B), once per block, before any LDS-DMA is in flight (plain loads:
   // hipcc waits for them here); visible to every wave after the raw barrier
@@ -1468,13 +1272,17 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   wait_lgkm0();
   raw_barrier();
   if (wm == 1) raw_barrier();
+  f32x16 xd;
   for (int kt = 0; kt < nk; ++kt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       // R_q
       read_frags(kt, q);
-      if (q == 1) { issue_b(kt + 1, 1); compute_x1(kt + 1, 1); }
-      if (q == 3) { issue_b(kt + 2, 0); issue_patch((kt + 4) / ktap); compute_x1(kt + 2, 0); }
+      // the A halves the DMA version loads at R_1 / R_3: contraction issued one phase earlier
+      if (q == 0) xd = x1_mfma(kt + 1, 1);
+      if (q == 1) { issue_b(kt + 1, 1); x1_store(kt + 1, 1, xd); }
+      if (q == 2) xd = x1_mfma(kt + 2, 0);
+      if (q == 3) { issue_b(kt + 2, 0); issue_patch((kt + 4) / ktap); x1_store(kt + 2, 0, xd); }
       if (wm == 1 && (q & 1)) wait_vmcnt<5>();   // before the barrier preceding row 0's R_{q+1}
       raw_barrier();
       // M_q
@@ -1516,35 +1324,6 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   }
 }
 
-// the direct (register) epilogue (CFM_GEMM_DIRECT=0: the LDS-image epilogue, A/B measurements)
-int g_gemm_direct = [] { const char* s = getenv("CFM_GEMM_DIRECT"); return s ? atoi(s) : 0; }();
-
-// Tiles the direct epilogue is instantiated for: bf16, one or two K-groups, whole LayerNorm granules.
-template <class TL> constexpr bool direct_tile() {
-  // only the tiles pick_tile chooses for these epilogues (compile time)
-  constexpr bool used = std::is_same<TL, T256x256w>::value || std::is_same<TL, T128x128k4>::value ||
-                        std::is_same<TL, T64x128k>::value || std::is_same<TL, T128x128k>::value ||
-                        std::is_same<TL, T64x128s2>::value;
-  return used && (TL::KG == 1 || (TL::KG == 2 && (TL::MR * TL::NR) % 2 == 0 &&
-                          TL::WM * TL::WN * TL::MR * TL::NR * 64 * 64 <= TL::RS_OFF - TL::BM * (TL::BN / 32) * 8)) &&
-         TL::BN % LN_GRANULE == 0 && TL::BM * (TL::BN / 32) * 8 <= TL::RS_OFF;
-}
-// Shapes / epilogues the direct path covers (everything else keeps the LDS-image epilogue).
-bool direct_ok(const GemmParams& p, int es) {
-  const GemmEpi& e = p.epi;
-  if (!g_gemm_direct || es != 2 || e.out_scalar || e.utt_tp > 0) return false;
-  switch (e.mode) {
-    case EPI_STORE: case EPI_RELU: case EPI_SWISH:
-      return (e.ldc * 2) % 16 == 0 && ((uintptr_t)e.C % 16) == 0;
-    case EPI_RESID: case EPI_SCALE_F32:
-      if (e.ldx % 4 || p.N % 4 || ((uintptr_t)e.X % 16)) return false;
-      if (e.mode == EPI_RESID && e.Xin && ((uintptr_t)e.Xin % 16)) return false;
-      if (e.ln_out && (e.ldx % 8 || p.N % 8 || ((uintptr_t)e.xb % 16))) return false;
-      return true;
-    default: return false;
-  }
-}
-
 template <typename T, class TL, template <int> class AL, class ALArgs>
 void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   using ALoad = AL<TL::GA>;
@@ -1554,18 +1333,6 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   if constexpr (ALoad::kConv) {
     cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al);
     return;
-  }
-  if constexpr (!ALoad::kConv && std::is_same<T, bf16_t>::value && direct_tile<TL>()) {
-    if (direct_ok(p, 2)) {
-      switch (p.epi.mode) {
-        case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad, true>), grid, block, 0, st, p, al); return;
-        case EPI_RELU: cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad, true>), grid, block, 0, st, p, al); return;
-        case EPI_SWISH: cfm_launch((gemm_kernel<T, EPI_SWISH, TL, ALoad, true>), grid, block, 0, st, p, al); return;
-        case EPI_RESID: cfm_launch((gemm_kernel<T, EPI_RESID, TL, ALoad, true>), grid, block, 0, st, p, al); return;
-        case EPI_SCALE_F32: cfm_launch((gemm_kernel<T, EPI_SCALE_F32, TL, ALoad, true>), grid, block, 0, st, p, al); return;
-        default: break;
-      }
-    }
   }
   switch (p.epi.mode) {
     case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
@@ -1610,10 +1377,14 @@ int g_gemm8_dense = [] { const char* s = getenv("CFM_GEMM8_DENSE"); return s ? a
 // write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 
-// Tile ids (CFM_GEMM_TILE / set_gemm_tile_override):
+// Tile ids (CFM_GEMM_TILE / set_gemm_tile_override; other ids run tile 0):
 //   0 128x128 NS2 | 1 256x128 NS3 | 5 64x128 NS2          (128-byte K-steps, several blocks / CU)
-//   7 256x256 NS4 | 8 128x128 NS8 | 9 256x128 NS5 | 10 128x256 NS5   (64-byte K-steps, 1 block / CU)
-//   11 256x256 NS2 (128-byte K-steps)
+//   11 256x256 NS2 (128-byte K-steps) | 12 128x128 2 K-groups NS3 | 14 128x128 2 K-groups NS4 |
+//   16 64x128 2 K-groups NS3
+// Measured and no longer instantiated (DESIGN §4 dead ends; their Tile aliases stay as the record):
+//   7 / 8 / 9 / 10 (64-byte K-step 1-block tiles), 13 / 15 / 17 (K-group variants), 18 (256-byte K-steps,
+//   2-deep ring: loop 17.0 -> 14.2 us without loads but 29.8 -> 36.4 us per ffn_down in the forward,
+//   profiles/r04e_tile18_ab.txt: one 64 KiB stage in flight does not cover the forward's load latency).
 // The fp32 parity mode instantiates 0, 1 and 5 only (other ids fall back to 0).
 // Automatic choice (tools/gemm_bench.py, MI355X, bf16): the implicit conv and the wide FFN-up
 // GEMM run best on 256x256 (tile 11); the N = 512 layer GEMMs on 64x128 at 3 blocks / CU (tile 5);
@@ -1659,6 +1430,10 @@ int pick_tile(int dtype, int M, int Nw, int epi, bool conv, int K = 0) {
     // the subsampling Linear (K = C * F2 = 10240, N = d): 64 tiles of 256x256 fill a quarter of the
     // chip; 128x128 in two K-groups (same K order as the small-M 64x128 K-group tile): 154 -> ~100 us
     if (epi == EPI_SCALE_F32 && K >= 4096) return M >= 4096 ? 12 : 16;
+    // very tall fp32-output GEMMs (the RNN-T joint's B*T'*(U+1) x (V+1) logits, 646k rows at config 4):
+    // 256x256 tiles, bench.py --mode joint 9.68 against 10.21 ms for 128x128 K-group tiles
+    // (profiles/r04e_joint_tile_ab.txt)
+    if (epi == EPI_SCALE_F32 && M >= 65536 && Nw >= 512) return 11;
     // the training step's fp32-output dgrads (M = B*T' rows, N = d): 128x128 K-group tiles
     // (tools/train_ab.sh: 38.5-38.8 against 38.9-39.2 ms per step for the 64x128 tile)
     if (epi == EPI_SCALE_F32 && M >= 4096) return 14;
@@ -1684,17 +1459,10 @@ void dispatch(int tile, GemmParams p, const ALArgs& args, hipStream_t st) {
   }
   if constexpr (kDeep) {
     switch (tile) {
-      case 7: setup(256, 256); launch_epi<T, T256x256, AL>(p, args, st); return;
-      case 8: setup(128, 128); launch_epi<T, T128x128d, AL>(p, args, st); return;
-      case 9: setup(256, 128); launch_epi<T, T256x128d, AL>(p, args, st); return;
-      case 10: setup(128, 256); launch_epi<T, T128x256d, AL>(p, args, st); return;
       case 11: setup(256, 256); launch_epi<T, T256x256w, AL>(p, args, st); return;
       case 12: setup(128, 128); launch_epi<T, T128x128k, AL>(p, args, st); return;
-      case 13: setup(128, 128); launch_epi<T, T128x128k2, AL>(p, args, st); return;
       case 14: setup(128, 128); launch_epi<T, T128x128k4, AL>(p, args, st); return;
-      case 15: setup(128, 256); launch_epi<T, T128x256k, AL>(p, args, st); return;
       case 16: setup(64, 128); launch_epi<T, T64x128k, AL>(p, args, st); return;
-      case 17: setup(128, 128); launch_epi<T, T128x128q, AL>(p, args, st); return;
       default: break;
     }
   }
@@ -1868,7 +1636,9 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   e.C = X2;
   e.ldc = C;
   GemmParams p = make_params(2, M, Wp, Kpad, C, e);
-  p.probe = 0;
+  // bit 8: split the two column tiles over the XCD parities (CFM_C12_XCD_COLS=0: contiguous tile ranges)
+  static const int xcd_cols = [] { const char* s = getenv("CFM_C12_XCD_COLS"); return s ? atoi(s) : 1; }();
+  p.probe = xcd_cols ? 8 : 0;
   p.Mtiles = (M + 255) / 256;
   p.Ntiles = (C + 255) / 256;
   Conv12Args a{(const uint4*)patch, w1h, (const char*)zero_page, T1, F1, T2, F2, C};

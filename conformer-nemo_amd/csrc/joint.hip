@@ -55,22 +55,30 @@ __global__ __launch_bounds__(256) void bdl_to_rows_kernel(const float* __restric
 // Hj[(b,t,u)][h] = act(f[b*T+t][h] + g[b*U+u][h]); 8 h per thread (16-byte bf16 / 2x16-byte fp32 stores).
 // Block (b*T + t, chunk of kHidU u's): 32-bit index math only, f's row loaded once per thread item,
 // 16-byte f / g loads when H % 8 == 0.
+// Tail columns (ntail > 0, compute-type hidden): the last ntail logits of every row, out[row][col0 + c] =
+// Hj[row] . W[col0 + c] + b[col0 + c], from the hidden values as stored (rounded to the compute type) and
+// the packed W rows - so the logits GEMM covers a whole number of 128-column tiles (V + 1 = 1025 -> 1024:
+// its last 256-wide tile would otherwise compute 1 column of 256).  Per-row sums in a fixed order.
 constexpr int kHidU = 16;
+constexpr int kTailMax = 4;
 template <typename TO>
 __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restrict__ f, const float* __restrict__ g,
                                                            int B, int T, int U, int H, int Hp, int act,
-                                                           TO* __restrict__ out, Drop drop) {
+                                                           TO* __restrict__ out, Drop drop, int ntail,
+                                                           const TO* __restrict__ wt, long ldw, const float* __restrict__ bt,
+                                                           float* __restrict__ lo, long ldo) {
+  __shared__ float tred[kTailMax * kHidU * 128];   // [c][uu][hg] partial dot products (Hp <= 1024)
   const int HG = Hp / 8;
-  const int bt = blockIdx.x;
-  const int b = bt / T;
+  const int bt_ = blockIdx.x;
+  const int b = bt_ / T;
   const int u0 = blockIdx.y * kHidU;
   const int nu = min(kHidU, U - u0);
   const bool vec = (H & 7) == 0;
-  const float* fr = f + (long)bt * H;
+  const float* fr = f + (long)bt_ * H;
   for (int j = threadIdx.x; j < nu * HG; j += 256) {
     const int uu = j / HG, hg = j - uu * HG;
     const int u = u0 + uu;
-    const long row = (long)bt * U + u;
+    const long row = (long)bt_ * U + u;
     const float* gr = g + ((long)b * U + u) * H;
     float v[8];
     if (vec && hg * 8 < H) {
@@ -96,18 +104,40 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
     }
     TO* o = out + row * Hp + hg * 8;
     if constexpr (sizeof(TO) == 2) {
-      *(uint4*)o = Vec16<bf16_t>::from_f32(v);
+      const uint4 packed = Vec16<bf16_t>::from_f32(v);
+      *(uint4*)o = packed;
+      if (ntail > 0) {
+        float vr[8], w8[8];
+        Vec16<bf16_t>::to_f32(packed, vr);   // the hidden as the logits GEMM reads it
+        for (int c = 0; c < ntail; ++c) {
+          Vec16<bf16_t>::to_f32(*(const uint4*)(wt + (long)c * ldw + hg * 8), w8);
+          float a = 0.0f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a = fmaf(vr[e], w8[e], a);
+          tred[(c * kHidU + uu) * 128 + hg] = a;
+        }
+      }
     } else {
       *(uint4*)o = Vec16<float>::from_f32(v);
       *(uint4*)(o + 4) = Vec16<float>::from_f32(v + 4);
     }
   }
+  if (ntail > 0) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < nu * ntail; t += 256) {
+      const int uu = t / ntail, c = t - uu * ntail;
+      float a = 0.0f;
+      for (int hg = 0; hg < HG; ++hg) a += tred[(c * kHidU + uu) * 128 + hg];
+      lo[((long)bt_ * U + u0 + uu) * ldo + c] = a + bt[c];
+    }
+  }
 }
 template <typename TO>
 void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, int Hp, int act, TO* out, Drop drop,
-                  hipStream_t st) {
+                  hipStream_t st, int ntail = 0, const TO* wt = nullptr, long ldw = 0, const float* bt = nullptr,
+                  float* lo = nullptr, long ldo = 0) {
   cfm_launch(joint_hidden_kernel<TO>, dim3((unsigned)(B * T), (unsigned)((U + kHidU - 1) / kHidU)), dim3(256), 0, st,
-             f, g, B, T, U, H, Hp, act, out, drop);
+             f, g, B, T, U, H, Hp, act, out, drop, ntail, wt, ldw, bt, lo, ldo);
 }
 
 // in-place log_softmax over rows of C fp32 values, one wave per row
@@ -373,11 +403,17 @@ void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu
          epi_f32((const float*)(h->wbuf + h->b_enc), fp, h->H, sc), h->zero, st);
     gemm(dt, ws + w.ag, H2p, B * U, h->H2, h->wbuf + h->w_pred, H2p, h->H,
          epi_f32((const float*)(h->wbuf + h->b_pred), gp, h->H, sc), h->zero, st);
+    // the last (C % 128) <= kTailMax logits of each row come from the hidden kernel, the GEMM covers
+    // whole 128-column tiles (bf16 mode; V + 1 = 1025 -> 1024 + 1)
+    const int ntail = (dt == DT_BF16 && h->C > 128 && h->C % 128 <= kTailMax && Hp <= 1024) ? h->C % 128 : 0;
+    const int Cm = h->C - ntail;
     if (dt == DT_F32)
       joint_hidden<float>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop, st);
     else
-      joint_hidden<bf16_t>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop, st);
-    gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), h->C,
+      joint_hidden<bf16_t>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop, st,
+                           ntail, (const bf16_t*)(h->wbuf + h->w_out) + (long)Cm * h->kp(h->H), h->kp(h->H),
+                           (const float*)(h->wbuf + h->b_out) + Cm, out + Cm, h->C);
+    gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), Cm,
          epi_f32((const float*)(h->wbuf + h->b_out), out, h->C, h->C % 4 ? 1 : 0), h->zero, st);
     if (log_softmax)
       cfm_launch(row_log_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, out, rows, h->C);

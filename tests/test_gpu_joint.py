@@ -62,3 +62,28 @@ def test_joint_large_shape_properties():
     s = torch.logsumexp(lp.double(), -1)
     assert torch.allclose(s, torch.zeros_like(s), atol=1e-4)
     assert torch.equal(lp[1:2], one)
+
+
+def test_joint_tail_columns_match_torch():
+    """V + 1 = 1025 classes: the logits GEMM covers 1024 columns and the hidden kernel the last one
+    (csrc/joint.hip, tail columns).  Against a torch fp32 restatement of RNNTJoint.joint (rnnt.py:951-1008)
+    on the module's own weights: whole logits and the tail column alone within the bf16 gate."""
+    from nemo.collections.asr.modules import RNNTJoint
+    torch.manual_seed(1)
+    j = RNNTJoint(jointnet=dict(encoder_hidden=64, pred_hidden=48, joint_hidden=64, activation="relu"),
+                  num_classes=1024).cuda().eval()
+    j.set_compute_mode("bf16")
+    enc = torch.randn(2, 64, 19, device="cuda")
+    dec = torch.randn(2, 48, 7, device="cuda")
+    with torch.no_grad():
+        j.log_softmax = None
+        lo = j(encoder_outputs=enc, decoder_outputs=dec)
+        out = j.joint_net[-1]
+        f = enc.transpose(1, 2) @ j.enc.weight.t() + j.enc.bias
+        g = dec.transpose(1, 2) @ j.pred.weight.t() + j.pred.bias
+        hid = torch.relu(f[:, :, None, :] + g[:, None, :, :])
+        ref = hid @ out.weight.t() + out.bias
+    assert lo.shape == ref.shape == (2, 19, 7, 1025)
+    assert rel_l2(lo.cpu().numpy(), ref.cpu().numpy()) <= GATE["bf16"]
+    assert rel_l2(lo[..., 1024:].cpu().numpy(), ref[..., 1024:].cpu().numpy()) <= GATE["bf16"]
+    assert rel_l2(lo[..., 1000:1024].cpu().numpy(), ref[..., 1000:1024].cpu().numpy()) <= GATE["bf16"]
