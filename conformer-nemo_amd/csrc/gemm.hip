@@ -1131,7 +1131,6 @@ constexpr int C12_LDS = 2 * G8_BUF + C12_PATCH + C12_MAXC * 32;
 static_assert(C12_LDS <= 160 * 1024, "conv12 LDS");
 
 __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca) {
-  auto c12_xcd_cols = [&] { return (p.probe & 8) != 0; };
   __shared__ __attribute__((aligned(16))) char smem[C12_LDS];
   typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1139,21 +1138,13 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   const int wm = wave >> 2, wn = wave & 3;
   const int C = ca.C;
 
-  // Block -> tile: with two 256-column tiles (C = 512) the XCDs of one parity take one column tile, so each
-  // XCD's L2 holds half of W2 (2.4 MB) instead of all of it; otherwise gemm8_kernel's contiguous ranges.
+  // block -> tile as gemm8_kernel (giving each XCD parity one of the two column tiles, so that an XCD's L2
+  // holds half of W2, measured neutral: profiles/r04g_conv12_xcd_cols_ab.txt)
   const int nblocks = p.Mtiles * p.Ntiles;
   const int bid = blockIdx.x;
-  int mt, ntl;
-  if (p.Ntiles == 2 && c12_xcd_cols()) {
-    const int full = nblocks >> 3;
-    if (bid < 8 * full) { mt = (bid >> 3) * 4 + ((bid & 7) >> 1); ntl = bid & 1; }
-    else { const int t = bid - 8 * full; mt = 4 * full + (t >> 1); ntl = t & 1; }
-  } else {
-    const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
-    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-    mt = wg / p.Ntiles;
-    ntl = wg - mt * p.Ntiles;
-  }
+  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
   const int m0 = mt * 256, n0 = ntl * 256;
 
   // B staging (W2 rows): as gemm8_kernel
@@ -1636,9 +1627,7 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   e.C = X2;
   e.ldc = C;
   GemmParams p = make_params(2, M, Wp, Kpad, C, e);
-  // bit 8: split the two column tiles over the XCD parities (CFM_C12_XCD_COLS=0: contiguous tile ranges)
-  static const int xcd_cols = [] { const char* s = getenv("CFM_C12_XCD_COLS"); return s ? atoi(s) : 1; }();
-  p.probe = xcd_cols ? 8 : 0;
+  p.probe = 0;
   p.Mtiles = (M + 255) / 256;
   p.Ntiles = (C + 255) / 256;
   Conv12Args a{(const uint4*)patch, w1h, (const char*)zero_page, T1, F1, T2, F2, C};

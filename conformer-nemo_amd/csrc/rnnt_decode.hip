@@ -447,6 +447,89 @@ __global__ void pack_lstm_kernel(const float* __restrict__ wih, const float* __r
   if (i < 4L * H) bc[i] = bih[i] + bhh[i];
 }
 
+// The same LSTM step on the matrix cores (fp32 in, fp32 sums: v_mfma_f32_16x16x4_f32, exact fp32
+// products like the VALU kernel, in another summation order).  Block = 4 hidden units x 16 batch rows;
+// its 16 W rows are ordered unit-major (row 4u + g = gate g of unit u0 + u), so the 16x16 output puts
+// the four gates (i, f, g, o) of unit u0 + (lane >> 4) for batch row b0 + (lane & 15) in one lane's
+// accumulator: the cell update needs no exchange.  K = I + H is split over the 8 waves in 16-wide
+// groups (a float4 of A and of B per lane and group: MFMA j takes element j of both, so each group's
+// 16 products are summed whatever the k order inside it); the eight partial tiles are summed in a
+// fixed order through LDS.  A block reads its 16 W rows (80 KB at H = 640) and the batch's [x | h]
+// rows once per step; the XCD that owns a unit block keeps its W rows in L2 across steps.
+template <int NT>
+__global__ __launch_bounds__(512) void lstm_step_mfma_kernel(const float* __restrict__ W, const float* __restrict__ bias,
+                                                             const float* __restrict__ emb, int nemb,
+                                                             const int32_t* __restrict__ xlab, const float* __restrict__ xsrc,
+                                                             const float* __restrict__ h, const float* __restrict__ c,
+                                                             float* __restrict__ h2, float* __restrict__ c2,
+                                                             float* __restrict__ gout, long gstride, int B, int I, int H,
+                                                             const int* __restrict__ run_flag,
+                                                             float* __restrict__ gates_out, Drop gdrop, int gstep) {
+  __shared__ f32x4 part[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int u0 = blockIdx.x * 4, b0 = blockIdx.y * 16;
+  const int K = I + H, G = K / 16;   // NT = ceil(G / 8) groups per wave
+  if (run_flag && *run_flag == 0) return;   // uniform: every utterance finished
+  // operand rows of this lane: W row (unit u0 + rr / 4, gate rr % 4), batch row b0 + rr
+  const int rr = lane & 15, kq = lane >> 4;
+  const int wu = min(u0 + (rr >> 2), H - 1), wg = rr & 3;
+  const float* wrow = W + ((long)wg * H + wu) * K + 4 * kq;
+  const int b = b0 + rr;
+  const int bc = min(b, B - 1);
+  // the row's input part: the previous layer's h, an embedding row, or zero (start of sequence; rows past
+  // B) - always loaded from a valid address and zeroed by a select (no per-lane conditional loads)
+  const int lab = xsrc ? 0 : xlab[bc];
+  const bool xok = b < B && (xsrc != nullptr || lab >= 0);
+  const float* xrow = xsrc ? xsrc + (long)bc * I : emb + (long)min(max(lab, 0), nemb - 1) * I;
+  const float* hrow = h + (long)bc * H;
+  const bool hok = b < B;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float4 wa[NT], xa[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {   // all loads first (latency), then the MFMAs
+    const int gi = min(w + 8 * t, G - 1);
+    const int k = gi * 16 + 4 * kq;
+    wa[t] = *(const float4*)(wrow + gi * 16);
+    const bool inx = k < I;
+    const float4 v = *(const float4*)(inx ? xrow + k : hrow + (k - I));
+    xa[t] = (inx ? xok : hok) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (w + 8 * t < G) {   // wave-uniform
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].x, xa[t].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].y, xa[t].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].z, xa[t].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].w, xa[t].w, acc, 0, 0, 0);
+    }
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 s = part[0][lane];
+#pragma unroll
+  for (int ww = 1; ww < 8; ++ww) {
+    const f32x4 t = part[ww][lane];
+    s[0] += t[0]; s[1] += t[1]; s[2] += t[2]; s[3] += t[3];
+  }
+  // lane: batch row b0 + (lane & 15), unit u0 + (lane >> 4); s[e] = gate e's sum
+  const int bb = b0 + (lane & 15), j = u0 + (lane >> 4);
+  if (bb >= B || j >= H) return;
+  const float gi = sigm(s[0] + bias[j]);
+  const float gf = sigm(s[1] + bias[H + j]);
+  const float gg = tanhf(s[2] + bias[2 * H + j]);
+  const float go = sigm(s[3] + bias[3 * H + j]);
+  const float cn = gf * c[(long)bb * H + j] + gi * gg;
+  const float hn = go * tanhf(cn);
+  c2[(long)bb * H + j] = cn;
+  h2[(long)bb * H + j] = hn;
+  if (gout) gout[(long)bb * gstride + j] = hn * drop_mul(gdrop, ((uint64_t)bb * (gstride / H) + gstep) * H + j);
+  if (gates_out) {
+    float* gr = gates_out + (long)bb * 4L * H;
+    gr[j] = gi; gr[H + j] = gf; gr[2 * H + j] = gg; gr[3 * H + j] = go;
+  }
+}
+
 size_t lstm_lds(int K) { return (size_t)(RB * K + RED + 4 * 4 * RB) * sizeof(float); }
 
 // > 64 KB of dynamic LDS needs the per-kernel opt-in; done once per process.
@@ -467,13 +550,39 @@ void check_device(const cfm_rnnt_decoder* h) {
   if (cur != h->device) HIP_OK(hipSetDevice(h->device));
 }
 
+// one LSTM layer step: the matrix-core kernel when the shapes allow it (I, H multiples of 16, H % 4 == 0,
+// K <= 3072; CFM_LSTM_MFMA=0 keeps the VALU kernel), else lstm_step_kernel
+void launch_lstm_step(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, const float* xsrc, const float* hcur,
+                      const float* ccur, float* hn, float* cn, float* gout, long gstride, int B, const int* flag,
+                      float* gates_out, Drop gdrop, int gstep, hipStream_t st) {
+  static const int mfma = [] { const char* e = getenv("CFM_LSTM_MFMA"); return e ? atoi(e) : 1; }();
+  const int H = d->H, I = H, K = I + H;
+  const int NT = (K / 16 + 7) / 8;
+  if (mfma && H % 16 == 0 && I % 16 == 0 && (NT == 4 || NT == 5 || NT == 8 || NT == 10 || NT == 12 || NT == 16)) {
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)(H / 4), (unsigned)((B + 15) / 16)), dim3(512), 0, st, d->W(l), d->bias(l),
+                         d->emb(), d->V + 1, xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, I, H, flag, gates_out,
+                         gdrop, gstep);
+    };
+    switch (NT) {
+      case 4: go(lstm_step_mfma_kernel<4>); break;
+      case 5: go(lstm_step_mfma_kernel<5>); break;
+      case 8: go(lstm_step_mfma_kernel<8>); break;
+      case 10: go(lstm_step_mfma_kernel<10>); break;
+      case 12: go(lstm_step_mfma_kernel<12>); break;
+      default: go(lstm_step_mfma_kernel<16>); break;
+    }
+    return;
+  }
+  const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
+  hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(K), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
+                     xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, I, H, flag, gates_out, gdrop, gstep);
+}
+
 void lstm_layer(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, const float* xsrc, const float* hcur,
                 const float* ccur, float* hn, float* cn, float* gout, long gstride, int B, const int* flag,
                 hipStream_t st) {
-  const int H = d->H, K = 2 * H;
-  const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
-  hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(K), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
-                     xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, H, H, flag);
+  launch_lstm_step(d, l, xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, flag, nullptr, Drop{0u, 0u, 1.0f}, 0, st);
 }
 
 struct GreedyWs {
@@ -787,16 +896,14 @@ cfm_status cfm_rnnt_decoder_train_forward(cfm_rnnt_decoder* d, const int64_t* y,
                        add_sos ? 1 : 0, d->V + 1, tp.xlab);
     HIP_OK(hipMemsetAsync(tp.zero, 0, (size_t)bh * 4, st));
     const Drop gdrop = make_drop(dropout, seed, 2);
-    const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
     for (int u = 0; u < S; ++u)
       for (int l = 0; l < L; ++l) {
         const bool top = l == L - 1;
         const float* hprev = u ? tp.h(l, u - 1) : tp.zero;
         const float* cprev = u ? tp.c(l, u - 1) : tp.zero;
-        hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(2 * H), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
-                           tp.xlab + (long)u * B, l ? tp.h(l - 1, u) : nullptr, hprev, cprev, tp.h(l, u), tp.c(l, u),
-                           top ? g + (long)u * H : nullptr, (long)S * H, B, H, H, (const int*)nullptr, tp.gates(l, u),
-                           gdrop, u);
+        launch_lstm_step(d, l, tp.xlab + (long)u * B, l ? tp.h(l - 1, u) : nullptr, hprev, cprev, tp.h(l, u), tp.c(l, u),
+                         top ? g + (long)u * H : nullptr, (long)S * H, B, (const int*)nullptr, tp.gates(l, u), gdrop, u,
+                         st);
       }
     HIP_OK(hipGetLastError());
   });
