@@ -626,7 +626,7 @@ TrainTape train_tape(const cfm_rnnt_decoder* d, char* tape, int B, int S) {
   t.zero = (float*)(after + round_up((long)(S + 1) * B * 4, 256));   // (B, H) zeros: the initial state
   return t;
 }
-struct BwdWs { long dy, dgates, dh, dc, x, hp, lin, total; };
+struct BwdWs { long dy, dgates, dh, dc, x, hp, wt, lin, total; };
 constexpr int kHhSplits = 16;   // row splits of the recurrent W_hh^T . dgates product
 BwdWs bwd_ws(const cfm_rnnt_decoder* d, int B, int S) {
   BwdWs w{};
@@ -639,9 +639,73 @@ BwdWs bwd_ws(const cfm_rnnt_decoder* d, int B, int S) {
   w.dc = take((long)B * d->H * 4);
   w.x = take(sbh);
   w.hp = take(sbh);
+  w.wt = take(4L * d->H * d->H * 4);              // W_hh^T of the layer (the matrix-core recurrent product)
   w.lin = take((long)cfm_op_linear_backward_ws_size(CFM_COMPUTE_FP32, S * B, d->H, 4 * d->H));
   w.total = round_up(o, 256);
   return w;
+}
+
+// W_hh (4H, H) -> W_hh^T (H, 4H), 32x32 LDS tiles
+__global__ __launch_bounds__(256) void transpose_whh_kernel(const float* __restrict__ w, int R, int Cc, float* __restrict__ wt) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8)
+    if (r0 + k < R && c0 + tx < Cc) tile[k][tx] = w[(long)(r0 + k) * Cc + c0 + tx];
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8)
+    if (c0 + k < Cc && r0 + tx < R) wt[(long)(c0 + k) * R + r0 + tx] = tile[tx][k];
+}
+
+// The recurrent gradient dh[b][k] = sum_r W_hh[r][k] dgates[b][r] of one step on the matrix cores
+// (v_mfma_f32_16x16x4_f32, fp32 sums): block = 16 hidden rows k x 16 batch rows, the 4H-long contraction
+// split over 8 waves in 16-wide groups (a float4 of W_hh^T and of dgates per lane and group), partial
+// tiles summed in a fixed order through LDS; writes the whole dh (the cell backward reads one part).
+template <int NT>
+__global__ __launch_bounds__(512) void lstm_hh_bwd_mfma_kernel(const float* __restrict__ dgates,
+                                                               const float* __restrict__ whhT, int B, int H,
+                                                               float* __restrict__ dh) {
+  __shared__ f32x4 part[8][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  const int R = 4 * H, G = R / 16;
+  const int rr = lane & 15, kq = lane >> 4;
+  const float* arow = whhT + (long)min(k0 + rr, H - 1) * R + 4 * kq;
+  const int b = min(b0 + rr, B - 1);
+  const float* brow = dgates + (long)b * R + 4 * kq;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float4 wa[NT], xa[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int gi = min(w + 8 * t, G - 1);
+    wa[t] = *(const float4*)(arow + gi * 16);
+    xa[t] = *(const float4*)(brow + gi * 16);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (w + 8 * t < G) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].x, xa[t].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].y, xa[t].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].z, xa[t].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[t].w, xa[t].w, acc, 0, 0, 0);
+    }
+  }
+  part[w][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+  f32x4 s = part[0][lane];
+#pragma unroll
+  for (int ww = 1; ww < 8; ++ww) {
+    const f32x4 t = part[ww][lane];
+    s[0] += t[0]; s[1] += t[1]; s[2] += t[2]; s[3] += t[3];
+  }
+  // lane: batch column b0 + (lane & 15), hidden rows k0 + 4 (lane >> 4) + e
+  const int bb = b0 + (lane & 15);
+  if (bb >= B) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = k0 + 4 * (lane >> 4) + e;
+    if (k < H) dh[(long)bb * H + k] = s[e];
+  }
 }
 
 // dy[u][b][j] = dg[b][u][j] * dropout'(b, u, j)  (LSTMDropout's output dropout)
@@ -946,15 +1010,30 @@ cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int 
                                                   lws_bytes, st);
       if (r != CFM_OK) fail(r, std::string("prediction-net backward: ") + cfm_last_error());
     };
+    // the recurrent product on the matrix cores (CFM_LSTM_MFMA=0: 16 VALU row splits)
+    static const int mfma = [] { const char* e = getenv("CFM_LSTM_MFMA"); return e ? atoi(e) : 1; }();
+    const int NT = (4 * H / 16 + 7) / 8;
+    const bool hh_mfma = mfma && H % 16 == 0 && (NT == 10 || NT == 16 || NT == 20);
+    float* whhT = (float*)(ws + w.wt);
     for (int l = L - 1; l >= 0; --l) {
       HIP_OK(hipMemsetAsync(dc, 0, (size_t)B * H * 4, st));
+      if (hh_mfma)
+        hipLaunchKernelGGL(transpose_whh_kernel, dim3((unsigned)((H + 31) / 32), (unsigned)((4 * H + 31) / 32)), dim3(256),
+                           0, st, w_hh[l], 4 * H, H, whhT);
       for (int u = S - 1; u >= 0; --u) {
         hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3((unsigned)((B * H + 255) / 256)), dim3(256), 0, st,
                            dy + (long)u * B * H, tp.gates(l, u), tp.c(l, u), u ? tp.c(l, u - 1) : tp.zero, B, H,
-                           (const float*)dh, u == S - 1 ? 0 : kHhSplits, dc, dgt + (long)u * B * 4 * H);
-        if (u > 0)
+                           (const float*)dh, u == S - 1 ? 0 : (hh_mfma ? 1 : kHhSplits), dc, dgt + (long)u * B * 4 * H);
+        if (u > 0 && hh_mfma) {
+          const dim3 grid((unsigned)((H + 15) / 16), (unsigned)((B + 15) / 16));
+          const float* dgu = dgt + (long)u * B * 4 * H;
+          if (NT == 10) hipLaunchKernelGGL(lstm_hh_bwd_mfma_kernel<10>, grid, dim3(512), 0, st, dgu, whhT, B, H, dh);
+          else if (NT == 16) hipLaunchKernelGGL(lstm_hh_bwd_mfma_kernel<16>, grid, dim3(512), 0, st, dgu, whhT, B, H, dh);
+          else hipLaunchKernelGGL(lstm_hh_bwd_mfma_kernel<20>, grid, dim3(512), 0, st, dgu, whhT, B, H, dh);
+        } else if (u > 0) {
           hipLaunchKernelGGL(lstm_hh_bwd_kernel, dim3((unsigned)((H + 63) / 64), kHhSplits), dim3(256), 0, st,
                              dgt + (long)u * B * 4 * H, w_hh[l], B, H, dh);
+        }
       }
       // the layer's input rows and h_{u-1} rows (S, B, H)
       if (l == 0)
