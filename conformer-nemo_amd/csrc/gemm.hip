@@ -59,7 +59,10 @@ struct Tile {
   // column (c, d)
   static constexpr int RS_OFF = (NSTAGE * STAGE_BYTES > EPI_BYTES) ? NSTAGE * STAGE_BYTES : EPI_BYTES;
   static constexpr int CD_OFF = RS_OFF + BM * 8;
-  static constexpr int LDS_BYTES = CD_OFF + BN * 8;
+  // the norm_out fold's second row table (mean, rstd) and column table (c2, c3) (GemmEpi::ln2_in)
+  static constexpr int RS2_OFF = CD_OFF + BN * 8;
+  static constexpr int C23_OFF = RS2_OFF + BM * 8;
+  static constexpr int LDS_BYTES = C23_OFF + BN * 8;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
   static_assert(BKB == 64 || BKB == 128 || BKB == 256, "stage depth");
   // 256-byte K-steps run only where the host checked p.kb % 256 == 0 (dispatch)
@@ -235,6 +238,7 @@ struct GemmParams {
   long split_x;   // split-K (gridDim.y > 1, dense A only): slice y covers K bytes [y*kb, (y+1)*kb) and
                   // writes its fp32 partial at epi.X + y * split_x
   int probe;   // microbenchmark probes only (cfm_bench_gemm): 1 no main-loop loads, 2 no epilogue, 4 one K-step
+  int ahead;   // K-group tiles with >= 3 stages: the read-ahead main loop (g_gemm_ahead)
   GemmEpi epi;
 };
 
@@ -253,6 +257,11 @@ CFM_DEV int real_row(const GemmParams& p, int m, int BM) {
 // Folded LayerNorm (GemmEpi::ln_in): rs[r] = (mean, rstd) of the pass's local row r, cd[j] = (c, d)
 // of the tile's local column j.
 CFM_DEV float ln_fold(float2 s, float v, float2 cd) { return s.y * (v - s.x * cd.x) + cd.y; }
+// Two stacked LayerNorms (GemmEpi::ln2_in): s / s2 = (mean, rstd) of the first / second one's input,
+// cd = (c1, c4), c23 = (c2, c3) of the column
+CFM_DEV float ln_fold2(float2 s, float2 s2, float v, float2 cd, float2 c23) {
+  return s2.y * (s.y * (v - s.x * cd.x) + c23.y - s2.x * c23.x) + cd.y;
+}
 
 // Sum over the 32 lanes of a half-wave, the same value in every lane: DPP quad permutes and row
 // mirrors (VALU) for 16 lanes, one xor-16 shuffle.
@@ -270,12 +279,13 @@ CFM_DEV float halfwave_sum(float v) {
 
 // FOLD: the LayerNorm fold is active for this launch (GemmEpi::ln_in set: consumer; ln_out / xb
 // set: EPI_RESID producer) - a compile-time flag, so no per-element branches in the unrolled loops.
-template <typename T, int EPI, class TL, bool FOLD>
+template <typename T, int EPI, class TL, bool FOLD, bool FOLD2 = false>
 CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, long xoff, const float2* rs,
-                      const float2* cd) {
+                      const float2* cd, const float2* rs2 = nullptr, const float2* c23 = nullptr) {
   const GemmEpi& e = p.epi;
   const int tid = threadIdx.x;
   constexpr bool fold = FOLD;
+  static_assert(!FOLD2 || FOLD, "the norm_out fold is a LayerNorm fold");
   if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
     // fp32 output (N % 4 == 0), 4 columns per thread-chunk
     constexpr int CPR = TL::BN / 4;                 // chunks per row
@@ -319,6 +329,19 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       for (int q = 0; q < NP; ++q) {
         const int m = min(m0 + r0 + q * RPP, p.M - 1);
         xv[q] = *(const float4*)(XI + xoff + (long)m * e.ldx + nc);
+      }
+      if constexpr (FOLD) {
+        if (e.xln_g) {   // the residual is norm_out(y): y read, normalised here (rs = y's row statistics)
+          const float4 gg = *(const float4*)(e.xln_g + nc), bb = *(const float4*)(e.xln_b + nc);
+#pragma unroll
+          for (int q = 0; q < NP; ++q) {
+            const float2 st = rs[r0 + q * RPP];
+            xv[q].x = (xv[q].x - st.x) * st.y * gg.x + bb.x;
+            xv[q].y = (xv[q].y - st.x) * st.y * gg.y + bb.y;
+            xv[q].z = (xv[q].z - st.x) * st.y * gg.z + bb.z;
+            xv[q].w = (xv[q].w - st.x) * st.y * gg.w + bb.w;
+          }
+        }
       }
     }
 #pragma unroll
@@ -379,6 +402,16 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           const float a0 = o.x - mean, a1 = o.y - mean, a2 = o.z - mean, a3 = o.w - mean;
           const float q2 = halfwave_sum(ok ? (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3) : 0.0f);
           if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, q2);
+          if (e.ln2_out) {
+            // the sums the consumer's second LayerNorm statistics are formed from (GemmEpi::ln2_out)
+            const float4 gg = *(const float4*)(e.ln2_g + nc), bb = *(const float4*)(e.ln2_b + nc);
+            const float u0 = a0 * gg.x, u1 = a1 * gg.y, u2 = a2 * gg.z, u3 = a3 * gg.w;
+            const float sa = halfwave_sum(ok ? (u0 + u1) + (u2 + u3) : 0.0f);
+            const float sb = halfwave_sum(ok ? (u0 * u0 + u1 * u1) + (u2 * u2 + u3 * u3) : 0.0f);
+            const float sc = halfwave_sum(ok ? (u0 * gg.x + u1 * gg.y) + (u2 * gg.z + u3 * gg.w) : 0.0f);
+            const float sd = halfwave_sum(ok ? (u0 * bb.x + u1 * bb.y) + (u2 * bb.z + u3 * bb.w) : 0.0f);
+            if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln2_out[(long)m * e.ln_parts + g] = make_float4(sa, sb, sc, sd);
+          }
         }
       }
     }
@@ -519,8 +552,9 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
-      float2 st;
+      float2 st, st2;
       if constexpr (fold) st = rs[r];
+      if constexpr (FOLD2) st2 = rs2[r];
       float zf[VE];
       if constexpr (EPI == EPI_SWISH_BWD) {
         // z row chunk of this output chunk (host guarantees N % VE == 0); rows past M read row M-1
@@ -531,7 +565,8 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
         float v = img[r * TL::EPS + cc * VE + i];
-        if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
+        if constexpr (FOLD2) v = ln_fold2(st, st2, v, cd[cc * VE + i], c23[cc * VE + i]);
+        else if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
         if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
         if constexpr (EPI == EPI_SWISH) v = swishf(v);
         if constexpr (EPI == EPI_SWISH_BWD) {
@@ -658,6 +693,67 @@ CFM_DEV void pack_chunks16(const float* v, uint4& c0, uint4& c1) {
   c1 = make_uint4(s2[0], s3[0], s2[1], s3[1]);
 }
 
+// norm_out fold tables (GemmEpi::ln2_in): row tid's (mean, rstd) of y (the first LayerNorm's input,
+// from its (mean, M2) granule partials, prefetched in ln_pre) and of w = LN1(y) (the second one's
+// input), formed from the producer's granule sums around m_g and LN1's constants:
+//   S_A = sum_k (y_k - m1) g_k        = sum_g A_g + (m_g - m1) G_g
+//   m2  = mean(b) + r1 S_A / W
+//   S_B = sum_k (y_k - m1)^2 g_k^2    = sum_g B_g + 2 (m_g - m1) C_g + (m_g - m1)^2 G2_g
+//   S_D = sum_k (y_k - m1) g_k b_k    = sum_g D_g + (m_g - m1) GB_g
+//   W var2 = r1^2 S_B + 2 r1 (S_D - m2 S_A) + sum (b - mean b)^2 + W (mean b - m2)^2
+// and column tid's (c1, c4) / (c2, c3).
+template <class P>
+CFM_DEV void ln2_tables(const P& p, int m0, int n0, int BM, int BN, const float2 (&ln_pre)[LN_PRE], float2 cd_pre,
+                        float2* rs_tab, float2* cd_tab, float2* rs2_tab, float2* c23_tab) {
+  const int tid = threadIdx.x;
+  const GemmEpi& e = p.epi;
+  const int W = e.ln_width, np = e.ln_parts;
+  if (tid < BM) {
+    const long row = real_row(p, m0 + tid, BM);
+    const float2* pp = e.ln_in + row * np;
+    const float4* qq = e.ln2_in + row * np;
+    auto cnt = [&](int g) { return (float)min(LN_GRANULE, W - g * LN_GRANULE); };
+    float sm = 0.0f;
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g) sm += g < np ? cnt(g) * ln_pre[g].x : 0.0f;
+    for (int g = LN_PRE; g < np; ++g) sm += cnt(g) * pp[g].x;
+    const float m1 = sm / (float)W;
+    // the first LN_PRE granules' sums and constants load unconditionally (clamped granule; a load under
+    // a per-granule branch would be issued and waited for one at a time)
+    float4 s4p[LN_PRE], k4p[LN_PRE];
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g) {
+      const int gc = min(g, np - 1);
+      s4p[g] = qq[gc];
+      k4p[g] = *(const float4*)(e.ln2_k + 4 * gc);   // (sum g, sum g^2, sum g b, 0) of granule gc
+    }
+    float q1 = 0.0f, sa = 0.0f, sb = 0.0f, sd = 0.0f;
+    auto add = [&](int g, float2 pg, float4 s4, float4 k4) {
+      const float dm = pg.x - m1;
+      q1 += pg.y + cnt(g) * dm * dm;
+      sa += s4.x + dm * k4.x;
+      sb += s4.y + 2.0f * dm * s4.z + dm * dm * k4.y;
+      sd += s4.w + dm * k4.z;
+    };
+#pragma unroll
+    for (int g = 0; g < LN_PRE; ++g)
+      if (g < np) add(g, ln_pre[g], s4p[g], k4p[g]);
+    for (int g = LN_PRE; g < np; ++g) add(g, pp[g], qq[g], *(const float4*)(e.ln2_k + 4 * g));
+    const float r1 = 1.0f / sqrtf(q1 / (float)W + 1e-5f);
+    const float bmean = e.ln2_k[4 * np], bvar = e.ln2_k[4 * np + 1];
+    const float m2 = bmean + r1 * sa / (float)W;
+    const float db = bmean - m2;
+    const float q2 = r1 * r1 * sb + 2.0f * r1 * (sd - m2 * sa) + bvar + (float)W * db * db;
+    rs_tab[tid] = make_float2(m1, r1);
+    rs2_tab[tid] = make_float2(m2, 1.0f / sqrtf(fmaxf(q2, 0.0f) / (float)W + 1e-5f));
+  }
+  if (tid < BN) {
+    const int nc = n0 + tid;
+    cd_tab[tid] = cd_pre;
+    c23_tab[tid] = make_float2(e.ln_c2[nc], e.ln_c3[nc]);
+  }
+}
+
 template <typename T, int EPI, class TL, class ALoad>
 __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload) {
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
@@ -693,18 +789,26 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     wrow[i] = p.W + koff + (long)(n0 + rr) * p.ldw_b + ((lane % TL::SLOTS) ^ TL::swz(rr)) * 16;
   }
   const uint32_t smem_base = lds_addr(smem);
+  if (p.probe & 16) {   // debug probe: poison the whole LDS image (NaN) so a read of an unwritten byte shows
+    for (int i = tid; i < TL::LDS_BYTES / 4; i += TL::NT) ((uint32_t*)smem)[i] = 0xffffffffu;
+    __syncthreads();
+  }
 
   // folded LayerNorm operands, loaded now and consumed by the epilogue (the loads complete during
   // the main loop): row tid's first LN_PRE granule partials, column tid's (c, d)
+  // (the residual's partials instead for EPI_RESID's LayerNorm-on-read, GemmEpi::xln_in)
   float2 ln_pre[LN_PRE];
   float2 cd_pre = make_float2(0.0f, 0.0f);
-  if (p.epi.ln_in) {
+  const float2* ln_src = p.epi.ln_in ? p.epi.ln_in : p.epi.xln_in;
+  if (ln_src) {
     const int np = p.epi.ln_parts;
-    const float2* pp = p.epi.ln_in + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
+    const float2* pp = ln_src + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
 #pragma unroll
     for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
-    const int nc = n0 + min(tid, TL::BN - 1);
-    cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
+    if (p.epi.ln_in) {
+      const int nc = n0 + min(tid, TL::BN - 1);
+      cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
+    }
   }
 
   auto stage = [&](int kt, int slot) {
@@ -739,44 +843,98 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
     for (int j = 0; j < TL::NR; ++j) bf[j] = *(const uint4*)(Sb + (b_row0 + j * 32) * TL::BKB + so);
   };
+  constexpr bool kAheadTile = TL::KG > 1 && NS >= 3;
+  const bool ahead = kAheadTile && p.ahead;
+  const int npro = ahead ? NS : NS - 1;   // the read-ahead loop keeps one more stage in flight
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nk) stage(s, s);
-  // Software pipeline: the fragments of substep g+1 are read from LDS while the MFMAs of substep
-  // g run.  The ring wait + barrier for K-step kt+1 sit in front of the LAST substep of kt, so the
-  // first fragments of kt+1 are already in registers when kt+1 starts.
-  wait_stages<G, NS - 2>(min(NS - 2, nk - 1));
-  wait_lgkm0();
-  raw_barrier();
-  uint4 afc[TL::MR], bfc[TL::NR];
-  read_frags(smem, 0, afc, bfc);
-  int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // refill the slot K-step kt-1 used: every wave finished reading it before the last barrier
-    if (kt + NS - 1 < nk && !(p.probe & 1)) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
-    const char* Sb = smem + slot * TL::STAGE_BYTES;
-    const int nslot = (slot == NS - 1) ? 0 : slot + 1;
+  for (int s = 0; s < NS; ++s)
+    if (s < npro && s < nk) stage(s, s);
+  float2* rs_tab = (float2*)(smem + TL::RS_OFF);
+  float2* cd_tab = (float2*)(smem + TL::CD_OFF);
+  float2* rs2_tab = (float2*)(smem + TL::RS2_OFF);
+  float2* c23_tab = (float2*)(smem + TL::C23_OFF);
+  if constexpr (EPI == EPI_SWISH) {
+    // norm_out fold: both LayerNorms' row statistics, computed while the first stages land (the
+    // tables sit behind the ring and the epilogue image; read after the epilogue's first barrier)
+    if (p.epi.ln2_in && !(p.probe & 32)) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
+  }
+  if constexpr (kAheadTile) {
+    if (ahead) {
+      // Read-ahead loop: K-step kt's fragments (all substeps) are in registers when kt starts, and
+      // kt+1's are read from LDS while kt multiplies.  The barrier at the top of kt certifies that
+      // K-step kt+1 has landed for every wave and that every wave holds kt's fragments, so kt's slot
+      // is refilled at once (stage kt+NS: NS-1 stages in flight).  Two fragment sets alternate (the
+      // loop is unrolled by two), so no register copies.
+      uint4 fa[KSUB][TL::MR + TL::NR], fb[KSUB][TL::MR + TL::NR];
+      wait_stages<G, NS - 1>(min(NS - 1, nk - 1));   // K-step 0 has landed (this wave's part)
+      wait_lgkm0();
+      raw_barrier();
 #pragma unroll
-    for (int kk = 0; kk < KSUB; ++kk) {
-      uint4 afn[TL::MR], bfn[TL::NR];
-      if (kk + 1 < KSUB) {
-        read_frags(Sb, kk + 1, afn, bfn);
-      } else if (kt + 1 < nk) {
-        wait_stages<G, NS - 2>(min(NS - 2, nk - 2 - kt));   // K-step kt+1 has landed
-        wait_lgkm0();
-        raw_barrier();
-        read_frags(smem + nslot * TL::STAGE_BYTES, 0, afn, bfn);
+      for (int kk = 0; kk < KSUB; ++kk) read_frags(smem, kk, fa[kk], fa[kk] + TL::MR);
+      auto body = [&](int kt, uint4 (&cur)[KSUB][TL::MR + TL::NR], uint4 (&nxt)[KSUB][TL::MR + TL::NR]) {
+        if (kt + 1 < nk) {
+          wait_stages<G, NS - 2>(min(NS - 2, nk - 2 - kt));   // K-step kt+1 has landed (this wave's part)
+          wait_lgkm0();                                      // this wave holds K-step kt's fragments
+          raw_barrier();
+          if (kt + NS < nk && !(p.probe & 1)) stage(kt + NS, kt % NS);
+        }
+        // past the last K-step the reads fetch a stale slot that no MFMA uses
+        const char* Sn = smem + ((kt + 1) % NS) * TL::STAGE_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < KSUB; ++kk) {
+          read_frags(Sn, kk, nxt[kk], nxt[kk] + TL::MR);
+          // keep the reads ahead of this substep's MFMAs (the scheduler would sink them past all of
+          // them, and the next barrier's lgkmcnt(0) would then wait on their full latency)
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+            for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], cur[kk][i], cur[kk][TL::MR + j]);
+        }
+      };
+      for (int kt = 0; kt < nk; kt += 2) {
+        body(kt, fa, fb);
+        if (kt + 1 < nk) body(kt + 1, fb, fa);
       }
-#pragma unroll
-      for (int i = 0; i < TL::MR; ++i)
-#pragma unroll
-        for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
-#pragma unroll
-      for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
-#pragma unroll
-      for (int j = 0; j < TL::NR; ++j) bfc[j] = bfn[j];
     }
-    slot = nslot;
+  }
+  if (!ahead) {
+    // Software pipeline: the fragments of substep g+1 are read from LDS while the MFMAs of substep
+    // g run.  The ring wait + barrier for K-step kt+1 sit in front of the LAST substep of kt, so the
+    // first fragments of kt+1 are already in registers when kt+1 starts.
+    wait_stages<G, NS - 2>(min(NS - 2, nk - 1));
+    wait_lgkm0();
+    raw_barrier();
+    uint4 afc[TL::MR], bfc[TL::NR];
+    read_frags(smem, 0, afc, bfc);
+    int slot = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      // refill the slot K-step kt-1 used: every wave finished reading it before the last barrier
+      if (kt + NS - 1 < nk && !(p.probe & 1)) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
+      const char* Sb = smem + slot * TL::STAGE_BYTES;
+      const int nslot = (slot == NS - 1) ? 0 : slot + 1;
+#pragma unroll
+      for (int kk = 0; kk < KSUB; ++kk) {
+        uint4 afn[TL::MR], bfn[TL::NR];
+        if (kk + 1 < KSUB) {
+          read_frags(Sb, kk + 1, afn, bfn);
+        } else if (kt + 1 < nk) {
+          wait_stages<G, NS - 2>(min(NS - 2, nk - 2 - kt));   // K-step kt+1 has landed
+          wait_lgkm0();
+          raw_barrier();
+          read_frags(smem + nslot * TL::STAGE_BYTES, 0, afn, bfn);
+        }
+#pragma unroll
+        for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+          for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
+#pragma unroll
+        for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j) bfc[j] = bfn[j];
+      }
+      slot = nslot;
+    }
   }
 
   if (p.probe & 2) {   // probe: no epilogue (keep the accumulators alive)
@@ -836,11 +994,12 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   // folded LayerNorm: (mean, rstd) of row tid from its granule partials (Chan et al.'s pairwise
   // combination of (count, mean, M2)) and (c, d) of column tid, from the values prefetched at the
   // kernel start; visible after the first pass's barrier
-  float2* rs_tab = (float2*)(smem + TL::RS_OFF);
-  float2* cd_tab = (float2*)(smem + TL::CD_OFF);
-  if (p.epi.ln_in) {
+  if constexpr (EPI == EPI_SWISH) {   // debug probe 32: the norm_out fold tables after the main loop
+    if (p.epi.ln2_in && (p.probe & 32)) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
+  }
+  if (ln_src && !p.epi.ln2_in) {
     const int W = p.epi.ln_width, np = p.epi.ln_parts;
-    const float2* pp = p.epi.ln_in + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
+    const float2* pp = ln_src + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
     float sm = 0.0f;
 #pragma unroll
     for (int g = 0; g < LN_PRE; ++g)
@@ -859,7 +1018,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
       m2 += pg.y + (float)min(LN_GRANULE, W - g * LN_GRANULE) * dm * dm;
     }
     if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
-    if (tid < TL::BN) cd_tab[tid] = cd_pre;
+    if (tid < TL::BN && p.epi.ln_in) cd_tab[tid] = cd_pre;
   }
   constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
@@ -879,7 +1038,17 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
         }
     }
     __syncthreads();
-    if (p.epi.ln_in || p.epi.ln_out)
+    bool done = false;
+    if constexpr (EPI == EPI_SWISH) {
+      if (p.epi.ln2_in) {
+        epilogue<T, EPI, EpiView<TL>, true, true>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
+                                                  rs_tab + pass * EpiView<TL>::BM, cd_tab,
+                                                  rs2_tab + pass * EpiView<TL>::BM, c23_tab);
+        done = true;
+      }
+    }
+    if (done) {
+    } else if (p.epi.ln_in || p.epi.ln_out)
       epilogue<T, EPI, EpiView<TL>, true>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
                                           rs_tab + pass * EpiView<TL>::BM, cd_tab);
     else
@@ -1367,6 +1536,9 @@ int g_gemm8 = [] { const char* s = getenv("CFM_GEMM8"); return s ? atoi(s) : 1; 
 int g_gemm8_dense = [] { const char* s = getenv("CFM_GEMM8_DENSE"); return s ? atoi(s) : 0; }();
 // write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
+// K-group tiles (KG > 1, >= 3 ring stages): the whole next K-step's fragments are read while the
+// current one multiplies (gemm_kernel's read-ahead loop); CFM_GEMM_AHEAD=0 keeps the substep pipeline
+int g_gemm_ahead = [] { const char* s = getenv("CFM_GEMM_AHEAD"); return s ? atoi(s) : 1; }();
 
 // Tile ids (CFM_GEMM_TILE / set_gemm_tile_override; other ids run tile 0):
 //   0 128x128 NS2 | 1 256x128 NS3 | 5 64x128 NS2          (128-byte K-steps, several blocks / CU)
@@ -1467,6 +1639,7 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
   p.ldw_b = (long)Kpad * es;
   p.kb = (int)((long)Kpad * es);
   p.probe = 0;
+  p.ahead = g_gemm_ahead;
   p.split_x = 0;
   p.Mtiles = p.Ntiles = 0;
   p.M = M;
@@ -1480,7 +1653,9 @@ GemmParams make_params(int es, int M, const void* Wp, int Kpad, int N, const Gem
 
 }  // namespace
 
-int g_gemm_probe = 0;
+// CFM_GEMM_PROBE: the cfm_bench_gemm probe bits on every dense / GLU GEMM of a run (timing studies only:
+// the outputs are garbage)
+int g_gemm_probe = [] { const char* s = getenv("CFM_GEMM_PROBE"); return s ? atoi(s) : 0; }();
 int set_gemm_probe(int probe) {
   const int prev = g_gemm_probe;
   g_gemm_probe = probe;
@@ -1496,6 +1671,9 @@ int set_gemm_tile_override(int tile) {
 void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int Kpad, int N, const GemmEpi& epi,
           const void* zero_page, hipStream_t st) {
   if (M <= 0) return;
+  if ((epi.xln_in && (epi.mode != EPI_RESID || !epi.ln_out)) || (epi.ln2_in && (epi.mode != EPI_SWISH || !epi.ln_in)) ||
+      (epi.ln2_out && (epi.mode != EPI_RESID || !epi.ln_out)))
+    fail(CFM_ERR_INVALID_ARG, "gemm: norm_out fold operands on the wrong epilogue");
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};
