@@ -167,6 +167,11 @@ def stage_breakdown(args, enc, dev, x, lengths, B, T, d, L, H, es):
     roof["traffic_unit"] = "bytes/launch (HBM, PMC)"
     if tr is not None:
         roof["traffic_source"] = tr["file"]
+    # the clock's own cost per kernel (empty kernels timed the same way), reported beside the sum
+    try:
+        breakdown["_clock_overhead_us"] = round(native.stage_clock_overhead_us(200), 3)
+    except Exception:  # noqa: BLE001 - an older library: no calibration entry
+        pass
     return roof, breakdown
 
 
@@ -428,9 +433,16 @@ def main():
         }
         if breakdown:
             # kernel durations only: the rest of ms_per_step is dispatch gaps between the kernels
+            ovh = breakdown.pop("_clock_overhead_us", None)
             bsum = sum(v["ms_total"] for v in breakdown.values())
             out["breakdown_sum"] = {"ms": round(bsum, 4), "of_ms_per_step": round(bsum / ms_step, 4),
                                     "clock": os.environ.get("CFM_STAGE_CLOCK", "packet")}
+            if ovh is not None:
+                # minus the clock's own begin -> end of an empty kernel, once per launch
+                nl = sum(v["launches"] for v in breakdown.values())
+                net = bsum - nl * ovh * 1e-3
+                out["breakdown_sum"].update({"clock_overhead_us_per_kernel": ovh, "launches": nl,
+                                             "ms_net": round(net, 4), "net_of_ms_per_step": round(net / ms_step, 4)})
         print(json.dumps(out), flush=True)
     if dist:
         torch.distributed.destroy_process_group()
@@ -571,6 +583,24 @@ def run_joint(args, world, rank, dev, dist, barrier):
     with torch.inference_mode():
         elapsed, out = timed_loop(step, args.warmup, args.steps, barrier)
         assert torch.isfinite(out[:1]).all().item()
+        # per-module device time (rank 0, after the timed loop): each module's call timed alone with
+        # stream events over a few repetitions, on the outputs of the timed step's inputs
+        parts = {}
+        if rank == 0 and not args.no_breakdown:
+            y, yl = enc(audio_signal=x, length=lengths)
+            pred, _, _ = dec(targets=targets, target_length=tlen)
+            calls = {"encoder": lambda: enc(audio_signal=x, length=lengths),
+                     "prediction_net": lambda: dec(targets=targets, target_length=tlen),
+                     "joint": lambda: joint(encoder_outputs=y, decoder_outputs=pred)}
+            for name, fn in calls.items():
+                fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(5):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                parts[name] = e0.elapsed_time(e1) / 5
     t_max = max_over_ranks(elapsed, dev, dist)
     ms_step = 1000.0 * t_max / args.steps
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -580,6 +610,24 @@ def run_joint(args, world, rank, dev, dist, barrier):
     f_joint = 2 * B * Tp * d * 640 + 2 * B * (U + 1) * 640 * 640 + 2 * B * Tp * (U + 1) * 640 * (V + 1)
     f_pred = 2 * B * (U + 1) * (2 * 640) * (4 * 640)
     tot = f_enc + f_joint + f_pred
+    breakdown = None
+    roof = None
+    if parts:
+        logit_bytes = B * Tp * (U + 1) * (V + 1) * 4
+        work = {"encoder": ("flop", f_enc), "prediction_net": ("flop", f_pred), "joint": ("flop", f_joint)}
+        breakdown = {}
+        for k, ms in parts.items():
+            kind, amt = work[k]
+            breakdown[k] = {"ms": round(ms, 4), "TFLOP/s": round(amt / (ms * 1e-3) / 1e12, 1)}
+        breakdown["joint"]["logits_GB/s"] = round(logit_bytes / (parts["joint"] * 1e-3) / 1e9, 1)
+        # the joint's bound: its GEMM FLOPs at the MFMA peak or its fp32 logits at the HBM peak
+        t_mfma = f_joint / (PEAK[args.compute] * 1e12) * 1e3
+        t_hbm = logit_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
+        roof = {"kernel": "joint (hidden + logits GEMM)", "bound": "hbm" if t_hbm >= t_mfma else "mfma",
+                "floor_ms": round(max(t_mfma, t_hbm), 4), "achieved_ms": round(parts["joint"], 4),
+                "frac": round(max(t_mfma, t_hbm) / parts["joint"], 4),
+                "note": f"{f_joint / 1e9:.0f} GFLOP at {PEAK[args.compute]} TFLOP/s = {t_mfma:.3f} ms; "
+                        f"{logit_bytes / 1e9:.2f} GB fp32 logits at {HBM_PEAK_GBS} GB/s = {t_hbm:.3f} ms"}
     emit(rank, dist, {
         "metric": JOINT_METRIC, "value": round(job_throughput(t_max, world, B, T, args.steps), 1),
         "unit": "audio-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -594,6 +642,7 @@ def run_joint(args, world, rank, dev, dist, barrier):
                         "joint_GFLOP": round(f_joint / 1e9, 1), "prediction_net_GFLOP": round(f_pred / 1e9, 2),
                         "TFLOP/s_per_gpu": round(tot / (ms_step * 1e-3) / 1e12, 1),
                         "frac_of_peak": round(tot / (ms_step * 1e-3) / 1e12 / PEAK[args.compute], 4)},
+        **({"breakdown": breakdown, "roofline": roof} if breakdown else {}),
     })
 
 

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "cfm_last_error", "cfm_version", "cfm_half_mode", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
     "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_abs_pos", "cfm_encoder_abs_pos", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
-    "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
+    "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_stage_clock_overhead", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
     "cfm_op_rel_attention", "cfm_bench_gemm", "cfm_encoder_layers_workspace_size", "cfm_encoder_layers_forward",
     "cfm_op_conv_glu_dwconv_ws_size", "cfm_op_conv_glu_dwconv",
 )
@@ -146,6 +146,7 @@ def load(variant: str = "bf16") -> ctypes.CDLL:
         "cfm_encoder_forward": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp]),
         "cfm_num_stages": (ci, []),
         "cfm_stage_name": (ctypes.c_char_p, [ci]),
+        "cfm_stage_clock_overhead": (ci, [vp, ci, ctypes.POINTER(ctypes.c_float)]),
         "cfm_encoder_forward_timed": (ci, [vp, vp, vp, ci, ci, vp, vp, vp, sz, vp, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(ci)]),
         "cfm_op_layernorm": (ci, [ci, vp, ci, ci, vp, vp, vp, vp, vp]),

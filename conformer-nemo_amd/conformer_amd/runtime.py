@@ -222,3 +222,12 @@ class NativeEncoder:
                                                       out_len.data_ptr(), ws.data_ptr(), nbytes, ctypes.c_void_p(stream),
                                                       ms, cnt), "cfm_encoder_forward_timed", lib=self.lib)
         return {self.lib.cfm_stage_name(i).decode(): (float(ms[i]), int(cnt[i])) for i in range(n)}
+
+    def stage_clock_overhead_us(self, n: int = 200) -> float:
+        """The stage clock's own cost per kernel (cfm_stage_clock_overhead): the mean begin -> end of n
+        empty one-wave kernels timed the way forward_timed times each kernel."""
+        us = ctypes.c_float(0.0)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self.lib.cfm_stage_clock_overhead(ctypes.c_void_p(stream), int(n), ctypes.byref(us)),
+                   "cfm_stage_clock_overhead", lib=self.lib)
+        return float(us.value)

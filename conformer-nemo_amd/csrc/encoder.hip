@@ -768,7 +768,6 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
     };
     // norm_out fold: layer l's norm_out is applied by layer l+1's FFN1 GEMMs (GemmEpi::ln2_in / xln_in)
     const bool fold2 = fold && h->ln_fold2;
-    static const int dbg2 = [] { const char* e = getenv("CFM_FOLD2_DBG"); return e ? atoi(e) : 0; }();
     float2* lns2 = fold2 ? (float2*)(ws + wl.LS2) : nullptr;
     float4* ln4 = fold2 ? (float4*)(ws + wl.LS4) : nullptr;
     const long ldp = (long)L * H * dkp;
@@ -780,8 +779,7 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
     for (int l = 0; l < L; ++l) {
       const LayerW& Lw = h->layers[l];
       // X / Hn hold the previous layer's output before its norm_out (y, bf16 copy), LS2 / LS4 its sums
-      const bool in2 = fold2 && l > 0 && dbg2 != 1 && dbg2 != 4;
-      const bool xin2 = fold2 && l > 0 && dbg2 != 1 && dbg2 != 3;
+      const bool in2 = fold2 && l > 0;
       // ---- FFN1 (conformer_modules.py:99-101) ----
       {
         TM(ST_FFN_UP);
@@ -796,7 +794,7 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff1_b2), 0.5f);
         r.X = X; r.ldx = d;
         produce(r);
-        if (xin2) {
+        if (in2) {
           const LayerW& Lp = h->layers[l - 1];
           r.xln_in = lns2; r.xln_g = Wf(Lp.ln_w[4]); r.xln_b = Wf(Lp.ln_b[4]); r.ln_width = d;
         }
@@ -910,16 +908,7 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
       }
       // ---- norm_out (conformer_modules.py:120), fused with the next layer's first LayerNorm ----
       const bool next = l + 1 < L;
-      if (fold2 && next && dbg2 == 3) {
-        layernorm(dt, X, M, d, Wf(Lw.ln_w[4]), Wf(Lw.ln_b[4]), X, nullptr, nullptr, nullptr, 0, st);
-        continue;
-      }
-      if (fold2 && next && dbg2 == 4) {
-        layernorm(dt, X, M, d, Wf(Lw.ln_w[4]), Wf(Lw.ln_b[4]), nullptr, Wf(h->layers[l + 1].ln_w[0]),
-                  Wf(h->layers[l + 1].ln_b[0]), Hn, 0, st);
-        continue;
-      }
-      if (fold2 && next && dbg2 != 1) continue;   // applied by the next layer's FFN1 GEMMs
+      if (fold2 && next) continue;   // applied by the next layer's FFN1 GEMMs
       const bool want_t = next || h->has_out_proj;
       TM(ST_LN);
       layernorm(dt, X, M, d, Wf(Lw.ln_w[4]), Wf(Lw.ln_b[4]), X, next ? Wf(h->layers[l + 1].ln_w[0]) : nullptr,
@@ -1040,8 +1029,6 @@ void run_split(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, 
     const int bi = B / n + (i < B % n ? 1 : 0);
     hipStream_t si = h->sub_streams[i];
     HIP_OK(hipStreamWaitEvent(si, h->sub_events[0], 0));
-    static const bool serial = [] { const char* e = getenv("CFM_MB_SERIAL"); return e && atoi(e); }();
-    if (serial && i > 0) HIP_OK(hipStreamWaitEvent(si, h->sub_events[i], 0));   // debug: parts one after another
     run_forward(h, x_bft + (long)b0 * h->F * T, len_b ? len_b + b0 : nullptr, bi, T,
                 y_bdt + (long)b0 * h->dout * Tp, out_len_b + b0, ws + (long)i * wl.total, wl.total, si, nullptr,
                 h->L > 0 ? P : nullptr);
@@ -1144,6 +1131,28 @@ cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const i
       run_forward(h, x_bft, len_b, B, T, y_bdt, out_len_b, workspace, workspace_bytes, (hipStream_t)stream, &tm);
     }
     tm.finish(stage_ms, stage_launches);
+  });
+}
+
+__global__ void clock_probe_kernel(float* sink) {
+  if (sink && threadIdx.x == 0) sink[blockIdx.x] = 0.0f;
+}
+
+cfm_status cfm_stage_clock_overhead(void* stream, int n, float* us_per_kernel) {
+  return guarded([&] {
+    if (n <= 0 || !us_per_kernel) fail(CFM_ERR_INVALID_ARG, "n > 0 and a result pointer");
+    StageTimer tm;
+    {
+      ClockGuard g(&tm);
+      for (int i = 0; i < n; ++i) {
+        tm.mark(0);
+        cfm_launch(clock_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (float*)nullptr);
+      }
+    }
+    std::vector<float> ms(ST_COUNT, 0.0f);
+    std::vector<int> cnt(ST_COUNT, 0);
+    tm.finish(ms.data(), cnt.data());
+    *us_per_kernel = cnt[0] ? 1e3f * ms[0] / (float)cnt[0] : 0.0f;
   });
 }
 

@@ -856,7 +856,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   if constexpr (EPI == EPI_SWISH) {
     // norm_out fold: both LayerNorms' row statistics, computed while the first stages land (the
     // tables sit behind the ring and the epilogue image; read after the epilogue's first barrier)
-    if (p.epi.ln2_in && !(p.probe & 32)) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
+    if (p.epi.ln2_in) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
   }
   if constexpr (kAheadTile) {
     if (ahead) {
@@ -994,9 +994,6 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   // folded LayerNorm: (mean, rstd) of row tid from its granule partials (Chan et al.'s pairwise
   // combination of (count, mean, M2)) and (c, d) of column tid, from the values prefetched at the
   // kernel start; visible after the first pass's barrier
-  if constexpr (EPI == EPI_SWISH) {   // debug probe 32: the norm_out fold tables after the main loop
-    if (p.epi.ln2_in && (p.probe & 32)) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
-  }
   if (ln_src && !p.epi.ln2_in) {
     const int W = p.epi.ln_width, np = p.epi.ln_parts;
     const float2* pp = ln_src + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
@@ -1538,7 +1535,7 @@ int g_gemm8_dense = [] { const char* s = getenv("CFM_GEMM8_DENSE"); return s ? a
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 // K-group tiles (KG > 1, >= 3 ring stages): the whole next K-step's fragments are read while the
 // current one multiplies (gemm_kernel's read-ahead loop); CFM_GEMM_AHEAD=0 keeps the substep pipeline
-int g_gemm_ahead = [] { const char* s = getenv("CFM_GEMM_AHEAD"); return s ? atoi(s) : 1; }();
+int g_gemm_ahead = [] { const char* s = getenv("CFM_GEMM_AHEAD"); return s ? atoi(s) : 0; }();
 
 // Tile ids (CFM_GEMM_TILE / set_gemm_tile_override; other ids run tile 0):
 //   0 128x128 NS2 | 1 256x128 NS3 | 5 64x128 NS2          (128-byte K-steps, several blocks / CU)

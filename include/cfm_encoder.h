@@ -172,6 +172,9 @@ const char* cfm_stage_name(int i);
 cfm_status cfm_encoder_forward_timed(cfm_encoder* h, const float* x_bft, const int32_t* len_b, int B, int T,
                                      float* y_bdt, int32_t* out_len_b, void* workspace, size_t workspace_bytes,
                                      void* stream, float* stage_ms, int* stage_launches);
+/* The stage clock's own cost: n empty one-wave kernels timed exactly as forward_timed times a kernel
+ * (same CFM_STAGE_CLOCK mode); *us_per_kernel = their mean begin -> end (us).  Synchronises. */
+cfm_status cfm_stage_clock_overhead(void* stream, int n, float* us_per_kernel);
 
 /* ---- kernel-level entry points (used by the per-kernel parity tests) ---------------------- */
 /* All buffers are device pointers; `dtype` is CFM_COMPUTE_FP32 (float) or CFM_COMPUTE_BF16 (uint16 bf16). */

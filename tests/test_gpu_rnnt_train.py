@@ -134,3 +134,61 @@ def test_rnnt_training_step_trains(tmp_path):
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0], losses
+
+
+def _recipe_modules(z, compute):
+    """rnnt_train_h640.npz (gen_rnnt_train_h640_golden.py): the weights are replayed from the fixture's
+    recipe - one torch.randn per parameter in the reference's named_parameters order (`porder`), scaled
+    by 1/sqrt(fan_in) (0.1 for vectors), the embedding's padding row zeroed."""
+    from nemo.collections.asr.modules import RNNTDecoder, RNNTJoint
+    V, Hp, L, H1, J = (int(v) for v in z["meta"][:5])
+    dec = RNNTDecoder(prednet=dict(pred_hidden=Hp, pred_rnn_layers=L, dropout=0.0), vocab_size=V)
+    joint = RNNTJoint(jointnet=dict(encoder_hidden=H1, pred_hidden=Hp, joint_hidden=J, activation=str(z["act"])),
+                      num_classes=V, log_softmax=False)
+    mods = {"dec": dec, "joint": joint}
+    sds = {n: m.state_dict() for n, m in mods.items()}
+    g = torch.Generator().manual_seed(int(z["wseed"]))
+    new = {"dec": {}, "joint": {}}
+    for full in z["porder"]:
+        mname, key = str(full).split(".", 1)
+        shape = sds[mname][key].shape
+        scale = 1.0 / float(np.sqrt(shape[-1])) if len(shape) > 1 else 0.1
+        new[mname][key] = torch.randn(shape, generator=g) * scale
+    new["dec"]["prediction.embed.weight"][V].zero_()
+    for n, m in mods.items():
+        m.load_state_dict({k: new[n].get(k, v) for k, v in sds[n].items()})
+    joint.set_compute_mode(compute)
+    return dec.cuda().eval(), joint.cuda().eval()
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_prediction_net_and_joint_gradients_h640(compute):
+    """The config-4 widths (pred / joint hidden 640, U = 24 labels, tanh joint) against the reference's
+    autograd (tests/golden/rnnt_train_h640.npz): logits and d(enc) in full, the 640-wide weight gradients
+    on a fixed 16,384-element sample plus their full norms.  tanh has no mask to flip, so bf16 keeps a
+    tight gate (2e-2) on every gradient."""
+    z = np.load(os.path.join(GOLDEN, "rnnt_train_h640.npz"))
+    dec, joint = _recipe_modules(z, compute)
+    enc = torch.from_numpy(z["enc"]).cuda().requires_grad_(True)
+    y = torch.from_numpy(z["y"]).cuda()
+    yl = torch.full((y.shape[0],), y.shape[1], dtype=torch.int64, device="cuda")
+    g, _, _ = dec(targets=y, target_length=yl)
+    out = joint(encoder_outputs=enc, decoder_outputs=g)
+    tol = 1e-4 if compute == "fp32" else 2e-2
+    assert rel_l2(out.detach().cpu().numpy(), z["logits"]) < tol
+    (out * torch.from_numpy(z["G"]).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    errs = {"enc": rel_l2(enc.grad.cpu().numpy(), z["g::enc"])}
+    for name, m in (("dec", dec), ("joint", joint)):
+        for k, p in m.named_parameters():
+            assert p.grad is not None, f"{name}.{k} has no gradient"
+            gr = p.grad.detach().float().cpu().numpy()
+            if f"g::{name}.{k}" in z.files:
+                errs[f"{name}.{k}"] = rel_l2(gr, z[f"g::{name}.{k}"])
+            else:
+                flat = gr.reshape(-1)
+                errs[f"{name}.{k}[sample]"] = rel_l2(flat[z[f"gi::{name}.{k}"]], z[f"gs::{name}.{k}"])
+                ref_n = float(z[f"gn::{name}.{k}"])
+                errs[f"{name}.{k}[norm]"] = abs(float(np.linalg.norm(flat.astype(np.float64))) - ref_n) / ref_n
+    bad = {k: e for k, e in errs.items() if e > tol}
+    assert not bad, f"h640/{compute}: " + ", ".join(f"{k} {e:.2e}" for k, e in sorted(bad.items()))
