@@ -594,8 +594,9 @@ __global__ __launch_bounds__(NW * 64) void rel_attn_lds_kernel(AttnParams p) {
   }
   __syncthreads();
 
+  // query tiles: blockIdx.y of gridDim.y blocks per (b, h) (each stages the whole K / Vt), NW waves each
   const int nqt = (Tp + 31) / 32;
-  for (int qt = wave; qt < nqt; qt += NW) {
+  for (int qt = blockIdx.y * NW + wave; qt < nqt; qt += NW * gridDim.y) {
     const int i0 = qt * 32;
     uint4 qu[NS], qv[NS];
     {
@@ -916,12 +917,21 @@ bool launch_lds(const AttnParams& p, int B, hipStream_t st) {
   static const int force_nw = [] { const char* s = getenv("CFM_ATTN_NW"); return s ? atoi(s) : 0; }();
   const LdsGeom g8 = lds_geom(p.Tp, p.dkp, p.vt_rows, 8);
   const LdsGeom g4 = lds_geom(p.Tp, p.dkp, p.vt_rows, 4);
+  // fewer (b, h) pairs than CUs: split each pair's query tiles over blocks (every block stages the
+  // whole K / Vt; the tiles are computed exactly as by one block)
+  const int nqt = (p.Tp + 31) / 32;
+  static const bool split_ok = [] { const char* e = getenv("CFM_ATTN_QSPLIT"); return !(e && !atoi(e)); }();
+  auto qsplit = [&](int nw) {
+    if (!split_ok) return 1;
+    const int want = 256 / std::max(B * p.H, 1);
+    return std::max(1, std::min(want, (nqt + nw - 1) / nw));
+  };
   if (force_nw != 4 && g8.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, (NS <= 4), QN>), dim3(B * p.H), dim3(512), g8.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 8, (NS <= 4), QN>), dim3(B * p.H, qsplit(8)), dim3(512), g8.bytes, st, p);
     return true;
   }
   if (g4.bytes <= LDS_MAX) {
-    cfm_launch((rel_attn_lds_kernel<NS, ND, 4, true, QN>), dim3(B * p.H), dim3(256), g4.bytes, st, p);
+    cfm_launch((rel_attn_lds_kernel<NS, ND, 4, true, QN>), dim3(B * p.H, qsplit(4)), dim3(256), g4.bytes, st, p);
     return true;
   }
   return false;

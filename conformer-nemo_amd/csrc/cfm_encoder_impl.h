@@ -61,7 +61,7 @@ struct cfm_encoder {
   // following GEMM (the residual GEMM before each writes the compute-type rows and per-row granule
   // statistics); off in the fp32 parity mode (CFM_LN_FOLD=0/1 overrides for A/B).
   bool ln_fold = false;
-  // bf16 eval forward with T' <= 256: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish as
+  // bf16 eval forward with T' <= 678: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish as
   // one launch (gemm_glu_dw); CFM_GLU_DW=0 keeps the two launches (A/B)
   bool fuse_glu_dw = true;
   bool fuse_conv12 = true;     // conv.0 on the matrix cores inside conv.2's implicit GEMM (CFM_CONV12=0: two kernels)

@@ -60,7 +60,8 @@ enum Epilogue {
   EPI_GLU_MASK = 5,    // C[m, c] = (a + ba) * sigmoid(g + bg), zero for padded frames (GLU-packed W)
   EPI_QKV = 6,         // packed cols [q | k | v]: C = [q+u | q+v | k] (ldc = 3*H*dkp), v -> Vt[(b*H+h)][d][t]
   EPI_GLU_DW = 7,      // EPI_GLU_MASK + depthwise conv (k 31) + BatchNorm (running stats) + Swish on an
-                       // utterance-aligned 256-row tile (utt_tp <= 256 frames): C = conv module's S rows
+                       // utterance-aligned 256-row tile (one per utterance at T' <= 256, else tiles of 226
+                       // output frames with 15 context frames either side): C = conv module's S rows
   EPI_SWISH_BWD = 8,   // training: C (compute type) = acc * dropout'(m*ldz + n) * swish'(zin[m][n]), the
                        // FFN hidden's backward through Swish and its dropout (conformer_modules.py:196-198)
   EPI_SWISH_Z = 9,     // training: C = z = acc + bias and C2 = dropout(swish(z)) (mask index m*ldc + n), both
@@ -151,6 +152,7 @@ struct GemmEpi {
   // Utterance-aligned rows (EPI_GLU_DW): GEMM row m is frame t = m % 256 of utterance b = m / 256,
   // A / output row b * utt_tp + t (t < utt_tp; utt_M real rows); 0 = rows are plain.
   int utt_tp, utt_M;
+  int utt_nt, utt_out, utt_halo;   // tiles per utterance, output frames per tile, context frames either side
   const float* dw_w;   // EPI_GLU_DW: depthwise weight [31][d], bias [d], BatchNorm mean / 1/sqrt(var+eps) / w / b
   const float* dw_b;
   const float *bn_mean, *bn_inv, *bn_w, *bn_b;
@@ -201,7 +203,7 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
 void gemm_tconv(int dtype, const TConvGeom& g, const void* Wp, int Kpad, int N, const GemmEpi& epi,
                 const void* zero_page, hipStream_t st);
 // pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish in one launch (bf16, epi.mode = EPI_GLU_DW,
-// epi.utt_tp = T' <= 256, N = d, d % 64 == 0): one 256x128 tile per (utterance, 64 channels).
+// epi.utt_tp = T' <= 678, N = d, d % 64 == 0): 256x128 tiles per (utterance, 64 channels), 1-3 per utterance.
 bool gemm_glu_dw_supported(int dtype, int Tp, int d, int K);
 void gemm_glu_dw(int dtype, const void* A, long lda, int B, int Tp, int K, const void* Wp, int Kpad, int N,
                  const GemmEpi& epi, const void* zero_page, hipStream_t st);

@@ -112,7 +112,9 @@ template <int G>
 struct ALoadDense {
   static constexpr bool kConv = false;
   const char* A; long lda_b; int M; long kbytes; const char* zero;
-  int utt_tp, utt_rows;   // utterance-aligned rows (GemmEpi::utt_tp): m -> (m / utt_rows) * utt_tp + m % utt_rows
+  // utterance-aligned rows (GemmEpi::utt_tp): tile i = m / utt_rows is tile j = i % utt_nt of utterance
+  // b = i / utt_nt, its row r = m % utt_rows frame t = j * utt_out - utt_halo + r (valid in [0, utt_tp))
+  int utt_tp, utt_rows, utt_nt, utt_out, utt_halo;
   struct State { const char* row_ptr[G]; };
   CFM_DEV void shift_k(long koff) { A += koff; kbytes -= koff; }
   CFM_DEV void prepare(State& s, int m0, const int* rows) const {
@@ -121,9 +123,10 @@ struct ALoadDense {
       int m = m0 + rows[i];
       bool ok = m < M;
       if (utt_tp > 0) {
-        const int b = m / utt_rows, t = m - b * utt_rows;
+        const int ti = m / utt_rows, r = m - ti * utt_rows;
+        const int b = ti / utt_nt, t = (ti - b * utt_nt) * utt_out - utt_halo + r;
         m = b * utt_tp + t;
-        ok = t < utt_tp && m < M;
+        ok = t >= 0 && t < utt_tp && m < M;
       }
       s.row_ptr[i] = ok ? A + (long)m * lda_b : nullptr;
     }
@@ -250,8 +253,9 @@ struct GemmParams {
 // (GemmEpi::utt_tp, tile height BM) frame m % BM of utterance m / BM.
 CFM_DEV int real_row(const GemmParams& p, int m, int BM) {
   if (p.epi.utt_tp <= 0) return min(m, p.M - 1);
-  const int b = m / BM, t = m - b * BM;
-  return min(b * p.epi.utt_tp + min(t, p.epi.utt_tp - 1), p.epi.utt_M - 1);
+  const int ti = m / BM, r = m - ti * BM;
+  const int b = ti / p.epi.utt_nt, t = (ti - b * p.epi.utt_nt) * p.epi.utt_out - p.epi.utt_halo + r;
+  return min(b * p.epi.utt_tp + min(max(t, 0), p.epi.utt_tp - 1), p.epi.utt_M - 1);
 }
 
 // Folded LayerNorm (GemmEpi::ln_in): rs[r] = (mean, rstd) of the pass's local row r, cd[j] = (c, d)
@@ -425,7 +429,9 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       const int cc = tid % CPR, r0 = tid / CPR;
       const int oc_local = cc * VE;
       const int ca = (oc_local / 32) * 64 + oc_local % 32, cg = ca + 32;
-      const int b = m0 / 256, Tp = e.utt_tp;
+      // tile j of utterance b: row r is frame f0 + r (T' > 256: tiles of utt_out frames with utt_halo
+      // frames of context either side; the conv's zero padding outside [0, len))
+      const int ti = m0 / 256, b = ti / e.utt_nt, f0 = (ti - b * e.utt_nt) * e.utt_out - e.utt_halo, Tp = e.utt_tp;
       const int len = e.lens ? min(e.lens[b], Tp) : Tp;   // frames >= T' are zero padding of the conv
       float gv[NP][VE];
 #pragma unroll
@@ -438,7 +444,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           float a = img[r * TL::EPS + ca + i];
           float g = img[r * TL::EPS + cg + i];
           if constexpr (fold) { a = ln_fold(st, a, cd[ca + i]); g = ln_fold(st, g, cd[cg + i]); }
-          gv[q][i] = r < len ? a * sigmoidf_(g) : 0.0f;
+          gv[q][i] = (f0 + r >= 0 && f0 + r < len) ? a * sigmoidf_(g) : 0.0f;
         }
       }
       __syncthreads();                     // every wave has read the accumulator image
@@ -484,8 +490,9 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       constexpr int VO = 16 / (int)sizeof(T);            // channels per 16-byte run
       for (int i = tid; i < 256 * 64 / VO; i += TL::NT) {
         const int t = i / (64 / VO), c8 = (i % (64 / VO)) * VO;
-        if (t < Tp && n0 / 2 + c8 < p.N)
-          *(uint4*)((T*)e.C + ((long)b * Tp + t) * e.ldc + n0 / 2 + c8) = *(const uint4*)(simg + t * 64 + c8);
+        const int ft = f0 + t;
+        if (t >= e.utt_halo && t < e.utt_halo + e.utt_out && ft < Tp && n0 / 2 + c8 < p.N)
+          *(uint4*)((T*)e.C + ((long)b * Tp + ft) * e.ldc + n0 / 2 + c8) = *(const uint4*)(simg + t * 64 + c8);
       }
     }
   } else if constexpr (EPI == EPI_GLU_MASK) {
@@ -1507,9 +1514,10 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
 
 struct DenseArgs {
   const char* A; long lda_b; int M; long kbytes; const char* zero;
-  int utt_tp = 0, utt_rows = 0;
+  int utt_tp = 0, utt_rows = 0, utt_nt = 1, utt_out = 0, utt_halo = 0;
   template <class AL> void fill(AL& al) const {
     al.A = A; al.lda_b = lda_b; al.M = M; al.kbytes = kbytes; al.zero = zero; al.utt_tp = utt_tp; al.utt_rows = utt_rows;
+    al.utt_nt = utt_nt; al.utt_out = utt_out; al.utt_halo = utt_halo;
   }
 };
 struct ConvArgs {
@@ -1728,23 +1736,33 @@ void gemm_splitk(int dtype, const void* A, long lda, int M, int K, const void* W
   g_splits = 1;
 }
 
+// T' <= 256: one 256-row tile per utterance; up to 3 tiles of 226 output frames with 15 frames of
+// context either side (the depthwise conv's reach) up to T' = 678
+constexpr int kGluTileOut = 256 - 2 * 15;
 bool gemm_glu_dw_supported(int dtype, int Tp, int d, int K) {
-  return dtype == DT_BF16 && Tp >= 1 && Tp <= 256 && d % 64 == 0 && K == 31;
+  return dtype == DT_BF16 && Tp >= 1 && Tp <= 3 * kGluTileOut && d % 64 == 0 && K == 31;
 }
 
 void gemm_glu_dw(int dtype, const void* A, long lda, int B, int Tp, int K, const void* Wp, int Kpad, int N,
                  const GemmEpi& epi, const void* zero_page, hipStream_t st) {
   if (B <= 0) return;
   if (!gemm_glu_dw_supported(dtype, Tp, N, 31) || epi.mode != EPI_GLU_DW || epi.utt_tp != Tp)
-    fail(CFM_ERR_UNSUPPORTED, "gemm_glu_dw: bf16, T' <= 256, d % 64 == 0 only");
+    fail(CFM_ERR_UNSUPPORTED, "gemm_glu_dw: bf16, T' <= 678, d % 64 == 0 only");
   using TL = T256x128;
-  GemmParams p = make_params(2, B * TL::BM, Wp, Kpad, N, epi);
+  const int nt = Tp <= TL::BM ? 1 : (Tp + kGluTileOut - 1) / kGluTileOut;
+  GemmParams p = make_params(2, B * nt * TL::BM, Wp, Kpad, N, epi);
   p.probe = g_gemm_probe;
   p.epi.utt_M = B * Tp;
+  p.epi.utt_nt = nt;
+  p.epi.utt_out = nt == 1 ? TL::BM : kGluTileOut;
+  p.epi.utt_halo = nt == 1 ? 0 : 15;
   DenseArgs a{(const char*)A, lda * 2, B * Tp, (long)K * 2, (const char*)zero_page};
   a.utt_tp = Tp;
   a.utt_rows = TL::BM;
-  p.Mtiles = B;
+  a.utt_nt = p.epi.utt_nt;
+  a.utt_out = p.epi.utt_out;
+  a.utt_halo = p.epi.utt_halo;
+  p.Mtiles = B * nt;
   p.Ntiles = packed_width(epi, N) / TL::BN;
   ALoadDense<TL::GA> al;
   a.fill(al);

@@ -247,7 +247,7 @@ def test_bf16_layernorm_fold_matches_unfolded(path, monkeypatch):
 @pytest.mark.parametrize("path", [f for f in ENC_FILES if "large17" in f or "tiny_ctx" in f or "nopadmask" in f
                                   or "xl_h8" in f], ids=lambda f: os.path.basename(f)[4:-4])
 def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
-    """bf16, T' <= 256: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish run as one launch
+    """bf16: pointwise_conv1 + GLU + depthwise conv + BatchNorm + Swish run as one launch
     (gemm_glu_dw, the GLU output stays in LDS); CFM_GLU_DW=0 keeps the GLU GEMM + dwconv kernel.
     Both meet the bf16 gate and agree to bf16 rounding (the fused conv reads the unrounded GLU)."""
     z = np.load(path)
@@ -262,6 +262,34 @@ def test_bf16_fused_conv_module_matches_unfused(path, monkeypatch):
     d = rel_l2(out["1"][0], out["0"][0])
     print(f"bf16 relL2 vs reference: fused {out['1'][1]:.3e}, unfused {out['0'][1]:.3e}; fused vs unfused {d:.3e}")
     assert d <= 1e-2, f"fused vs unfused relL2 {d:.3e}"
+
+
+# T' > 256: the fused conv module runs 2-3 tiles of 226 output frames per utterance with 15 frames of
+# context either side (halos at every tile edge, ragged lengths cutting tiles, T' = 600 -> 3 tiles)
+GLU_HALO_CASES = {
+    "d256_tp600_ragged": (dict(d_model=256, n_heads=4, n_layers=2), 3, 2400, [2400, 1500, 907]),
+    "d512_tp400": (dict(d_model=512, n_heads=8, n_layers=1), 2, 1600, [1600, 1213]),
+    "d256_tp257": (dict(d_model=256, n_heads=4, n_layers=1), 2, 1028, [1028, 1021]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(GLU_HALO_CASES))
+def test_bf16_fused_conv_module_halo_tiles(case, monkeypatch):
+    """bf16, T' > 256: gemm_glu_dw's halo tiles against the oracle and against the GLU GEMM + dwconv pair."""
+    cfg, B, T, lens = GLU_HALO_CASES[case]
+    sd = make_state_dict(cfg, 5)
+    x, lens = make_inputs(B, T, seed=23, lengths=lens)
+    yr, ylr = O.encoder_forward(x, lens, sd, cfg)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CFM_GLU_DW", flag)
+        y, yl = run(native(cfg, "bf16"), sd, x, lens)
+        np.testing.assert_array_equal(yl, ylr)
+        out[flag] = (y, check(y, yr, "bf16"))
+    d = rel_l2(out["1"][0], out["0"][0])
+    print(f"{case}: bf16 relL2 vs oracle: fused {out['1'][1]:.3e}, two kernels {out['0'][1]:.3e}; between {d:.3e}")
+    assert d <= 1e-2, f"fused vs two-kernel relL2 {d:.3e}"
+    assert out["1"][1] <= 1.1 * out["0"][1] + 1e-4
 
 
 # (cfg, B, T, lengths) cases that take the fused QKV + attention launch (dkp = 64, d in {256, 512},
