@@ -132,12 +132,106 @@ __global__ __launch_bounds__(256) void joint_hidden_kernel(const float* __restri
     }
   }
 }
+// As joint_hidden_kernel for H % 8 == 0 and Hp <= 1024, with the loads batched: thread (hg, group) keeps
+// f's 8-column chunk hg (and the tail W chunk) in registers and issues the g chunks of all its u's
+// (u = group + k * groups) before any arithmetic, so a block's memory traffic is in flight at once.
+// The same values and the same tail partials as joint_hidden_kernel (bitwise).
+template <typename TO>
+__global__ __launch_bounds__(256) void joint_hidden_batched_kernel(const float* __restrict__ f,
+                                                                   const float* __restrict__ g, int B, int T, int U,
+                                                                   int H, int Hp, int act, TO* __restrict__ out,
+                                                                   Drop drop, int ntail, const TO* __restrict__ wt,
+                                                                   long ldw, const float* __restrict__ bt,
+                                                                   float* __restrict__ lo, long ldo) {
+  __shared__ float tred[kTailMax * kHidU * 128];
+  constexpr int UPG = kHidU / 2;                    // u's per group (>= 2 groups since Hp <= 1024)
+  const int HG = Hp / 8;
+  const int ngrp = 256 / HG;
+  const int bt_ = blockIdx.x;
+  const int b = bt_ / T;
+  const int u0 = blockIdx.y * kHidU;
+  const int nu = min(kHidU, U - u0);
+  const int hg = threadIdx.x % HG, grp = threadIdx.x / HG;
+  const int h0 = hg * 8;
+  const bool hok = h0 < H;                          // columns H..Hp-1: zero padding
+  const int hc = hok ? h0 : 0;
+  if (grp < ngrp) {
+    const float* fr = f + (long)bt_ * H + hc;
+    const float4 f0 = *(const float4*)fr, f1 = *(const float4*)(fr + 4);
+    float4 ga[UPG], gb[UPG];
+#pragma unroll
+    for (int k = 0; k < UPG; ++k) {
+      const int uu = min(grp + k * ngrp, nu - 1);
+      const float* gr = g + ((long)b * U + u0 + uu) * H + hc;
+      ga[k] = *(const float4*)gr;
+      gb[k] = *(const float4*)(gr + 4);
+    }
+    float wtail[kTailMax][8] = {};
+    if constexpr (sizeof(TO) == 2) {
+      if (ntail > 0) {   // block-uniform
+#pragma unroll
+        for (int c = 0; c < kTailMax; ++c)
+          Vec16<bf16_t>::to_f32(*(const uint4*)(wt + (long)min(c, ntail - 1) * ldw + h0), wtail[c]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UPG; ++k) {
+      const int uu = grp + k * ngrp;
+      if (uu >= nu) continue;
+      const long row = (long)bt_ * U + u0 + uu;
+      float v[8] = {f0.x + ga[k].x, f0.y + ga[k].y, f0.z + ga[k].z, f0.w + ga[k].w,
+                    f1.x + gb[k].x, f1.y + gb[k].y, f1.z + gb[k].z, f1.w + gb[k].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = v[e];
+        if (act == CFM_JOINT_RELU) x = fmaxf(x, 0.0f);
+        else if (act == CFM_JOINT_SIGMOID) x = 1.0f / (1.0f + expf(-x));
+        else x = tanhf(x);
+        v[e] = hok ? x * drop_mul(drop, (uint64_t)row * H + h0 + e) : 0.0f;
+      }
+      TO* o = out + row * Hp + h0;
+      if constexpr (sizeof(TO) == 2) {
+        const uint4 packed = Vec16<bf16_t>::from_f32(v);
+        *(uint4*)o = packed;
+        if (ntail > 0) {
+          float vr[8];
+          Vec16<bf16_t>::to_f32(packed, vr);
+          for (int c = 0; c < ntail; ++c) {
+            float a = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a = fmaf(vr[e], wtail[c][e], a);
+            tred[(c * kHidU + uu) * 128 + hg] = a;
+          }
+        }
+      } else {
+        *(uint4*)o = Vec16<float>::from_f32(v);
+        *(uint4*)(o + 4) = Vec16<float>::from_f32(v + 4);
+      }
+    }
+  }
+  if (ntail > 0) {
+    __syncthreads();
+    for (int t = threadIdx.x; t < nu * ntail; t += 256) {
+      const int uu = t / ntail, c = t - uu * ntail;
+      float a = 0.0f;
+      for (int q = 0; q < HG; ++q) a += tred[(c * kHidU + uu) * 128 + q];
+      lo[((long)bt_ * U + u0 + uu) * ldo + c] = a + bt[c];
+    }
+  }
+}
+
 template <typename TO>
 void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, int Hp, int act, TO* out, Drop drop,
                   hipStream_t st, int ntail = 0, const TO* wt = nullptr, long ldw = 0, const float* bt = nullptr,
                   float* lo = nullptr, long ldo = 0) {
-  cfm_launch(joint_hidden_kernel<TO>, dim3((unsigned)(B * T), (unsigned)((U + kHidU - 1) / kHidU)), dim3(256), 0, st,
-             f, g, B, T, U, H, Hp, act, out, drop, ntail, wt, ldw, bt, lo, ldo);
+  static const bool batched = [] { const char* e = getenv("CFM_JOINT_HID_BATCHED"); return !(e && !atoi(e)); }();
+  const dim3 grid((unsigned)(B * T), (unsigned)((U + kHidU - 1) / kHidU));
+  if (batched && H % 8 == 0 && Hp <= 1024 && Hp % 8 == 0)
+    cfm_launch(joint_hidden_batched_kernel<TO>, grid, dim3(256), 0, st, f, g, B, T, U, H, Hp, act, out, drop, ntail,
+               wt, ldw, bt, lo, ldo);
+  else
+    cfm_launch(joint_hidden_kernel<TO>, grid, dim3(256), 0, st, f, g, B, T, U, H, Hp, act, out, drop, ntail, wt, ldw,
+               bt, lo, ldo);
 }
 
 // in-place log_softmax over rows of C fp32 values, one wave per row
