@@ -313,15 +313,24 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           const long g0 = xoff + (long)m * e.ldx + n0;
           const int lead = min((int)(((16 - ((uintptr_t)(e.X + g0) & 15)) & 15) >> 2), ncols);   // fp32 base: 4-B aligned
           const int nfull = (ncols - lead) / 4;
+          const int ntl = ncols - lead - 4 * nfull;   // < 4 trailing elements
           const float* ir = img + r * TL::EPS;
           if (cc < nfull) {
             const int j = lead + 4 * cc;
             *(float4*)(e.X + g0 + j) = make_float4(ir[j] * e.alpha, ir[j + 1] * e.alpha, ir[j + 2] * e.alpha,
                                                    ir[j + 3] * e.alpha);
-          } else if (cc == CPR - 1) {
-            for (int j = 0; j < lead; ++j) e.X[g0 + j] = ir[j] * e.alpha;
-            for (int j = lead + 4 * nfull; j < ncols; ++j) e.X[g0 + j] = ir[j] * e.alpha;
           }
+          if (e.out_scalar == 2) {   // A/B: the round-3 form, one thread storing all heads and tails
+            if (cc == CPR - 1) {
+              for (int j = 0; j < lead; ++j) e.X[g0 + j] = ir[j] * e.alpha;
+              for (int j = lead + 4 * nfull; j < ncols; ++j) e.X[g0 + j] = ir[j] * e.alpha;
+            }
+            continue;
+          }
+          // the <= 3 leading and <= 3 trailing elements: one element per lane (lanes 0.. and ..CPR-1),
+          // one store instruction for all of them
+          const int j1 = cc < lead ? cc : (cc >= CPR - ntl ? lead + 4 * nfull + (cc - (CPR - ntl)) : -1);
+          if (j1 >= 0 && CPR >= 8) e.X[g0 + j1] = ir[j1] * e.alpha;
         }
         return;
       }

@@ -276,7 +276,10 @@ GemmEpi epi_f32(const float* bias, float* X, long ldx, int scalar) {
   e.alpha = 1.0f;
   e.X = X;
   e.ldx = ldx;
-  e.out_scalar = scalar;
+  // unaligned rows: out_scalar 1 = heads / tails one element per lane; CFM_LOGITS_STORE=1 keeps the
+  // round-3 single-thread form (A/B)
+  static const int legacy = [] { const char* v = getenv("CFM_LOGITS_STORE"); return v ? atoi(v) : 0; }();
+  e.out_scalar = scalar ? (legacy == 1 ? 2 : 1) : 0;
   return e;
 }
 
