@@ -106,7 +106,8 @@ def main(argv):
         per_fw = tot / nf
         per_launch = tot / cnt
         kind, amt = work.get(st, ("byte", 0))
-        rate = amt / (per_launch * 1e-6) / (1e12 if kind == "flop" else 1e9) if amt else None
+        t_work = per_fw if st in bench.WORK_PER_FORWARD else per_launch
+        rate = amt / (t_work * 1e-6) / (1e12 if kind == "flop" else 1e9) if amt else None
         frac = rate / PEAK_TF if (rate and kind == "flop") else None
         u = util.get(st)
         res["stages"][st] = {"launches_per_forward": cnt // nf, "us_per_launch": round(per_launch, 2),

@@ -36,7 +36,9 @@ def stage_of(name, state):
         return "dwconv_bn_swish"
     if name.startswith("transpose_kernel"):
         return "output"
-    if "gemm8_kernel" in name:          # the 8-phase conv2 implicit GEMM
+    if "gemm8_kernel" in name or name.startswith(("conv12_kernel", "cfm::(anonymous namespace)::conv12_kernel")):
+        return "conv2_gemm"             # the 8-phase conv2 implicit GEMM (with conv.0 fused: conv12_kernel)
+    if "conv12_patch_kernel" in name:   # the fused front end's per-pixel input patches (bench: conv2 stage)
         return "conv2_gemm"
     m = re.match(r"(?:void )?(?:cfm::)?(?:\(anonymous namespace\)::)?gemm_kernel<[^,]+, (\d+),", name)
     if m:
