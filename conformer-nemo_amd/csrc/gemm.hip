@@ -1603,7 +1603,10 @@ int pick_tile(int dtype, int M, int Nw, int epi, bool conv, int K = 0) {
     // K-grouped tiles split each 128-byte K-step's substeps {0,1} | {2,3} between the groups, so
     // the small-M residual tile must be K-grouped the same way: an utterance's output is then
     // bitwise independent of the batch it runs in (tests/test_gpu_encoder.py)
-    if (epi == EPI_RESID) return M >= 4096 ? 14 : 16;
+    // K = 512 (linear_out, pointwise_conv2): the 64x128 K-group tile, two blocks per CU, so one block's
+    // store-bound epilogue overlaps the other's main loop (forward 4.716-4.751 -> 4.677-4.719 ms,
+    // profiles/r04r_resid_tile_ab.txt); K = 2048 (FFN linear2) keeps 128x128 (fewer bytes per CU)
+    if (epi == EPI_RESID) return (M >= 4096 && (K == 0 || K >= 1024)) ? 14 : 16;
     // the subsampling Linear (K = C * F2 = 10240, N = d): 64 tiles of 256x256 fill a quarter of the
     // chip; 128x128 in two K-groups (same K order as the small-M 64x128 K-group tile): 154 -> ~100 us
     if (epi == EPI_SCALE_F32 && K >= 4096) return M >= 4096 ? 12 : 16;
