@@ -113,6 +113,7 @@ struct GemmEpi {
   const float* uv;     // EPI_QKV: pos_bias_u then pos_bias_v, each [H][dkp] zero-padded
   float qscale;        // EPI_QKV: (q + u), (q + v) are written pre-multiplied by log2(e) / sqrt(dk)
   int out_scalar;      // EPI_SCALE_F32: element stores (fp32 rows whose stride is not a multiple of 4)
+  int nt_store;        // EPI_SCALE_F32 with out_scalar: non-temporal body stores (output read by no later kernel soon)
   int wt;              // set by gemm(): 16-byte output stores write-through (sc1), see store16_wt
   const float* Xin;    // EPI_RESID: residual input (null: X, updated in place)
   Drop drop;           // EPI_RESID: dropout on the branch, mask index m * ldx + n (thr 0: none)

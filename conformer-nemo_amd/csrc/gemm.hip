@@ -317,8 +317,10 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           const float* ir = img + r * TL::EPS;
           if (cc < nfull) {
             const int j = lead + 4 * cc;
-            *(float4*)(e.X + g0 + j) = make_float4(ir[j] * e.alpha, ir[j + 1] * e.alpha, ir[j + 2] * e.alpha,
-                                                   ir[j + 3] * e.alpha);
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const f4v v4 = {ir[j] * e.alpha, ir[j + 1] * e.alpha, ir[j + 2] * e.alpha, ir[j + 3] * e.alpha};
+            if (e.nt_store) __builtin_nontemporal_store(v4, (f4v*)(e.X + g0 + j));
+            else *(f4v*)(e.X + g0 + j) = v4;
           }
           if (e.out_scalar == 2) {   // A/B: the round-3 form, one thread storing all heads and tails
             if (cc == CPR - 1) {

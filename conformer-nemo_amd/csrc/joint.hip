@@ -504,14 +504,27 @@ void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu
     // whole 128-column tiles (bf16 mode; V + 1 = 1025 -> 1024 + 1)
     const int ntail = (dt == DT_BF16 && h->C > 128 && h->C % 128 <= kTailMax && Hp <= 1024) ? h->C % 128 : 0;
     const int Cm = h->C - ntail;
-    if (dt == DT_F32)
-      joint_hidden<float>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop, st);
-    else
-      joint_hidden<bf16_t>((const float*)fp, (const float*)gp, B, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop, st,
-                           ntail, (const bf16_t*)(h->wbuf + h->w_out) + (long)Cm * h->kp(h->H), h->kp(h->H),
-                           (const float*)(h->wbuf + h->b_out) + Cm, out + Cm, h->C);
-    gemm(dt, ws + w.hid, Hp, (int)rows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), Cm,
-         epi_f32((const float*)(h->wbuf + h->b_out), out, h->C, h->C % 4 ? 1 : 0), h->zero, st);
+    // inference: the lattice in chunks of `chunk` utterances (hidden kernel, then logits GEMM, per chunk), so
+    // each chunk's hidden is read back while it is still in the Infinity Cache (CFM_JOINT_CHUNK, 0 = whole)
+    static const int chunk_env = [] { const char* e = getenv("CFM_JOINT_CHUNK"); return e ? atoi(e) : 0; }();
+    const int chunk = (drop.thr == 0 && chunk_env > 0) ? std::min(chunk_env, B) : B;
+    for (int b0 = 0; b0 < B; b0 += chunk) {
+      const int nb = std::min(chunk, B - b0);
+      const long r0 = (long)b0 * T * U, nrows = (long)nb * T * U;
+      const float* fpc = fp + (long)b0 * T * h->H;
+      const float* gpc = gp + (long)b0 * U * h->H;
+      float* outc = out + r0 * h->C;
+      if (dt == DT_F32)
+        joint_hidden<float>(fpc, gpc, nb, T, U, h->H, Hp, h->act, (float*)(ws + w.hid), drop, st);
+      else
+        joint_hidden<bf16_t>(fpc, gpc, nb, T, U, h->H, Hp, h->act, (bf16_t*)(ws + w.hid), drop, st, ntail,
+                             (const bf16_t*)(h->wbuf + h->w_out) + (long)Cm * h->kp(h->H), h->kp(h->H),
+                             (const float*)(h->wbuf + h->b_out) + Cm, outc + Cm, h->C);
+      GemmEpi le = epi_f32((const float*)(h->wbuf + h->b_out), outc, h->C, h->C % 4 ? 1 : 0);
+      static const int nt_env = [] { const char* e = getenv("CFM_LOGITS_NT"); return e ? atoi(e) : 0; }();
+      le.nt_store = le.out_scalar ? nt_env : 0;
+      gemm(dt, ws + w.hid, Hp, (int)nrows, h->H, h->wbuf + h->w_out, (int)h->kp(h->H), Cm, le, h->zero, st);
+    }
     if (log_softmax)
       cfm_launch(row_log_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, out, rows, h->C);
     HIP_OK(hipGetLastError());
