@@ -33,12 +33,16 @@ using namespace cfm;
 struct cfm_rnnt_decoder {
   int V = 0, H = 0, L = 0, device = 0;
   float* wbuf = nullptr;        // emb (V+1, H) | per layer [W_ih | W_hh] (4H, 2H) | per layer bias (4H)
-  long emb_off = 0, w_off = 0, b_off = 0;
+  long emb_off = 0, w_off = 0, b_off = 0, x_off = -1;   // x_off >= 0: the layer-0 input table below
+  bool x_ready = false;         // the table matches the current weights (set_weights clears it)
   int* host_flag = nullptr;     // pinned, 2 slots (greedy done-flag polling)
   hipEvent_t ev[2] = {nullptr, nullptr};
   const float* emb() const { return wbuf + emb_off; }
   const float* W(int l) const { return wbuf + w_off + (long)l * 4 * H * 2 * H; }
   const float* bias(int l) const { return wbuf + b_off + (long)l * 4 * H; }
+  // layer 0's input projection for every embedding row: xtab[e][r] = sum_k emb[e][k] W_ih[r][k], (V+1, 4H),
+  // built on first use after set_weights; inference steps gather a row instead of contracting over the input
+  float* xtab() const { return x_off >= 0 ? wbuf + x_off : nullptr; }
 };
 
 namespace {
@@ -464,16 +468,19 @@ __global__ __launch_bounds__(512) void lstm_step_mfma_kernel(const float* __rest
                                                              float* __restrict__ h2, float* __restrict__ c2,
                                                              float* __restrict__ gout, long gstride, int B, int I, int H,
                                                              const int* __restrict__ run_flag,
-                                                             float* __restrict__ gates_out, Drop gdrop, int gstep) {
+                                                             float* __restrict__ gates_out, Drop gdrop, int gstep,
+                                                             const float* __restrict__ xtab) {
   __shared__ f32x4 part[8][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int u0 = blockIdx.x * 4, b0 = blockIdx.y * 16;
-  const int K = I + H, G = K / 16;   // NT = ceil(G / 8) groups per wave
+  // xtab (layer 0 from embedding rows only): the input part comes from the gathered table row, the
+  // contraction covers the h part alone
+  const int K = I + H, kb = xtab ? I : 0, G = (K - kb) / 16;   // NT = ceil(G / 8) groups per wave
   if (run_flag && *run_flag == 0) return;   // uniform: every utterance finished
   // operand rows of this lane: W row (unit u0 + rr / 4, gate rr % 4), batch row b0 + rr
   const int rr = lane & 15, kq = lane >> 4;
   const int wu = min(u0 + (rr >> 2), H - 1), wg = rr & 3;
-  const float* wrow = W + ((long)wg * H + wu) * K + 4 * kq;
+  const float* wrow = W + ((long)wg * H + wu) * K + kb + 4 * kq;
   const int b = b0 + rr;
   const int bc = min(b, B - 1);
   // the row's input part: the previous layer's h, an embedding row, or zero (start of sequence; rows past
@@ -488,11 +495,21 @@ __global__ __launch_bounds__(512) void lstm_step_mfma_kernel(const float* __rest
 #pragma unroll
   for (int t = 0; t < NT; ++t) {   // all loads first (latency), then the MFMAs
     const int gi = min(w + 8 * t, G - 1);
-    const int k = gi * 16 + 4 * kq;
+    const int k = kb + gi * 16 + 4 * kq;
     wa[t] = *(const float4*)(wrow + gi * 16);
     const bool inx = k < I;
     const float4 v = *(const float4*)(inx ? xrow + k : hrow + (k - I));
     xa[t] = (inx ? xok : hok) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // wave 0's epilogue lanes fetch their table entries now, under the MFMA latency
+  f32x4 xg = {0.f, 0.f, 0.f, 0.f};
+  if (xtab && w == 0) {
+    const int bb = b0 + (lane & 15), j = u0 + (lane >> 4);
+    const int lb = (bb < B && j < H) ? xlab[bb] : -1;
+    if (lb >= 0) {
+      const float* xr = xtab + (long)min(lb, nemb - 1) * 4 * H + j;
+      xg[0] = xr[0]; xg[1] = xr[H]; xg[2] = xr[2 * H]; xg[3] = xr[3 * H];
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -507,6 +524,7 @@ __global__ __launch_bounds__(512) void lstm_step_mfma_kernel(const float* __rest
   __syncthreads();
   if (w != 0) return;
   f32x4 s = part[0][lane];
+  s[0] += xg[0]; s[1] += xg[1]; s[2] += xg[2]; s[3] += xg[3];
 #pragma unroll
   for (int ww = 1; ww < 8; ++ww) {
     const f32x4 t = part[ww][lane];
@@ -530,6 +548,49 @@ __global__ __launch_bounds__(512) void lstm_step_mfma_kernel(const float* __rest
   }
 }
 
+// xtab[e][r] = sum_{k < I} emb[e][k] W[r][k] (W rows of stride ldw: layer 0's packed [W_ih | W_hh]);
+// 64x64 LDS-tiled fp32, once per set_weights (the table is (V+1) x 4H)
+__global__ __launch_bounds__(256) void lstm_xtab_kernel(const float* __restrict__ emb, const float* __restrict__ W,
+                                                        int M, int N, int I, int ldw, float* __restrict__ X) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Ws[16][64 + 4];
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < I; k0 += 16) {
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+      const int rr = i >> 4, kk = i & 15;
+      const int m = m0 + rr, n = n0 + rr, k = k0 + kk;
+      As[kk][rr] = (m < M && k < I) ? emb[(long)m * I + k] : 0.0f;
+      Ws[kk][rr] = (n < N && k < I) ? W[(long)n * ldw + k] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = Ws[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], w[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tx * 4 + j;
+      if (n < N) X[(long)m * N + n] = acc[i][j];
+    }
+  }
+}
+
 size_t lstm_lds(int K) { return (size_t)(RB * K + RED + 4 * 4 * RB) * sizeof(float); }
 
 // > 64 KB of dynamic LDS needs the per-kernel opt-in; done once per process.
@@ -550,23 +611,31 @@ void check_device(const cfm_rnnt_decoder* h) {
   if (cur != h->device) HIP_OK(hipSetDevice(h->device));
 }
 
+bool lstm_mfma_nt(int NT) { return NT == 1 || NT == 2 || NT == 3 || NT == 4 || NT == 5 || NT == 6 || NT == 8 || NT == 10 || NT == 12 || NT == 16; }
+
 // one LSTM layer step: the matrix-core kernel when the shapes allow it (I, H multiples of 16, H % 4 == 0,
-// K <= 3072; CFM_LSTM_MFMA=0 keeps the VALU kernel), else lstm_step_kernel
+// K <= 3072; CFM_LSTM_MFMA=0 keeps the VALU kernel), else lstm_step_kernel.  Layer 0 fed from embedding rows
+// outside training (no gates_out) uses the input table when the handle has one and it is current.
 void launch_lstm_step(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, const float* xsrc, const float* hcur,
                       const float* ccur, float* hn, float* cn, float* gout, long gstride, int B, const int* flag,
                       float* gates_out, Drop gdrop, int gstep, hipStream_t st) {
   static const int mfma = [] { const char* e = getenv("CFM_LSTM_MFMA"); return e ? atoi(e) : 1; }();
   const int H = d->H, I = H, K = I + H;
-  const int NT = (K / 16 + 7) / 8;
-  if (mfma && H % 16 == 0 && I % 16 == 0 && (NT == 4 || NT == 5 || NT == 8 || NT == 10 || NT == 12 || NT == 16)) {
+  const float* xt = (l == 0 && !xsrc && !gates_out && d->x_ready) ? d->xtab() : nullptr;
+  const int NT = ((xt ? H : K) / 16 + 7) / 8;
+  if (mfma && H % 16 == 0 && I % 16 == 0 && lstm_mfma_nt(NT)) {
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((unsigned)(H / 4), (unsigned)((B + 15) / 16)), dim3(512), 0, st, d->W(l), d->bias(l),
                          d->emb(), d->V + 1, xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, I, H, flag, gates_out,
-                         gdrop, gstep);
+                         gdrop, gstep, xt);
     };
     switch (NT) {
+      case 1: go(lstm_step_mfma_kernel<1>); break;
+      case 2: go(lstm_step_mfma_kernel<2>); break;
+      case 3: go(lstm_step_mfma_kernel<3>); break;
       case 4: go(lstm_step_mfma_kernel<4>); break;
       case 5: go(lstm_step_mfma_kernel<5>); break;
+      case 6: go(lstm_step_mfma_kernel<6>); break;
       case 8: go(lstm_step_mfma_kernel<8>); break;
       case 10: go(lstm_step_mfma_kernel<10>); break;
       case 12: go(lstm_step_mfma_kernel<12>); break;
@@ -577,6 +646,17 @@ void launch_lstm_step(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, con
   const dim3 grid((H + 3) / 4, (B + RB - 1) / RB);
   hipLaunchKernelGGL(lstm_step_kernel, grid, dim3(256), lstm_lds(K), st, d->W(l), d->bias(l), d->emb(), d->V + 1,
                      xlab, xsrc, hcur, ccur, hn, cn, gout, gstride, B, I, H, flag, gates_out, gdrop, gstep);
+}
+
+// (re)build the layer-0 input table after set_weights, on the stream of the call that will read it; only
+// when the matrix-core step can take it (shapes above; CFM_LSTM_XTAB=0 disables it)
+void ensure_xtab(cfm_rnnt_decoder* d, hipStream_t st) {
+  if (d->x_ready || !d->xtab()) return;
+  const int H = d->H, N = 4 * H, M = d->V + 1;
+  hipLaunchKernelGGL(lstm_xtab_kernel, dim3((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64)), dim3(256), 0, st,
+                     d->emb(), d->W(0), M, N, H, 2 * H, d->xtab());
+  HIP_OK(hipGetLastError());
+  d->x_ready = true;
 }
 
 void lstm_layer(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, const float* xsrc, const float* hcur,
@@ -807,16 +887,44 @@ __global__ void gather_emb_kernel(const int32_t* __restrict__ xlab, const float*
 // d_embed[label] += dx rows; the blank (padding_idx = V) and SOS rows get none (nn.Embedding padding_idx)
 // d(embedding) row v = sum of dx over the steps whose label is v, in step order (deterministic: one
 // block column per row, no atomics); the padding row (blank = V) and unused rows come out zero
+// d_embed[v] = sum over rows r with xlab[r] == v of dx[r] (r ascending: deterministic).  One block per
+// embedding row covering all H columns (<= 6 per thread); the labels are staged through LDS in chunks and
+// scanned four at a time, so a block costs ~S*B/4 LDS reads instead of S*B dependent global loads.
+constexpr int kEmbCols = 6, kEmbChunk = 8192;
 __global__ __launch_bounds__(256) void embed_grad_kernel(const int32_t* __restrict__ xlab, const float* __restrict__ dx,
                                                          int SB, int H, int V, float* __restrict__ demb) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int v = blockIdx.y;
-  if (j >= H) return;
-  float s = 0.0f;
-  if (v < V)
-    for (int r = 0; r < SB; ++r)
-      if (xlab[r] == v) s += dx[(long)r * H + j];
-  demb[(long)v * H + j] = s;
+  __shared__ int4 lab[kEmbChunk / 4];
+  const int v = blockIdx.x;
+  float acc[kEmbCols];
+#pragma unroll
+  for (int c = 0; c < kEmbCols; ++c) acc[c] = 0.0f;
+  if (v < V) {
+    for (int r0 = 0; r0 < SB; r0 += kEmbChunk) {
+      const int n = min(kEmbChunk, SB - r0);
+      __syncthreads();
+      for (int i = threadIdx.x; i < kEmbChunk; i += 256) ((int*)lab)[i] = i < n ? xlab[r0 + i] : -1;
+      __syncthreads();
+      for (int q = 0; q < (n + 3) / 4; ++q) {
+        const int4 l4 = lab[q];
+        const int ls[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (ls[e] != v) continue;   // block-uniform
+          const float* row = dx + (long)(r0 + 4 * q + e) * H;
+#pragma unroll
+          for (int c = 0; c < kEmbCols; ++c) {
+            const int j = threadIdx.x + 256 * c;
+            if (j < H) acc[c] += row[j];
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < kEmbCols; ++c) {
+    const int j = threadIdx.x + 256 * c;
+    if (j < H) demb[(long)v * H + j] = acc[c];
+  }
 }
 
 long predict_ws_bytes(const cfm_rnnt_decoder* d, int B, int U) {
@@ -846,7 +954,12 @@ cfm_status cfm_rnnt_decoder_create(int vocab_size, int pred_hidden, int layers, 
     d->emb_off = 0;
     d->w_off = round_up((long)(vocab_size + 1) * H, 64);
     d->b_off = d->w_off + (long)layers * 4 * H * 2 * H;
-    const long total = d->b_off + (long)layers * 4 * H;
+    long total = d->b_off + (long)layers * 4 * H;
+    static const int xtab_on = [] { const char* e = getenv("CFM_LSTM_XTAB"); return e ? atoi(e) : 1; }();
+    if (xtab_on && H % 16 == 0 && lstm_mfma_nt((int)(H / 16 + 7) / 8)) {
+      d->x_off = round_up(total, 64);
+      total = d->x_off + (long)(vocab_size + 1) * 4 * H;
+    }
     hipError_t e = hipMalloc((void**)&d->wbuf, total * sizeof(float));
     if (e == hipSuccess) e = hipHostMalloc((void**)&d->host_flag, 2 * sizeof(int), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->ev[0], hipEventDisableTiming);
@@ -877,6 +990,7 @@ cfm_status cfm_rnnt_decoder_set_weights(cfm_rnnt_decoder* d, const float* embed,
     check_device(d);
     hipStream_t st = (hipStream_t)stream;
     const long H = d->H;
+    d->x_ready = false;
     HIP_OK(hipMemcpyAsync(d->wbuf + d->emb_off, embed, (size_t)(d->V + 1) * H * sizeof(float),
                           hipMemcpyDeviceToDevice, st));
     for (int l = 0; l < d->L; ++l) {
@@ -919,6 +1033,7 @@ cfm_status cfm_rnnt_decoder_predict(cfm_rnnt_decoder* d, const int64_t* y, int B
     else HIP_OK(hipMemsetAsync(cs[0], 0, lbh * 4, st));
     hipLaunchKernelGGL(predict_labels_kernel, dim3((unsigned)(((long)S * B + 255) / 256)), dim3(256), 0, st, y, B,
                        U, S, add_sos ? 1 : 0, d->V + 1, xlab);
+    ensure_xtab(d, st);
     const long bh = (long)B * d->H;
     int cur = 0;
     for (int u = 0; u < S; ++u) {
@@ -1056,7 +1171,7 @@ cfm_status cfm_rnnt_decoder_backward(cfm_rnnt_decoder* d, const int64_t* y, int 
     }
     // dy now holds d(embedding rows) (S, B, H): summed per label row (not blank = padding_idx)
     if (d_embed) {
-      hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)((H + 255) / 256), (unsigned)(d->V + 1)), dim3(256), 0, st,
+      hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)(d->V + 1)), dim3(256), 0, st,
                          tp.xlab, dy, S * B, H, d->V, d_embed);
     }
     HIP_OK(hipGetLastError());
@@ -1114,6 +1229,7 @@ cfm_status cfm_rnnt_greedy_decode(cfm_rnnt_decoder* d, const float* enc_bdt, con
     hipLaunchKernelGGL(enc_proj_kernel, dim3((unsigned)(((long)B * T + 63) / 64), (J + 63) / 64), dim3(256), 0, st,
                        enc_bdt, w_enc, b_enc, B, T, D1, J, F);
     // hS and cS are adjacent in the workspace: zero both in one pass
+    ensure_xtab(d, st);
     hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)std::max<long>(1, std::min<long>((2 * lbh + 255) / 256, 1024))),
                        dim3(256), 0, st, enc_len, B, T, ct, ntok, scores, hS, (long)((char*)h2 - (char*)hS) / 4);
     HIP_OK(hipGetLastError());
