@@ -53,7 +53,7 @@ STREAM_SYMBOLS = ("cfm_frame_buffer_step",)
 MEL_SYMBOLS = ("cfm_mel_create", "cfm_mel_destroy", "cfm_mel_set_tables", "cfm_mel_num_frames", "cfm_mel_output_frames",
                "cfm_mel_forward", "cfm_normalize_batch", "cfm_mel_filterbank_slaney")
 # every symbol include/cfm_rnnt_loss.h declares
-RNNT_LOSS_SYMBOLS = ("cfm_rnnt_loss_workspace_size", "cfm_rnnt_loss")
+RNNT_LOSS_SYMBOLS = ("cfm_rnnt_loss_workspace_size", "cfm_rnnt_loss", "cfm_rnnt_loss_costs", "cfm_rnnt_loss_grad")
 # every symbol include/cfm_augment.h declares
 AUGMENT_SYMBOLS = ("cfm_spec_mask_rects", "cfm_spec_shot")
 # every symbol include/cfm_rnnt_decode.h declares (bound in conformer_amd/rnnt_decode.py)
@@ -194,6 +194,9 @@ def load(variant: str = "bf16") -> ctypes.CDLL:
         "cfm_rnnt_loss_workspace_size": (sz, [ci, ci, ci]),
         "cfm_rnnt_loss": (ci, [vp, vp, ci, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, ctypes.c_float, vp, vp, vp, sz,
                                vp]),
+        "cfm_rnnt_loss_costs": (ci, [vp, vp, ci, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, vp, vp, sz, vp]),
+        "cfm_rnnt_loss_grad": (ci, [vp, vp, ci, vp, vp, ci, ci, ci, ci, ci, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float, vp, vp, vp, sz, vp]),
         "cfm_spec_mask_rects": (ci, [vp, ci, ci, ci, vp, ci, ctypes.c_float, vp]),
         "cfm_spec_shot": (ci, [vp, vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, vp]),
         "cfm_ctc_head_create": (ci, [ci, ci, ci, ci, ctypes.POINTER(vp)]),

@@ -41,6 +41,31 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
   }
 }
 
+// The non-transposed pack as row runs: a wave converts one row 128 columns at a time (two adjacent columns per
+// lane, one 4- or 8-byte store; no LDS), grid-striding over rows.  Same values as pack_kernel (zero outside src,
+// the same rounding); needs even dst_ld and cols_pad.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, long src_ld, int rows, int cols,
+                                                        T* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad) {
+  const int lane = threadIdx.x & 63;
+  for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows_pad; r += (long)gridDim.x * 4) {
+    const float* sr = src + r * src_ld;
+    T* dr = dst + r * dst_ld;
+    const bool rok = r < rows;
+#pragma unroll 4
+    for (int c = 2 * lane; c < cols_pad; c += 128) {
+      const float v0 = (rok && c < cols) ? sr[c] : 0.0f;
+      const float v1 = (rok && c + 1 < cols) ? sr[c + 1] : 0.0f;
+      if constexpr (sizeof(T) == 4) {
+        *(float2*)(dr + c) = make_float2(v0, v1);
+      } else {
+        const bf16_t b0 = f2bf(v0), b1 = f2bf(v1);
+        *(uint32_t*)(dr + c) = (uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+      }
+    }
+  }
+}
+
 // Column sums, stage 1: partial[chunk][n] = sum of a 256-row chunk (block = 64 columns x 4 row lanes,
 // every row read a coalesced 256-byte segment); stage 2 folds the chunks (16 columns x 16 lanes).
 // Fixed order: bitwise reproducible.
@@ -303,6 +328,15 @@ unsigned ew_grid(long n) { return (unsigned)std::min<long>((n + 255) / 256, 8192
 void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, bool transpose, void* dst, long dst_ld,
                  int rows_pad, int cols_pad, hipStream_t st) {
   if (rows_pad <= 0 || cols_pad <= 0) return;
+  static const int rows_path = [] { const char* e = getenv("CFM_PACK_ROWS"); return e ? atoi(e) : 1; }();
+  if (rows_path && !transpose && dst_ld % 2 == 0 && cols_pad % 2 == 0) {
+    const dim3 g((unsigned)std::min<long>(((long)rows_pad + 3) / 4, 32768)), b(256);
+    if (dtype == DT_F32)
+      cfm_launch(pack_rows_kernel<float>, g, b, 0, st, src, src_ld, rows, cols, (float*)dst, dst_ld, rows_pad, cols_pad);
+    else
+      cfm_launch(pack_rows_kernel<bf16_t>, g, b, 0, st, src, src_ld, rows, cols, (bf16_t*)dst, dst_ld, rows_pad, cols_pad);
+    return;
+  }
   const dim3 grid((cols_pad + 31) / 32, (rows_pad + 31) / 32), block(256);
   if (dtype == DT_F32)
     cfm_launch(pack_kernel<float>, grid, block, 0, st, src, src_ld, rows, cols, (int)transpose, (float*)dst, dst_ld,

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <string>
 
 #include "../../include/cfm_rnnt_loss.h"
 #include "cfm_abi.h"
@@ -100,16 +101,17 @@ __global__ __launch_bounds__(256) void rnnt_denom_kernel(const float* __restrict
 }
 
 // blockIdx.y == 0: alphas (gpu_rnnt_kernel.py:66-166); == 1: betas (168-260).
+template <int PT>   // per-thread label positions (u = tid + k * blockDim): 1 up to U = 1024, else 8
 __global__ __launch_bounds__(1024) void rnnt_lattice_kernel(const float* __restrict__ lpb, const float* __restrict__ lpl,
                                                             const int32_t* __restrict__ act_lens,
                                                             const int32_t* __restrict__ label_lens, Dims d,
                                                             float* __restrict__ alphas, float* __restrict__ betas,
                                                             float* __restrict__ llf, float* __restrict__ llb,
                                                             float* __restrict__ costs, float fastemit_lambda,
-                                                            int per_thread) {
+                                                            int per_thread, int dir0) {
   extern __shared__ float prev[];  // the previous diagonal, indexed by u
   const int b = blockIdx.x;
-  const bool fwd = blockIdx.y == 0;
+  const bool fwd = blockIdx.y + dir0 == 0;
   int Tb, Ub;
   lens(d, act_lens, label_lens, b, Tb, Ub);
   if (Tb < 1) {
@@ -120,14 +122,44 @@ __global__ __launch_bounds__(1024) void rnnt_lattice_kernel(const float* __restr
   }
   const long off = (long)b * d.T * d.U;
   float* lat = fwd ? alphas : betas;
-  float mine[8];  // this thread's value on the previous diagonal, per owned u (u = tid + k * blockDim)
+  float mine[PT];  // this thread's value on the previous diagonal, per owned u (u = tid + k * blockDim)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) mine[k] = kNegInf;
+  for (int k = 0; k < PT; ++k) mine[k] = kNegInf;
   const int ndiag = Tb + Ub - 1;
-  for (int n = 0; n < ndiag; ++n) {
-    float cur[8];
+  // The log-probabilities a thread needs on diagonal n (vb: lpb, vl: lpl; 0 where unused) are fetched two
+  // diagonals ahead, so their global-load latency overlaps two diagonals' LDS exchange and barriers instead of
+  // stalling every diagonal.  The arithmetic is unchanged.
+  auto fetch = [&](int n, int k, float& vb, float& vl) {
+    vb = 0.0f;
+    vl = 0.0f;
+    const int u = threadIdx.x + k * blockDim.x;
+    if (k >= per_thread || u >= Ub || n >= ndiag) return;
+    if (fwd) {
+      const int t = n - u;
+      if (t < 0 || t >= Tb) return;
+      if (t > 0) vb = lpb[off + (long)(t - 1) * d.U + u];
+      if (u > 0) vl = lpl[off + (long)t * d.U + u - 1];
+    } else {
+      const int t = Tb - 1 - (n - (Ub - 1 - u));
+      if (t < 0 || t >= Tb || n < Ub - 1 - u) return;
+      const long idx = off + (long)t * d.U + u;
+      vb = lpb[idx];
+      if (u < Ub - 1) vl = lpl[idx];
+    }
+  };
+  float pb0[PT], pl0[PT], pb1[PT], pl1[PT];   // diagonals n and n + 1
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < PT; ++k) {
+    fetch(0, k, pb0[k], pl0[k]);
+    fetch(1, k, pb1[k], pl1[k]);
+  }
+  for (int n = 0; n < ndiag; ++n) {
+    float pb2[PT], pl2[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) fetch(n + 2, k, pb2[k], pl2[k]);
+    float cur[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
       cur[k] = kNegInf;
       if (k >= per_thread) continue;
       const int u = threadIdx.x + k * blockDim.x;
@@ -137,9 +169,9 @@ __global__ __launch_bounds__(1024) void rnnt_lattice_kernel(const float* __restr
         if (t < 0 || t >= Tb) continue;
         float v;
         if (t == 0 && u == 0) v = 0.0f;
-        else if (u == 0) v = mine[k] + lpb[off + (long)(t - 1) * d.U];
-        else if (t == 0) v = prev[u - 1] + lpl[off + u - 1];
-        else v = log_sum_exp(prev[u - 1] + lpl[off + (long)t * d.U + u - 1], mine[k] + lpb[off + (long)(t - 1) * d.U + u]);
+        else if (u == 0) v = mine[k] + pb0[k];
+        else if (t == 0) v = prev[u - 1] + pl0[k];
+        else v = log_sum_exp(prev[u - 1] + pl0[k], mine[k] + pb0[k]);
         cur[k] = v;
         lat[off + (long)t * d.U + u] = v;
       } else {
@@ -148,17 +180,22 @@ __global__ __launch_bounds__(1024) void rnnt_lattice_kernel(const float* __restr
         if (t < 0 || t >= Tb || n < Ub - 1 - u) continue;
         float v;
         const long idx = off + (long)t * d.U + u;
-        if (t == Tb - 1 && u == Ub - 1) v = lpb[idx];
-        else if (u == Ub - 1) v = mine[k] + lpb[idx];
-        else if (t == Tb - 1) v = prev[u + 1] + lpl[idx];
-        else v = log_sum_exp(prev[u + 1] + lpl[idx], mine[k] + lpb[idx]);
+        if (t == Tb - 1 && u == Ub - 1) v = pb0[k];
+        else if (u == Ub - 1) v = mine[k] + pb0[k];
+        else if (t == Tb - 1) v = prev[u + 1] + pl0[k];
+        else v = log_sum_exp(prev[u + 1] + pl0[k], mine[k] + pb0[k]);
         cur[k] = v;
         lat[idx] = v;
       }
     }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      pb0[k] = pb1[k]; pl0[k] = pl1[k];
+      pb1[k] = pb2[k]; pl1[k] = pl2[k];
+    }
     __syncthreads();  // everyone has read the previous diagonal
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < PT; ++k) {
       if (k >= per_thread) continue;
       const int u = threadIdx.x + k * blockDim.x;
       if (u < Ub) {  // this diagonal's value (or -inf): read by u itself and by its neighbour next diagonal
@@ -184,7 +221,8 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
                                                         const int32_t* __restrict__ label_lens, Dims d,
                                                         const float* __restrict__ denom, const float* __restrict__ alphas,
                                                         const float* __restrict__ betas, const float* __restrict__ llf,
-                                                        float fastemit_lambda, float clamp, float* __restrict__ grads) {
+                                                        float fastemit_lambda, float clamp, float pre,
+                                                        const float* __restrict__ scale, float* __restrict__ grads) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)d.B * d.T * d.U) return;
@@ -205,6 +243,7 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
   const float be_u1 = u < Ub - 1 ? betas[row + 1] : 0.0f;
   const float lp_lab = lab >= 0 ? dn + a[lab] : 0.0f;
   const float l1p = log1pf(fastemit_lambda);
+  const float sc = scale ? scale[b] : 1.0f;
   auto gval = [&](int v, float av) {
     const float logpk = dn + av;
     float gr = expf(al + be + logpk - ll);
@@ -213,8 +252,26 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
     if (v == d.blank && t < Tb - 1) gr -= expf(al + logpk - ll + be_t1);
     if (u < Ub - 1 && v == lab) gr -= expf(l1p + al + logpk - ll + be_u1);
     if (clamp > 0.0f) gr = fmaxf(fminf(gr, clamp), -clamp);
+    if (pre != 1.0f) gr *= pre;   // as the host's in-place multiplies after the kernel, same order
+    if (scale) gr *= sc;
     return gr;
   };
+  if (d.V <= 64 * kDenomRegs) {
+    // the whole row in flight per lane (up to 32 independent loads), then the math and the stores: the wave's
+    // bytes in flight, not HBM bandwidth, bounded the four-at-a-time loop below
+    float av[kDenomRegs];
+#pragma unroll
+    for (int k = 0; k < kDenomRegs; ++k) {
+      const int v = lane + 64 * k;
+      av[k] = v < d.V ? a[v] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < kDenomRegs; ++k) {
+      const int v = lane + 64 * k;
+      if (v < d.V) g[v] = gval(v, av[k]);
+    }
+    return;
+  }
   // four logits in flight per lane (independent loads, then the math)
   int v0 = lane;
   for (; v0 + 192 < d.V; v0 += 256) {
@@ -228,6 +285,45 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
 }
 
 size_t ws_floats(int B, int T, int U) { return (size_t)5 * B * T * U + 2 * (size_t)B + 64; }
+
+void check_loss_args(const char* who, int B, int T, int U, int V, int blank, int labels_ld, size_t workspace_bytes,
+                      const void* workspace, size_t need) {
+  if (B < 0 || T < 1 || U < 1 || V < 1 || blank < 0 || blank >= V || labels_ld < U - 1)
+    fail(CFM_ERR_INVALID_ARG, std::string(who) + ": need T, U, V >= 1, 0 <= blank < V, labels_ld >= U - 1");
+  if (U > 8 * 1024) fail(CFM_ERR_UNSUPPORTED, std::string(who) + ": more than 8191 labels per utterance");
+  if (B > 0 && (workspace_bytes < need || !workspace)) fail(CFM_ERR_WORKSPACE, std::string(who) + ": workspace too small");
+}
+
+// denominators, the alpha lattice and the costs; the beta lattice when `betas`; the gradient when grads
+void loss_impl(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+               const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda, float clamp,
+               float* costs, float* grads, bool betas_too, void* workspace, size_t workspace_bytes, void* stream) {
+  check_loss_args("cfm_rnnt_loss", B, T, U, V, blank, labels_ld, workspace_bytes, workspace,
+                  ws_floats(B, T, U) * sizeof(float));
+  if (B == 0) return;
+  if (!acts || !act_lens || !label_lens || !costs || (U > 1 && !labels))
+    fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_loss: null input");
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)B * T * U;
+  float* w = (float*)workspace;
+  float *denom = w, *lpb = w + n, *lpl = w + 2 * n, *alphas = w + 3 * n, *betas = w + 4 * n;
+  float *llf = w + 5 * n, *llb = llf + B;
+  Dims d{B, T, U, V, blank, labels_ld};
+  const unsigned rows_blocks = (unsigned)((n + 3) / 4);
+  hipLaunchKernelGGL(rnnt_denom_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
+                     denom, lpb, lpl);
+  HIP_OK(hipGetLastError());
+  const int threads = std::min(1024, (U + 63) / 64 * 64);
+  const int per_thread = (U + threads - 1) / threads;
+  hipLaunchKernelGGL(per_thread == 1 ? rnnt_lattice_kernel<1> : rnnt_lattice_kernel<8>, dim3(B, betas_too ? 2 : 1), dim3(threads), (size_t)U * sizeof(float), st,
+                     lpb, lpl, act_lens, label_lens, d, alphas, betas, llf, llb, costs, fastemit_lambda, per_thread, 0);
+  HIP_OK(hipGetLastError());
+  if (grads) {
+    hipLaunchKernelGGL(rnnt_grad_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
+                       denom, alphas, betas, llf, fastemit_lambda, clamp, 1.0f, nullptr, grads);
+    HIP_OK(hipGetLastError());
+  }
+}
 
 }  // namespace
 
@@ -243,34 +339,38 @@ cfm_status cfm_rnnt_loss(const float* acts, const int32_t* labels, int labels_ld
                          float clamp, float* costs, float* grads, void* workspace, size_t workspace_bytes,
                          void* stream) {
   return guarded([&] {
-    if (B < 0 || T < 1 || U < 1 || V < 1 || blank < 0 || blank >= V || labels_ld < U - 1)
-      fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_loss: need T, U, V >= 1, 0 <= blank < V, labels_ld >= U - 1");
-    if (U > 8 * 1024) fail(CFM_ERR_UNSUPPORTED, "cfm_rnnt_loss: more than 8191 labels per utterance");
+    loss_impl(acts, labels, labels_ld, act_lens, label_lens, B, T, U, V, blank, fastemit_lambda, clamp, costs, grads,
+              grads != nullptr, workspace, workspace_bytes, stream);
+  });
+}
+
+cfm_status cfm_rnnt_loss_costs(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+                               const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
+                               float* costs, void* workspace, size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    loss_impl(acts, labels, labels_ld, act_lens, label_lens, B, T, U, V, blank, fastemit_lambda, 0.0f, costs, nullptr,
+              true, workspace, workspace_bytes, stream);
+  });
+}
+
+cfm_status cfm_rnnt_loss_grad(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+                              const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
+                              float clamp, float pre_scale, const float* scale, float* grads, const void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  return guarded([&] {
+    check_loss_args("cfm_rnnt_loss_grad", B, T, U, V, blank, labels_ld, workspace_bytes, workspace,
+                    ws_floats(B, T, U) * sizeof(float));
     if (B == 0) return;
-    if (!acts || !act_lens || !label_lens || !costs || (U > 1 && !labels))
-      fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_loss: null input");
-    if (workspace_bytes < cfm_rnnt_loss_workspace_size(B, T, U) || !workspace)
-      fail(CFM_ERR_WORKSPACE, "cfm_rnnt_loss: workspace too small");
-    hipStream_t st = (hipStream_t)stream;
+    if (!acts || !act_lens || !label_lens || !grads || (U > 1 && !labels))
+      fail(CFM_ERR_INVALID_ARG, "cfm_rnnt_loss_grad: null input");
     const long n = (long)B * T * U;
-    float* w = (float*)workspace;
-    float *denom = w, *lpb = w + n, *lpl = w + 2 * n, *alphas = w + 3 * n, *betas = w + 4 * n;
-    float *llf = w + 5 * n, *llb = llf + B;
+    const float* w = (const float*)workspace;
+    const float *denom = w, *alphas = w + 3 * n, *betas = w + 4 * n, *llf = w + 5 * n;
     Dims d{B, T, U, V, blank, labels_ld};
-    const unsigned rows_blocks = (unsigned)((n + 3) / 4);
-    hipLaunchKernelGGL(rnnt_denom_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
-                       denom, lpb, lpl);
+    hipLaunchKernelGGL(rnnt_grad_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, acts, labels,
+                       act_lens, label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, pre_scale, scale,
+                       grads);
     HIP_OK(hipGetLastError());
-    const int threads = std::min(1024, (U + 63) / 64 * 64);
-    const int per_thread = (U + threads - 1) / threads;
-    hipLaunchKernelGGL(rnnt_lattice_kernel, dim3(B, grads ? 2 : 1), dim3(threads), (size_t)U * sizeof(float), st, lpb,
-                       lpl, act_lens, label_lens, d, alphas, betas, llf, llb, costs, fastemit_lambda, per_thread);
-    HIP_OK(hipGetLastError());
-    if (grads) {
-      hipLaunchKernelGGL(rnnt_grad_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
-                         denom, alphas, betas, llf, fastemit_lambda, clamp, grads);
-      HIP_OK(hipGetLastError());
-    }
   });
 }
 

@@ -10,6 +10,8 @@ like the reference GPU path, the gradient is computed in forward and scaled in b
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from nemo.core.classes.common import typecheck
@@ -58,8 +60,17 @@ class _RNNTNative(torch.autograd.Function):
         certify_inputs(acts, labels, act_lens, label_lens)
         if clamp < 0:
             raise ValueError("`clamp` must be 0.0 or positive float value.")
-        costs, grads = rnnt_loss(acts, labels, act_lens, label_lens, blank, fastemit_lambda, clamp,
-                                 want_grads=acts.requires_grad)
+        # The reference writes the gradient here and scales it in place in the backward.  Deferred (default):
+        # the backward writes it once, already scaled (cfm_rnnt_loss_grad, the same fp32 roundings) - one
+        # pass over the (B, T, U, V) tensor instead of three.  CFM_RNNT_DEFER_GRAD=0: the reference order.
+        defer = acts.requires_grad and os.environ.get("CFM_RNNT_DEFER_GRAD", "1") != "0"
+        ctx.state, ctx.pre = None, 1.0
+        if defer:
+            costs, grads, ctx.state = rnnt_loss(acts, labels, act_lens, label_lens, blank, fastemit_lambda, clamp,
+                                                want_grads=False, keep_state=True)
+        else:
+            costs, grads = rnnt_loss(acts, labels, act_lens, label_lens, blank, fastemit_lambda, clamp,
+                                     want_grads=acts.requires_grad)
         costs = costs.to(acts.dtype)
         if reduction in ["sum", "mean"]:
             costs = costs.sum().unsqueeze_(-1)
@@ -67,11 +78,17 @@ class _RNNTNative(torch.autograd.Function):
                 costs /= acts.shape[0]
                 if grads is not None:
                     grads /= acts.shape[0]
+                ctx.pre = float(torch.tensor(1.0, dtype=torch.float32) / acts.shape[0])   # ATen's reciprocal
         ctx.grads = grads
         return costs
 
     @staticmethod
     def backward(ctx, grad_output):
+        if grad_output is not None and ctx.state is not None:
+            from conformer_amd.rnnt_loss import rnnt_loss_grad
+            grads = rnnt_loss_grad(ctx.state, ctx.pre, grad_output)
+            ctx.state = None
+            return grads, None, None, None, None, None, None, None
         if grad_output is not None and ctx.grads is not None:
             grad_output = grad_output.view(-1, 1, 1, 1).to(ctx.grads)
             return ctx.grads.mul_(grad_output), None, None, None, None, None, None, None

@@ -34,6 +34,19 @@ cfm_status cfm_rnnt_loss(const float* acts, const int32_t* labels, int labels_ld
                          const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
                          float clamp, float* costs, float* grads, void* workspace, size_t workspace_bytes,
                          void* stream);
+/* The gradient in the backward pass instead of the forward.  The reference computes it in the forward and
+ * scales it in place by the incoming gradient in the backward (rnnt_pytorch.py:36-84).  Here the forward
+ * is cfm_rnnt_loss_costs (costs, plus both lattices kept in `workspace`), and the backward's
+ * cfm_rnnt_loss_grad writes grads = g * pre_scale * scale[b] in one pass, with the same fp32 roundings as
+ * the multiply-after.  scale: (B) fp32 or NULL (= 1); pre_scale: 1, or the fp32 reciprocal of a mean's
+ * divisor.  Saves the backward's full re-read and re-write of the (B, T, U, V) gradient. */
+cfm_status cfm_rnnt_loss_costs(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+                               const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
+                               float* costs, void* workspace, size_t workspace_bytes, void* stream);
+cfm_status cfm_rnnt_loss_grad(const float* acts, const int32_t* labels, int labels_ld, const int32_t* act_lens,
+                              const int32_t* label_lens, int B, int T, int U, int V, int blank, float fastemit_lambda,
+                              float clamp, float pre_scale, const float* scale, float* grads, const void* workspace,
+                              size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,39 @@ def test_mean_batch_and_reductions():
         assert abs(float(v) - want) <= 1e-4 * abs(want)
 
 
+@pytest.mark.parametrize("path", FILES, ids=[os.path.basename(f) for f in FILES])
+def test_deferred_gradient_is_bitwise_the_reference_order(path, monkeypatch):
+    """The backward-time gradient (cfm_rnnt_loss_grad: pre-scale and per-utterance scale applied in the kernel)
+    against the reference order (gradient written in the forward, divided / multiplied in place after it):
+    bitwise equal for every reduction, with a non-uniform incoming gradient."""
+    from nemo.collections.asr.losses.rnnt import RNNTLoss, RNNTLossNumba
+    z = np.load(path)
+    blank = int(z["blank"])
+    kw = {"fastemit_lambda": float(z["fastemit_lambda"]), "clamp": float(z["clamp"])}
+    B = z["acts"].shape[0]
+    gen = torch.Generator().manual_seed(5)
+    gout = (torch.rand(B, generator=gen) + 0.5).cuda()
+
+    def grad(defer, red):
+        monkeypatch.setenv("CFM_RNNT_DEFER_GRAD", "1" if defer else "0")
+        acts, labels, al, ll = _inputs(z)
+        if red == "mean_batch":
+            if blank != acts.shape[-1] - 1:
+                return None
+            out = RNNTLoss(num_classes=acts.shape[-1] - 1, loss_kwargs=kw)(log_probs=acts, targets=labels,
+                                                                          input_lengths=al, target_lengths=ll)
+            out.backward()
+        else:
+            out = RNNTLossNumba(blank=blank, reduction=red, **kw)(acts, labels, al, ll)
+            out.backward(gout if red == "none" else gout[:1])
+        return acts.grad
+    for red in ("none", "sum", "mean", "mean_batch"):
+        a, b = grad(True, red), grad(False, red)
+        if a is None:
+            continue
+        assert torch.equal(a, b), red
+
+
 def test_cfg4_shape_against_oracle_and_no_grad():
     """BASELINE config-4-like lattice (V+1=1025, U+1=21, T=40, ragged) vs the oracle; forward-only
     (no grads) returns the same costs."""
