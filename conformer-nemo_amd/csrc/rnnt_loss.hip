@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/cfm_rnnt_loss.h"
@@ -284,7 +285,116 @@ __global__ __launch_bounds__(256) void rnnt_grad_kernel(const float* __restrict_
   for (int v = v0; v < d.V; v += 64) g[v] = gval(v, a[v]);
 }
 
+// The same gradient over a flat, 16-byte aligned span: a block owns kGradRows consecutive lattice rows, i.e.
+// kGradRows * V contiguous floats, which start 16-byte aligned whatever V (kGradRows * 4 bytes is a multiple
+// of 16).  The rows' scalars (denominator, lattice values, label terms, flags) go to LDS first; then float4
+// loads and stores stream the span, each element finding its row by a running (row, v) walk.  The unaligned
+// 1025-float rows made every wave-per-row store straddle cache lines.  Element values are rnnt_grad_kernel's
+// (same expression, same order).
+constexpr int kGradRows = 64;
+struct GradRow {
+  float dn, al, be, ll, be_t1, be_u1, lp_lab, sc;
+  int lab, flags;   // flags: 1 inside the lattice, 2 u < Ub - 1, 4 last node (t, u) = (Tb - 1, Ub - 1), 8 t < Tb - 1
+};
+__global__ __launch_bounds__(256) void rnnt_grad_flat_kernel(const float* __restrict__ acts,
+                                                             const int32_t* __restrict__ labels,
+                                                             const int32_t* __restrict__ act_lens,
+                                                             const int32_t* __restrict__ label_lens, Dims d,
+                                                             const float* __restrict__ denom,
+                                                             const float* __restrict__ alphas,
+                                                             const float* __restrict__ betas,
+                                                             const float* __restrict__ llf, float fastemit_lambda,
+                                                             float clamp, float pre, const float* __restrict__ scale,
+                                                             float* __restrict__ grads) {
+  __shared__ GradRow rows[kGradRows];
+  const long nrow = (long)d.B * d.T * d.U;
+  const long r0 = (long)blockIdx.x * kGradRows;
+  const int nr = (int)min((long)kGradRows, nrow - r0);
+  if (threadIdx.x < nr) {
+    const long row = r0 + threadIdx.x;
+    const int u = (int)(row % d.U);
+    const long bt = row / d.U;
+    const int t = (int)(bt % d.T), b = (int)(bt / d.T);
+    int Tb, Ub;
+    lens(d, act_lens, label_lens, b, Tb, Ub);
+    GradRow g{};
+    if (t < Tb && u < Ub) {
+      g.dn = denom[row]; g.al = alphas[row]; g.be = betas[row]; g.ll = llf[b];
+      g.lab = u < Ub - 1 ? label_at(d, labels, b, u) : -1;
+      g.be_t1 = t < Tb - 1 ? betas[row + d.U] : 0.0f;
+      g.be_u1 = u < Ub - 1 ? betas[row + 1] : 0.0f;
+      g.lp_lab = g.lab >= 0 ? g.dn + acts[row * d.V + g.lab] : 0.0f;
+      g.sc = scale ? scale[b] : 1.0f;
+      g.flags = 1 | (u < Ub - 1 ? 2 : 0) | (t == Tb - 1 && u == Ub - 1 ? 4 : 0) | (t < Tb - 1 ? 8 : 0);
+    }
+    rows[threadIdx.x] = g;
+  }
+  __syncthreads();
+  const float l1p = log1pf(fastemit_lambda);
+  auto gval = [&](const GradRow& r, int v, float av) {
+    if (!(r.flags & 1)) return 0.0f;
+    const float logpk = r.dn + av;
+    float gr = expf(r.al + r.be + logpk - r.ll);
+    if (fastemit_lambda > 0.0f && (r.flags & 2)) gr = gr + fastemit_lambda * expf(r.al + r.lp_lab + r.be_u1 + logpk - r.ll);
+    if (v == d.blank && (r.flags & 4)) gr -= expf(r.al + logpk - r.ll);
+    if (v == d.blank && (r.flags & 8)) gr -= expf(r.al + logpk - r.ll + r.be_t1);
+    if ((r.flags & 2) && v == r.lab) gr -= expf(l1p + r.al + logpk - r.ll + r.be_u1);
+    if (clamp > 0.0f) gr = fmaxf(fminf(gr, clamp), -clamp);
+    if (pre != 1.0f) gr *= pre;
+    if (scale) gr *= r.sc;
+    return gr;
+  };
+  const float* a = acts + r0 * d.V;
+  float* g = grads + r0 * d.V;
+  const int len = nr * d.V, nvec = len / 4;
+  constexpr int UNR = 4;
+  for (int q0 = threadIdx.x; q0 < nvec; q0 += 256 * UNR) {
+    float4 av[UNR];
+#pragma unroll
+    for (int j = 0; j < UNR; ++j) {
+      const int q = q0 + 256 * j;
+      av[j] = q < nvec ? *(const float4*)(a + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < UNR; ++j) {
+      const int q = q0 + 256 * j;
+      if (q >= nvec) break;
+      const int e = 4 * q;
+      int rl = e / d.V, v = e - rl * d.V;
+      float o[4];
+      const float in[4] = {av[j].x, av[j].y, av[j].z, av[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (v >= d.V) { v -= d.V; ++rl; }
+        o[c] = gval(rows[rl], v, in[c]);
+        ++v;
+      }
+      *(float4*)(g + e) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  for (int e = 4 * nvec + threadIdx.x; e < len; e += 256) {   // < 4 trailing floats
+    const int rl = e / d.V;
+    g[e] = gval(rows[rl], e - rl * d.V, a[e]);
+  }
+}
+
 size_t ws_floats(int B, int T, int U) { return (size_t)5 * B * T * U + 2 * (size_t)B + 64; }
+
+// the flat kernel when both tensors are 16-byte aligned (CFM_RNNT_GRAD_FLAT=0: the wave-per-row kernel)
+void launch_grad(const float* acts, const int32_t* labels, const int32_t* act_lens, const int32_t* label_lens,
+                 const Dims& d, const float* denom, const float* alphas, const float* betas, const float* llf,
+                 float fastemit_lambda, float clamp, float pre, const float* scale, float* grads, hipStream_t st) {
+  static const int flat = [] { const char* e = getenv("CFM_RNNT_GRAD_FLAT"); return e ? atoi(e) : 1; }();
+  const long n = (long)d.B * d.T * d.U;
+  if (flat && !(((uintptr_t)acts | (uintptr_t)grads) & 15) && (long)kGradRows * d.V < (1L << 30))
+    hipLaunchKernelGGL(rnnt_grad_flat_kernel, dim3((unsigned)((n + kGradRows - 1) / kGradRows)), dim3(256), 0, st,
+                       acts, labels, act_lens, label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, pre,
+                       scale, grads);
+  else
+    hipLaunchKernelGGL(rnnt_grad_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, acts, labels, act_lens,
+                       label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, pre, scale, grads);
+  HIP_OK(hipGetLastError());
+}
 
 void check_loss_args(const char* who, int B, int T, int U, int V, int blank, int labels_ld, size_t workspace_bytes,
                       const void* workspace, size_t need) {
@@ -311,7 +421,7 @@ void loss_impl(const float* acts, const int32_t* labels, int labels_ld, const in
   Dims d{B, T, U, V, blank, labels_ld};
   const unsigned rows_blocks = (unsigned)((n + 3) / 4);
   hipLaunchKernelGGL(rnnt_denom_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
-                     denom, lpb, lpl);
+                       denom, lpb, lpl);
   HIP_OK(hipGetLastError());
   const int threads = std::min(1024, (U + 63) / 64 * 64);
   const int per_thread = (U + threads - 1) / threads;
@@ -319,9 +429,8 @@ void loss_impl(const float* acts, const int32_t* labels, int labels_ld, const in
                      lpb, lpl, act_lens, label_lens, d, alphas, betas, llf, llb, costs, fastemit_lambda, per_thread, 0);
   HIP_OK(hipGetLastError());
   if (grads) {
-    hipLaunchKernelGGL(rnnt_grad_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
-                       denom, alphas, betas, llf, fastemit_lambda, clamp, 1.0f, nullptr, grads);
-    HIP_OK(hipGetLastError());
+    launch_grad(acts, labels, act_lens, label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, 1.0f, nullptr,
+                grads, st);
   }
 }
 
@@ -367,10 +476,8 @@ cfm_status cfm_rnnt_loss_grad(const float* acts, const int32_t* labels, int labe
     const float* w = (const float*)workspace;
     const float *denom = w, *alphas = w + 3 * n, *betas = w + 4 * n, *llf = w + 5 * n;
     Dims d{B, T, U, V, blank, labels_ld};
-    hipLaunchKernelGGL(rnnt_grad_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, acts, labels,
-                       act_lens, label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, pre_scale, scale,
-                       grads);
-    HIP_OK(hipGetLastError());
+    launch_grad(acts, labels, act_lens, label_lens, d, denom, alphas, betas, llf, fastemit_lambda, clamp, pre_scale, scale,
+                grads, (hipStream_t)stream);
   });
 }
 
