@@ -14,3 +14,4 @@ for m in joint rnnt_train train decode; do
 done
 cat $O/smoke.txt | tail -1
 for f in $O/bench*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f',d['value'],d['ms_per_step'],d.get('roofline',{}).get('frac'))"; done
+timeout -k 10 400 rocprofv3 --kernel-trace -d $O/prof -o run -- python3 bench.py --mode rnnt_train --steps 3 --warmup 1 > $O/prof_bench.json 2>> $O/err.txt || exit 1
