@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "cfm_last_error", "cfm_version", "cfm_half_mode", "cfm_encoded_length", "cfm_encoder_create", "cfm_encoder_destroy",
     "cfm_encoder_set_weights", "cfm_encoder_param_count", "cfm_encoder_param_name", "cfm_encoder_param_numel",
     "cfm_encoder_set_max_audio_length", "cfm_encoder_set_pad_mask", "cfm_encoder_set_abs_pos", "cfm_encoder_abs_pos", "cfm_encoder_set_microbatches", "cfm_encoder_max_audio_length", "cfm_encoder_workspace_size",
-    "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_stage_clock_overhead", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_rel_attention_ws_size",
+    "cfm_encoder_forward", "cfm_num_stages", "cfm_stage_name", "cfm_encoder_forward_timed", "cfm_stage_clock_overhead", "cfm_op_layernorm", "cfm_op_linear", "cfm_op_linear_pack", "cfm_op_linear_packed", "cfm_op_rel_attention_ws_size",
     "cfm_op_rel_attention", "cfm_bench_gemm", "cfm_encoder_layers_workspace_size", "cfm_encoder_layers_forward",
     "cfm_op_conv_glu_dwconv_ws_size", "cfm_op_conv_glu_dwconv",
 )
@@ -155,6 +155,8 @@ def load(variant: str = "bf16") -> ctypes.CDLL:
         "cfm_op_conv_glu_dwconv_ws_size": (sz, [ci, ci, ci, ci, ci]),
         "cfm_op_conv_glu_dwconv": (ci, [ci, vp, vp, ci, ci, ci, ci, vp, vp, ci, vp, vp, vp, vp, vp, vp, sz, vp]),
         "cfm_op_linear": (ci, [ci, vp, ci, ci, vp, vp, ci, ci, vp, vp, ctypes.POINTER(sz), vp]),
+        "cfm_op_linear_pack": (ci, [ci, vp, vp, ci, ci, vp, ctypes.POINTER(sz), vp]),
+        "cfm_op_linear_packed": (ci, [ci, vp, ci, ci, vp, ci, ci, vp, vp]),
         "cfm_op_rel_attention_ws_size": (sz, [ci, ci, ci, ci, ci]),
         "cfm_bench_gemm": (ci, [ci, ci, ci, ci, ci, ci, ci, ctypes.POINTER(ctypes.c_float)]),
         "cfm_op_rel_attention": (ci, [ci, vp, vp, vp, vp, vp, vp, vp, ci, ci, ci, ci, ci, ci, vp, vp, vp]),

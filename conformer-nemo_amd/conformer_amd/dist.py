@@ -115,6 +115,7 @@ class GradBuckets:
             else:
                 self.rows.append(None)
         self.table_end = off
+        self.n_table_members = len(self.members)
         for p in other_params:
             if p.requires_grad and id(p) not in seen:
                 seen.add(id(p))
@@ -131,8 +132,12 @@ class GradBuckets:
         self._works = []
         self._reduced = []           # (start, end) slices already issued this step
         self._fresh, self._pending, self._finish_queued, self._scratch, self._direct = True, 0, False, None, True
+        self._rescale_owed = False   # the buffer holds sums reduced without averaging (see the step notes)
         for p, v in zip(self.members, self.views):
             p.grad = v
+        # the owed rescale runs before autograd adds a later backward's gradient into a non-table view
+        for p in self.members[self.n_table_members:]:
+            p.register_hook(self._pay_rescale_hook)
 
     # ---- per step -------------------------------------------------------------------------------
     # Gradient accumulation (several backward() calls per optimizer step, or an encoder run twice in
@@ -143,14 +148,28 @@ class GradBuckets:
     # end of the backward.  All-reducing the accumulated sum is exact: the part already reduced is equal
     # on every rank, so sum_r(avg(g1) + g2_r) / W = avg(g1) + avg(g2).  Without averaging the reduced
     # part R = sum(g1) would come back W times, so the buffer is scaled by 1/W before the next backward
-    # of the step writes into it: sum_r(R / W + g2_r) = sum(g1) + sum(g2).
+    # of the step writes into it: sum_r(R / W + g2_r) = sum(g1) + sum(g2).  That rescale is owed from
+    # the moment a finish() leaves reduced sums in the buffer and is paid by the first write of the next
+    # backward that actually runs - a gradient hook on every non-table member (it fires before autograd
+    # accumulates into the view) or `native_outputs` for the encoder rows - never by a forward: a
+    # train-mode forward with no backward after it must leave the reduced gradients alone, and with
+    # pipelined accumulation (fwd1, fwd2, bwd1, bwd2) the second forward runs before the first finish.
     # A new step is recognised by a member's .grad being None or not its view: use
     # zero_grad(set_to_none=True) (the default) or call begin_step(); after zero_grad(set_to_none=False)
     # the next backward is taken for an accumulation (still exact, but without the per-layer overlap).
+    def _pay_rescale(self) -> None:
+        if self._rescale_owed:
+            self._rescale_owed = False
+            self.flat.mul_(1.0 / self.world)
+
+    def _pay_rescale_hook(self, grad):
+        self._pay_rescale()
+        return grad
+
     def begin_step(self) -> None:
         """Start a new optimizer step explicitly: zero the buffer, the next backward overlaps per layer."""
         self.flat.zero_()
-        self._fresh, self._pending, self._finished = True, 0, False
+        self._fresh, self._pending, self._finished, self._rescale_owed = True, 0, False, False
         for p, v in zip(self.members, self.views):
             p.grad = v
 
@@ -163,11 +182,7 @@ class GradBuckets:
             self._fresh = True
             self._pending = 0
             self._finished = False
-        elif getattr(self, "_finished", False):
-            # a later backward of the same step: the buffer holds reduced gradients
-            if not self.average and self.world > 1:
-                self.flat.mul_(1.0 / self.world)
-            self._finished = False
+            self._rescale_owed = False
         for p, v in zip(self.members, self.views):
             if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                 p.grad = v
@@ -182,6 +197,7 @@ class GradBuckets:
     def native_outputs(self, params: Sequence[torch.Tensor], want: Sequence[bool]) -> List[Optional[torch.Tensor]]:
         """Output pointers for cfm_train_backward: table row i writes straight into its view (first
         backward of a fresh step) or into the accumulation scratch (see `accumulate_scratch`)."""
+        self._pay_rescale()
         direct = getattr(self, "_fresh", True)
         if direct:
             base = self.flat
@@ -237,6 +253,7 @@ class GradBuckets:
         try:
             self._finish_impl()
             self._finished = True
+            self._rescale_owed = not self.average and self.world > 1
         finally:
             self._finish_queued = False
             self._pending = 0

@@ -104,26 +104,50 @@ def masks_to_lengths(att_mask: Optional[torch.Tensor], pad_mask: Optional[torch.
 
 
 # ---- kernel-level ops ------------------------------------------------------------------------------
+# packed weights of `linear`, per (weight, bias, compute): reused while neither tensor changed (same
+# storage and autograd version), re-packed on the device otherwise (cfm_op_linear_pack, stream-ordered)
+_LINEAR_PACKS: "dict" = {}
+
+
+def _linear_pack(lib, mode, compute, weight, bias, dev):
+    key = (id(weight), id(bias) if bias is not None else None, compute, str(dev))
+    ver = (weight.data_ptr(), weight._version, tuple(weight.shape), str(weight.dtype),
+           None if bias is None else (bias.data_ptr(), bias._version))
+    hit = _LINEAR_PACKS.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1], hit[2], hit[3]
+    w = weight.detach().reshape(weight.shape[0], -1).to(dev, torch.float32).contiguous()
+    N, K = w.shape
+    b = None if bias is None else bias.detach().to(dev, torch.float32).contiguous()
+    need = ctypes.c_size_t(0)
+    _lib.check(lib.cfm_op_linear_pack(mode, None, None, N, K, None, ctypes.byref(need), _stream(dev)),
+               "cfm_op_linear_pack", lib)
+    ws = torch.empty(need.value, dtype=torch.uint8, device=dev)
+    _lib.check(lib.cfm_op_linear_pack(mode, w.data_ptr(), None if b is None else b.data_ptr(), N, K, ws.data_ptr(),
+                                      ctypes.byref(need), _stream(dev)), "cfm_op_linear_pack", lib)
+    if len(_LINEAR_PACKS) > 256:
+        _LINEAR_PACKS.clear()
+    # w / b are kept alive with the pack so the device copy above never reads freed memory, and weight /
+    # bias themselves so that their id() (the key) cannot be reused by another tensor while cached
+    _LINEAR_PACKS[key] = (ver, ws, N, K, w, b, weight, bias)
+    return ws, N, K
+
+
 def linear(x2d: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], act: int, compute: str) -> torch.Tensor:
-    """x2d (M, K) in the compute dtype -> (M, N) compute dtype; act 0 none, 1 relu, 2 swish (cfm_op_linear)."""
+    """x2d (M, K) in the compute dtype -> (M, N) compute dtype; act 0 none, 1 relu, 2 swish
+    (cfm_op_linear_pack once per weight version, then cfm_op_linear_packed)."""
     lib = _lib.load(_lib.variant_of(compute))
     dev = x2d.device
     M, K = x2d.shape
-    w = weight.detach().reshape(weight.shape[0], -1).to(dev, torch.float32).contiguous()
-    N = w.shape[0]
-    if w.shape[1] != K:
-        raise ValueError(f"weight has {w.shape[1]} input features, x has {K}")
-    b = None if bias is None else bias.detach().to(dev, torch.float32).contiguous()
+    mode = COMPUTE_ID[compute]
+    ws, N, Kw = _linear_pack(lib, mode, compute, weight, bias, dev)
+    if Kw != K:
+        raise ValueError(f"weight has {Kw} input features, x has {K}")
     y = torch.empty((M, N), dtype=COMPUTE_DTYPE[compute], device=dev)
     if M == 0:
         return y
-    need = ctypes.c_size_t(0)
-    mode = COMPUTE_ID[compute]
-    _lib.check(lib.cfm_op_linear(mode, x2d.data_ptr(), M, K, w.data_ptr(), None if b is None else b.data_ptr(), N, act,
-                                 y.data_ptr(), None, ctypes.byref(need), _stream(dev)), "cfm_op_linear", lib)
-    ws = torch.empty(need.value, dtype=torch.uint8, device=dev)
-    _lib.check(lib.cfm_op_linear(mode, x2d.data_ptr(), M, K, w.data_ptr(), None if b is None else b.data_ptr(), N, act,
-                                 y.data_ptr(), ws.data_ptr(), ctypes.byref(need), _stream(dev)), "cfm_op_linear", lib)
+    _lib.check(lib.cfm_op_linear_packed(mode, x2d.data_ptr(), M, K, ws.data_ptr(), N, act, y.data_ptr(), _stream(dev)),
+               "cfm_op_linear_packed", lib)
     return y
 
 

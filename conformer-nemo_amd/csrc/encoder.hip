@@ -1168,42 +1168,69 @@ cfm_status cfm_op_layernorm(int dtype, const float* x, int rows, int d, const fl
   });
 }
 
-cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w, const float* bias, int N, int act,
-                         void* y, void* pack_ws, size_t* pack_ws_bytes, void* stream) {
+// The packed operand of cfm_op_linear: [Np][Kp] compute type | fp32 bias [Np] | a 4 KiB zero page.
+static size_t linear_pack_bytes(int dt, int N, int K, long* Kp_out = nullptr, long* Np_out = nullptr) {
+  const int es = dtype_size(dt);
+  const long Kp = round_up(K, GEMM_BK_BYTES / es), Np = round_up(N, GEMM_BN);
+  if (Kp_out) *Kp_out = Kp;
+  if (Np_out) *Np_out = Np;
+  return (size_t)(Np * Kp * es + round_up(Np * 4, 256) + 4096);
+}
+
+// w (N, K) fp32 + bias -> pack_ws, on the device and stream-ordered (no host round trip, no sync)
+cfm_status cfm_op_linear_pack(int dtype, const float* w, const float* bias, int N, int K, void* pack_ws,
+                              size_t* pack_ws_bytes, void* stream) {
   return guarded([&] {
     const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
-    const long Kp = round_up(K, GEMM_BK_BYTES / es), Np = round_up(N, GEMM_BN);
-    const size_t need = (size_t)(Np * Kp * es + round_up(Np * 4, 256) + 4096);
+    if (N <= 0 || K <= 0) fail(CFM_ERR_INVALID_ARG, "N and K must be positive");
+    long Kp, Np;
+    const size_t need = linear_pack_bytes(dt, N, K, &Kp, &Np);
     if (!pack_ws) {
       if (!pack_ws_bytes) fail(CFM_ERR_INVALID_ARG, "pack_ws_bytes");
       *pack_ws_bytes = need;
       return;
     }
+    if (!w) fail(CFM_ERR_INVALID_ARG, "null weight");
     if (K % (16 / es)) fail(CFM_ERR_UNSUPPORTED, "K must be a multiple of 16 bytes");
     if (pack_ws_bytes && *pack_ws_bytes < need) fail(CFM_ERR_WORKSPACE, "pack workspace too small");
     hipStream_t st = (hipStream_t)stream;
-    std::vector<float> hw((size_t)N * K), hb(Np, 0.0f);
-    HIP_OK(hipMemcpy(hw.data(), w, hw.size() * 4, hipMemcpyDeviceToHost));
-    if (bias) HIP_OK(hipMemcpy(hb.data(), bias, N * 4, hipMemcpyDeviceToHost));
-    std::vector<char> packed((size_t)(Np * Kp * es), 0);
-    for (int n = 0; n < N; ++n)
-      for (int k = 0; k < K; ++k) {
-        const float v = hw[(size_t)n * K + k];
-        if (es == 4) ((float*)packed.data())[n * Kp + k] = v;
-        else ((uint16_t*)packed.data())[n * Kp + k] = host_f2bf(v);
-      }
     char* base = (char*)pack_ws;
     char* bdev = base + Np * Kp * es;
     char* zero = bdev + round_up(Np * 4, 256);
-    HIP_OK(hipMemcpy(base, packed.data(), packed.size(), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(bdev, hb.data(), Np * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemset(zero, 0, 4096));
+    pack_matrix(dt, w, K, N, K, false, base, Kp, (int)Np, (int)Kp, st);
+    HIP_OK(hipMemsetAsync(bdev, 0, (size_t)Np * 4, st));
+    if (bias) HIP_OK(hipMemcpyAsync(bdev, bias, (size_t)N * 4, hipMemcpyDeviceToDevice, st));
+    HIP_OK(hipMemsetAsync(zero, 0, 4096, st));
+    HIP_OK(hipGetLastError());
+  });
+}
+
+cfm_status cfm_op_linear_packed(int dtype, const void* x, int M, int K, const void* pack_ws, int N, int act, void* y,
+                                void* stream) {
+  return guarded([&] {
+    const int dt = dtype == CFM_COMPUTE_FP32 ? DT_F32 : DT_BF16, es = dtype_size(dt);
+    if (!x || !pack_ws || !y) fail(CFM_ERR_INVALID_ARG, "null argument");
+    if (M < 0 || N <= 0 || K <= 0) fail(CFM_ERR_INVALID_ARG, "bad shape");
+    if (K % (16 / es)) fail(CFM_ERR_UNSUPPORTED, "K must be a multiple of 16 bytes");
+    long Kp, Np;
+    linear_pack_bytes(dt, N, K, &Kp, &Np);
+    const char* base = (const char*)pack_ws;
+    const char* bdev = base + Np * Kp * es;
+    const char* zero = bdev + round_up(Np * 4, 256);
     GemmEpi e = epi_of(act == 1 ? EPI_RELU : act == 2 ? EPI_SWISH : EPI_STORE, (const float*)bdev);
     e.C = y;
     e.ldc = N;
-    gemm(dt, x, K, M, K, base, (int)Kp, N, e, zero, st);
+    gemm(dt, x, K, M, K, base, (int)Kp, N, e, zero, (hipStream_t)stream);
     HIP_OK(hipGetLastError());
   });
+}
+
+cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w, const float* bias, int N, int act,
+                         void* y, void* pack_ws, size_t* pack_ws_bytes, void* stream) {
+  if (!pack_ws) return cfm_op_linear_pack(dtype, w, bias, N, K, nullptr, pack_ws_bytes, stream);
+  const cfm_status s = cfm_op_linear_pack(dtype, w, bias, N, K, pack_ws, pack_ws_bytes, stream);
+  if (s != CFM_OK) return s;
+  return cfm_op_linear_packed(dtype, x, M, K, pack_ws, N, act, y, stream);
 }
 
 // ---- ConformerConvolution's middle (conformer_modules.py:164-176) as a kernel-level op --------

@@ -1279,7 +1279,10 @@ __global__ __launch_bounds__(256) void conv12_patch_kernel(const float* __restri
                                                            int F1, uint4* __restrict__ patch, const float* __restrict__ w1,
                                                            const float* __restrict__ b1, int C, uint4* __restrict__ w1h) {
   typedef __attribute__((ext_vector_type(2))) _Float16 h2;
-  auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, h2{(_Float16)a, (_Float16)b}); };
+  // saturated to the fp16 range (v_med3_f32) before the conversion: an input or weight beyond +-65504
+  // gives a clamped product instead of inf / NaN in X1 (the two-kernel path stays in fp32 there)
+  auto sat = [](float v) { return (_Float16)__builtin_amdgcn_fmed3f(v, -65504.0f, 65504.0f); };
+  auto pk = [&](float a, float b) { return __builtin_bit_cast(uint32_t, h2{sat(a), sat(b)}); };
   const int W = F1 + 2, Hh = T1 + 2;
   const long n = (long)B * Hh * W;
   if (blockIdx.x == 0)   // conv.0 weights as [c][16] fp16 rows: W1[c][0..8], b1[c], zeros

@@ -33,8 +33,11 @@ using namespace cfm;
 struct cfm_rnnt_decoder {
   int V = 0, H = 0, L = 0, device = 0;
   float* wbuf = nullptr;        // emb (V+1, H) | per layer [W_ih | W_hh] (4H, 2H) | per layer bias (4H)
-  long emb_off = 0, w_off = 0, b_off = 0, x_off = -1;   // x_off >= 0: the layer-0 input table below
+  long emb_off = 0, w_off = 0, b_off = 0;
+  bool x_want = false;          // the matrix-core step can use the layer-0 input table below
   bool x_ready = false;         // the table matches the current weights (set_weights clears it)
+  float* xbuf = nullptr;        // that table: allocated by the first inference call (ensure_xtab), never by
+                                // training-only handles ((V+1) x 4H fp32: 10.5 MB at V 1024 / H 640, 134 MB at V 8192)
   int* host_flag = nullptr;     // pinned, 2 slots (greedy done-flag polling)
   hipEvent_t ev[2] = {nullptr, nullptr};
   const float* emb() const { return wbuf + emb_off; }
@@ -42,7 +45,7 @@ struct cfm_rnnt_decoder {
   const float* bias(int l) const { return wbuf + b_off + (long)l * 4 * H; }
   // layer 0's input projection for every embedding row: xtab[e][r] = sum_k emb[e][k] W_ih[r][k], (V+1, 4H),
   // built on first use after set_weights; inference steps gather a row instead of contracting over the input
-  float* xtab() const { return x_off >= 0 ? wbuf + x_off : nullptr; }
+  float* xtab() const { return xbuf; }
 };
 
 namespace {
@@ -651,8 +654,14 @@ void launch_lstm_step(const cfm_rnnt_decoder* d, int l, const int32_t* xlab, con
 // (re)build the layer-0 input table after set_weights, on the stream of the call that will read it; only
 // when the matrix-core step can take it (shapes above; CFM_LSTM_XTAB=0 disables it)
 void ensure_xtab(cfm_rnnt_decoder* d, hipStream_t st) {
-  if (d->x_ready || !d->xtab()) return;
+  if (d->x_ready || !d->x_want) return;
   const int H = d->H, N = 4 * H, M = d->V + 1;
+  if (!d->xbuf && hipMalloc((void**)&d->xbuf, (size_t)M * N * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();   // no room for the table: the steps contract over [x | h] as training does
+    d->xbuf = nullptr;
+    d->x_want = false;
+    return;
+  }
   hipLaunchKernelGGL(lstm_xtab_kernel, dim3((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64)), dim3(256), 0, st,
                      d->emb(), d->W(0), M, N, H, 2 * H, d->xtab());
   HIP_OK(hipGetLastError());
@@ -956,10 +965,7 @@ cfm_status cfm_rnnt_decoder_create(int vocab_size, int pred_hidden, int layers, 
     d->b_off = d->w_off + (long)layers * 4 * H * 2 * H;
     long total = d->b_off + (long)layers * 4 * H;
     static const int xtab_on = [] { const char* e = getenv("CFM_LSTM_XTAB"); return e ? atoi(e) : 1; }();
-    if (xtab_on && H % 16 == 0 && lstm_mfma_nt((int)(H / 16 + 7) / 8)) {
-      d->x_off = round_up(total, 64);
-      total = d->x_off + (long)(vocab_size + 1) * 4 * H;
-    }
+    d->x_want = xtab_on && H % 16 == 0 && lstm_mfma_nt((int)(H / 16 + 7) / 8);
     hipError_t e = hipMalloc((void**)&d->wbuf, total * sizeof(float));
     if (e == hipSuccess) e = hipHostMalloc((void**)&d->host_flag, 2 * sizeof(int), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&d->ev[0], hipEventDisableTiming);
@@ -976,6 +982,7 @@ void cfm_rnnt_decoder_destroy(cfm_rnnt_decoder* d) {
   if (!d) return;
   (void)hipSetDevice(d->device);
   if (d->wbuf) (void)hipFree(d->wbuf);
+  if (d->xbuf) (void)hipFree(d->xbuf);
   if (d->host_flag) (void)hipHostFree(d->host_flag);
   for (auto& e : d->ev)
     if (e) (void)hipEventDestroy(e);

@@ -64,10 +64,17 @@ class _RNNTNative(torch.autograd.Function):
         # the backward writes it once, already scaled (cfm_rnnt_loss_grad, the same fp32 roundings) - one
         # pass over the (B, T, U, V) tensor instead of three.  CFM_RNNT_DEFER_GRAD=0: the reference order.
         defer = acts.requires_grad and os.environ.get("CFM_RNNT_DEFER_GRAD", "1") != "0"
-        ctx.state, ctx.pre = None, 1.0
+        ctx.state, ctx.pre, ctx.alias = None, 1.0, False
         if defer:
             costs, grads, ctx.state = rnnt_loss(acts, labels, act_lens, label_lens, blank, fastemit_lambda, clamp,
                                                 want_grads=False, keep_state=True)
+            if ctx.state[0].data_ptr() == acts.data_ptr():
+                # the kept logits ARE acts: save them through autograd, so that an in-place change of acts
+                # before the backward raises (version check) and a second backward through a freed graph
+                # raises as usual, while a retained graph can be differentiated again
+                ctx.save_for_backward(acts)
+                ctx.state = (None,) + tuple(ctx.state[1:])
+                ctx.alias = True
         else:
             costs, grads = rnnt_loss(acts, labels, act_lens, label_lens, blank, fastemit_lambda, clamp,
                                      want_grads=acts.requires_grad)
@@ -86,8 +93,11 @@ class _RNNTNative(torch.autograd.Function):
     def backward(ctx, grad_output):
         if grad_output is not None and ctx.state is not None:
             from conformer_amd.rnnt_loss import rnnt_loss_grad
-            grads = rnnt_loss_grad(ctx.state, ctx.pre, grad_output)
-            ctx.state = None
+            state = ctx.state
+            if ctx.alias:
+                state = (ctx.saved_tensors[0],) + tuple(state[1:])
+            # the state stays with the node: a retained graph gets the same gradient on every backward
+            grads = rnnt_loss_grad(state, ctx.pre, grad_output)
             return grads, None, None, None, None, None, None, None
         if grad_output is not None and ctx.grads is not None:
             grad_output = grad_output.view(-1, 1, 1, 1).to(ctx.grads)

@@ -183,9 +183,20 @@ cfm_status cfm_stage_clock_overhead(void* stream, int n, float* us_per_kernel);
 cfm_status cfm_op_layernorm(int dtype, const float* x, int rows, int d, const float* w, const float* b, float* y_f32,
                             void* y_t, void* stream);
 /* y[M,N] = x[M,K] . w[N,K]^T + bias (fp32 weights, packed internally into `pack_ws`).
- * act: 0 none, 1 relu, 2 swish.  Returns the pack workspace size when pack_ws == NULL. */
+ * act: 0 none, 1 relu, 2 swish.  Returns the pack workspace size when pack_ws == NULL.
+ * Equivalent to cfm_op_linear_pack followed by cfm_op_linear_packed (nn.Linear.forward, used by the
+ * ConformerFeedForward / MultiHeadAttention projections run standalone, conformer_modules.py:195-200,
+ * multi_head_attention.py:71-75, 115). */
 cfm_status cfm_op_linear(int dtype, const void* x, int M, int K, const float* w, const float* bias, int N, int act,
                          void* y, void* pack_ws, size_t* pack_ws_bytes, void* stream);
+/* Pack w (N, K) fp32 and bias (N, or NULL) into pack_ws on the device, ordered on `stream` (no host
+ * synchronisation): pack_ws == NULL returns its size in *pack_ws_bytes.  A packed buffer stays valid
+ * for every later cfm_op_linear_packed call until the weights change (cache it per weight version). */
+cfm_status cfm_op_linear_pack(int dtype, const float* w, const float* bias, int N, int K, void* pack_ws,
+                              size_t* pack_ws_bytes, void* stream);
+/* y[M,N] = x[M,K] . W^T + bias (+ act) from a cfm_op_linear_pack buffer of the same dtype, N, K. */
+cfm_status cfm_op_linear_packed(int dtype, const void* x, int M, int K, const void* pack_ws, int N, int act, void* y,
+                                void* stream);
 /* Fused rel-pos attention core on projected q,k,v (M = B*T' rows, d = H*dk, compute type):
  * out[M, d] = softmax_mask(((q+u)k^T + rel_shift((q+v)p^T)) / sqrt(dk)) v, p = pos projection
  * rows (2T'-1, d).  Scratch `ws` of cfm_op_rel_attention_ws_size bytes. */

@@ -156,10 +156,13 @@ def test_bucketed_overlapped_allreduce_equals_flat_gloo_ws2():
         assert issued == [(12, 24), (0, 12), (24, 30)]
 
 
-def _accum_worker(rank, world, port, q, average=True):
+def _accum_worker(rank, world, port, q, average=True, order="interleaved"):
     """Two micro-batches per optimizer step through GradBuckets (accumulation): the first
     native backward writes into the views with overlapped per-layer all-reduces, the second writes into
-    the scratch and is added in; the result must equal the flat all-reduce of the summed plain grads."""
+    the scratch and is added in; the result must equal the flat all-reduce of the summed plain grads.
+    order "interleaved": fwd1 bwd1 fwd2 bwd2; "pipelined": fwd1 fwd2 bwd1 bwd2 (the second
+    forward runs before the first backward's finish).  Either way a train-mode forward after the last
+    backward (no backward of its own) must leave the reduced gradients unchanged."""
     sys.path.insert(0, os.path.join(ROOT, "conformer-nemo_amd"))
     from conformer_amd import dist as cdist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -174,23 +177,37 @@ def _accum_worker(rank, world, port, q, average=True):
         for p in P + [head]:
             p.grad = None                                      # zero_grad(set_to_none=True)
         overlaps = []
-        for vals, hv in micro:                                 # two forward/backward pairs, one step
-            gb.attach()                                        # what the train forward does
-            overlaps.append(gb.overlap)
+
+        def backward(vals, hv):
+            (head * hv).sum().backward()                       # the head's autograd accumulation into its view
             outs = gb.native_outputs(P, want)                  # what cfm_train_backward writes into
             for i, v in vals.items():
                 outs[i].copy_(v.reshape(-1))                   # overwrite semantics, as the kernels
             if gb.overlap:
                 gb.on_ready(0, 3)
             gb.after_backward()
-            head.grad += hv                                    # autograd accumulation into the view
             gb.finish()
+
+        if order == "interleaved":
+            for vals, hv in micro:                             # two forward/backward pairs, one step
+                gb.attach()                                    # what the train forward does
+                overlaps.append(gb.overlap)
+                backward(vals, hv)
+        else:
+            for _ in micro:
+                gb.attach()
+                overlaps.append(gb.overlap)
+            for vals, hv in micro:
+                backward(vals, hv)
         got = [p.grad.clone() for p in P + [head]]
+        gb.attach()                                            # a train-mode forward with no backward
+        after_fwd = [p.grad.clone() for p in P + [head]]
         Q = [torch.nn.Parameter(torch.zeros(t.shape)) for t in P + [head]]
         for j, qp in enumerate(Q):
             qp.grad = sum((micro[k][0][j] if j < 3 else micro[k][1]) for k in range(2)).clone()
         cdist.allreduce_gradients(Q, average=average)
         close = all(torch.allclose(a, qp.grad, rtol=1e-6, atol=1e-6) for a, qp in zip(got, Q))
+        close = close and all(torch.equal(a, b) for a, b in zip(got, after_fwd))
         # a new step (grads set to None) starts from zero again
         for p in P + [head]:
             p.grad = None
@@ -207,14 +224,16 @@ def _accum_worker(rank, world, port, q, average=True):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("order", ["interleaved", "pipelined"])
 @pytest.mark.parametrize("average", [True, False])
-def test_gradient_accumulation_through_buckets_gloo_ws2(average):
+def test_gradient_accumulation_through_buckets_gloo_ws2(average, order):
     """with average=False the reduced part of the first backward must not come back
-    world times after the second backward's all-reduce."""
+    world times after the second backward's all-reduce; ADVICE r04: nor in the pipelined order, and a
+    forward after the last backward must not rescale the reduced gradients."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q, average)) for r in range(world)]
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q, average, order)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -92,6 +92,35 @@ def test_deferred_gradient_is_bitwise_the_reference_order(path, monkeypatch):
         assert torch.equal(a, b), red
 
 
+def test_deferred_gradient_retained_graph_and_inplace_guard(monkeypatch):
+    """the deferred gradient keeps its state with the autograd node, so a retained graph gives
+    the same gradient on a second backward (accumulated twice, as the reference order does); acts are
+    saved through autograd, so changing them in place between forward and backward raises."""
+    from nemo.collections.asr.losses.rnnt import RNNTLossNumba
+    z = np.load(FILES[0])
+    blank = int(z["blank"])
+    kw = {"fastemit_lambda": float(z["fastemit_lambda"]), "clamp": float(z["clamp"])}
+    grads = {}
+    for defer in ("1", "0"):
+        monkeypatch.setenv("CFM_RNNT_DEFER_GRAD", defer)
+        acts, labels, al, ll = _inputs(z)
+        out = RNNTLossNumba(blank=blank, reduction="sum", **kw)(acts, labels, al, ll)
+        out.backward(retain_graph=True)
+        g1 = acts.grad.clone()
+        out.backward()
+        assert torch.isfinite(acts.grad).all()
+        grads[defer] = (g1, acts.grad.clone())
+    assert torch.equal(grads["1"][0], grads["0"][0])
+    assert torch.equal(grads["1"][1], 2 * grads["1"][0])
+    monkeypatch.setenv("CFM_RNNT_DEFER_GRAD", "1")
+    acts, labels, al, ll = _inputs(z)
+    out = RNNTLossNumba(blank=blank, reduction="sum", **kw)(acts, labels, al, ll)
+    with torch.no_grad():
+        acts.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.backward()
+
+
 def test_cfg4_shape_against_oracle_and_no_grad():
     """BASELINE config-4-like lattice (V+1=1025, U+1=21, T=40, ragged) vs the oracle; forward-only
     (no grads) returns the same costs."""

@@ -31,7 +31,8 @@ def attn(iters):
 GEMM_SHAPES = {"ffn_up": (8000, 2048, 512, 2), "ffn_down": (8000, 512, 2048, 3), "qkv": (8000, 1536, 512, 6), "qkvs": (8000, 1536, 512, 0), "qkvs4k": (4000, 1536, 512, 0),
                "ffn_up4k": (4000, 2048, 512, 2), "ffn_down4k": (4000, 512, 2048, 3), "out4k": (4000, 512, 512, 3),
                "out": (8000, 512, 512, 3), "ffd_split2": (16000, 512, 1024, 4), "ffd_split4": (32000, 512, 512, 4),
-               "ffd": (8000, 512, 2048, 4), "ref4096": (4096, 4096, 4096, 0), "conv2": (160000, 512, 4608, 0)}
+               "ffd": (8000, 512, 2048, 4), "ref4096": (4096, 4096, 4096, 0), "conv2": (160000, 512, 4608, 0),
+               "ref4096s": (4096, 4096, 4096, 2), "conv2s": (160000, 512, 4608, 2)}
 
 
 def gemm(iters):
