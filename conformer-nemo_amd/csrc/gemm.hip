@@ -73,9 +73,16 @@ struct Tile {
   static CFM_DEV int swz(int row) { return (row / SWDIV) % SLOTS; }
 };
 // The rows of one epilogue pass, seen by the epilogue as a (BM/EP) x BN tile.
-template <class TL>
+template <class TL, bool SWZ_ = false>
 struct EpiView {
   static constexpr int BM = TL::BM / TL::EP, BN = TL::BN, NT = TL::NT, EPS = TL::EPS;
+  // fp32 image element (r, c).  SWZ: the swapped-operand tiles write 4 consecutive columns of one row per
+  // lane (ds_write_b128), so the 16-byte slots of a row are XOR-swizzled by (r & 7): the 8 rows of a
+  // write lane group then hit 8 distinct slots (conflict-free), and so do the row-wise float4 reads.
+  static CFM_DEV int fidx(int r, int c) {
+    if constexpr (SWZ_) return r * EPS + ((((c >> 2) ^ (r & 7)) << 2) | (c & 3));
+    else return r * EPS + c;
+  }
 };
 
 using T128x128 = Tile<128, 128, 2, 2, 2>;   // 2 x 32 KiB ring: 2 blocks / CU
@@ -234,6 +241,10 @@ struct ALoadTConv {
 };
 
 thread_local int g_splits = 1;
+// bf16 dense STORE / RELU / SWISH / RESID GEMMs with swapped MFMA operands and register epilogues
+// (gemm_kernel's SW); CFM_GEMM_SWAP=0 keeps the unswapped kernels
+int g_gemm_swap = [] { const char* s = getenv("CFM_GEMM_SWAP"); return s ? atoi(s) : 0; }();
+
 constexpr int LN_PRE = 4;   // folded-LayerNorm granule partials prefetched per row (d <= 512 fully)   // grid.y of the next split-K launch (gemm_splitk)
 
 struct GemmParams {
@@ -363,7 +374,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
-      const float4 a = *(const float4*)(img + r * TL::EPS + cc * 4);
+      const float4 a = *(const float4*)(img + TL::fidx(r, cc * 4));
       float4 o;
       if constexpr (EPI == EPI_RESID) {
         if (e.drop.thr) {   // training: x_out = x_in + alpha * dropout(branch)
@@ -772,8 +783,25 @@ CFM_DEV void ln2_tables(const P& p, int m0, int n0, int BM, int BN, const float2
   }
 }
 
-template <typename T, int EPI, class TL, class ALoad>
+// SW (bf16 dense STORE / RELU / SWISH / RESID): the MFMA operands are swapped (weight rows as the A
+// operand), so each lane's accumulator groups hold 4 consecutive output COLUMNS of one row.  The epilogue
+// then works from registers: RESID writes its fp32 image as float4 runs (swizzled, EpiView SWZ), the
+// compute-type outputs apply bias / fold / activation in registers and write a bf16 image of the whole
+// tile in one pass (8-byte runs, 16-byte slots swizzled by row % 16) that is copied out as 16-byte rows.
+// Same products in the same K order: bitwise the same values as the unswapped kernel.
+template <typename T, int EPI, class TL, bool SW>
+struct SwapCfg {
+  static constexpr bool OUT16 = SW && (EPI == EPI_SWISH || EPI == EPI_STORE || EPI == EPI_RELU);
+  static constexpr bool F32 = SW && EPI == EPI_RESID;
+  static_assert(!SW || sizeof(T) == 2, "swapped operands: 16-bit compute type only");
+  static_assert(!OUT16 || TL::BM * TL::BN * 2 <= TL::RS_OFF, "bf16 tile image fits below the tables");
+  static_assert(!OUT16 || TL::BN >= 128, "bf16 image swizzle needs >= 16 slots per row");
+  static_assert(!F32 || TL::EP == 1, "swapped RESID: one epilogue pass");
+};
+
+template <typename T, int EPI, class TL, class ALoad, bool SW = false>
 __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload) {
+  using SC = SwapCfg<T, EPI, TL, SW>;
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -907,7 +935,10 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
           for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-            for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], cur[kk][i], cur[kk][TL::MR + j]);
+            for (int j = 0; j < TL::NR; ++j) {
+              if constexpr (SW) mfma_slab<T>(acc[i][j], cur[kk][TL::MR + j], cur[kk][i]);
+              else mfma_slab<T>(acc[i][j], cur[kk][i], cur[kk][TL::MR + j]);
+            }
         }
       };
       for (int kt = 0; kt < nk; kt += 2) {
@@ -919,39 +950,58 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   if (!ahead) {
     // Software pipeline: the fragments of substep g+1 are read from LDS while the MFMAs of substep
     // g run.  The ring wait + barrier for K-step kt+1 sit in front of the LAST substep of kt, so the
-    // first fragments of kt+1 are already in registers when kt+1 starts.
+    // first fragments of kt+1 are already in registers when kt+1 starts.  Two fragment sets alternate
+    // by substep parity (compile-time indices): a copy of the next set into the current one at the
+    // end of each substep made hipcc wait for the reads it had just issued (lgkmcnt(0) ahead of the
+    // copy), exposing every LDS read latency; with the alternation nothing waits on the reads in flight
+    // until the substep that uses them.  An odd substep count runs the K-step loop unrolled by two.
     wait_stages<G, NS - 2>(min(NS - 2, nk - 1));
     wait_lgkm0();
     raw_barrier();
-    uint4 afc[TL::MR], bfc[TL::NR];
-    read_frags(smem, 0, afc, bfc);
+    uint4 fa[2][TL::MR], fb[2][TL::NR];
+    read_frags(smem, 0, fa[0], fb[0]);
     int slot = 0;
-    for (int kt = 0; kt < nk; ++kt) {
+    auto kstep = [&](int kt, auto par0) {
+      constexpr int P0 = decltype(par0)::value;   // the set holding this K-step's first fragments
       // refill the slot K-step kt-1 used: every wave finished reading it before the last barrier
       if (kt + NS - 1 < nk && !(p.probe & 1)) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
       const char* Sb = smem + slot * TL::STAGE_BYTES;
       const int nslot = (slot == NS - 1) ? 0 : slot + 1;
 #pragma unroll
       for (int kk = 0; kk < KSUB; ++kk) {
-        uint4 afn[TL::MR], bfn[TL::NR];
-        if (kk + 1 < KSUB) {
-          read_frags(Sb, kk + 1, afn, bfn);
-        } else if (kt + 1 < nk) {
+        const int cur = (P0 + kk) & 1;
+        const bool last = kk + 1 == KSUB, more = kt + 1 < nk;
+        if (!last) {
+          read_frags(Sb, kk + 1, fa[cur ^ 1], fb[cur ^ 1]);
+        } else if (more) {
           wait_stages<G, NS - 2>(min(NS - 2, nk - 2 - kt));   // K-step kt+1 has landed
-          wait_lgkm0();
+          // lgkmcnt(0) through the builtin, which hipcc's wait pass sees (this wave's reads of kt are done)
+          __builtin_amdgcn_s_waitcnt(0xC07F);
           raw_barrier();
-          read_frags(smem + nslot * TL::STAGE_BYTES, 0, afn, bfn);
         }
 #pragma unroll
         for (int i = 0; i < TL::MR; ++i)
 #pragma unroll
-          for (int j = 0; j < TL::NR; ++j) mfma_slab<T>(acc[i][j], afc[i], bfc[j]);
-#pragma unroll
-        for (int i = 0; i < TL::MR; ++i) afc[i] = afn[i];
-#pragma unroll
-        for (int j = 0; j < TL::NR; ++j) bfc[j] = bfn[j];
+          for (int j = 0; j < TL::NR; ++j) {
+            if constexpr (SW) mfma_slab<T>(acc[i][j], fb[cur][j], fa[cur][i]);
+            else mfma_slab<T>(acc[i][j], fa[cur][i], fb[cur][j]);
+          }
+        if (last && more) {
+          // the next K-step's first fragments are read behind this substep's MFMAs, whose operands are
+          // already in registers (read ahead of them, hipcc waited for these reads before the MFMAs)
+          __builtin_amdgcn_sched_barrier(0);
+          read_frags(smem + nslot * TL::STAGE_BYTES, 0, fa[cur ^ 1], fb[cur ^ 1]);
+        }
       }
       slot = nslot;
+    };
+    if constexpr (KSUB % 2 == 0) {
+      for (int kt = 0; kt < nk; ++kt) kstep(kt, std::integral_constant<int, 0>{});
+    } else {
+      for (int kt = 0; kt < nk; kt += 2) {
+        kstep(kt, std::integral_constant<int, 0>{});
+        if (kt + 1 < nk) kstep(kt + 1, std::integral_constant<int, 1>{});
+      }
     }
   }
 
@@ -969,7 +1019,50 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   raw_barrier();                         // every wave is done reading the ring
   float* img = (float*)smem;
   const int col = lane & 31;
-  if constexpr (TL::KG > 1) {
+  if constexpr (TL::KG > 1 && SW) {
+    // as below, with float4 runs of the swapped layout (4 consecutive columns per accumulator group)
+    using EV = EpiView<TL, true>;
+    auto at4 = [&](int i, int j, int g) -> float4* {
+      const int r = wm * (TL::BM / TL::WM) + i * 32 + col;
+      const int c = wn * (TL::BN / TL::WN) + j * 32 + 8 * g + 4 * (lane >> 5);
+      return (float4*)(img + EV::fidx(r, c));
+    };
+#pragma unroll
+    for (int g = 1; g < TL::KG; ++g) {
+      if (kg == g) {
+#pragma unroll
+        for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+          for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              float4* d = at4(i, j, q4);
+              const float4 v = make_float4(acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2],
+                                           acc[i][j][4 * q4 + 3]);
+              if (g == 1) {
+                *d = v;
+              } else {
+                const float4 o = *d;
+                *d = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+              }
+            }
+      }
+      __syncthreads();
+    }
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+        for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const float4 o = *at4(i, j, q4);
+            acc[i][j][4 * q4] += o.x; acc[i][j][4 * q4 + 1] += o.y;
+            acc[i][j][4 * q4 + 2] += o.z; acc[i][j][4 * q4 + 3] += o.w;
+          }
+    }
+    __syncthreads();
+  } else if constexpr (TL::KG > 1) {
     // the other K-groups hand their partial sums to K-group 0 through the image, in a fixed order
     // (img = p1; img += p2; ...; acc0 += img): bitwise reproducible, the same for every tile with
     // the same K-grouping
@@ -1005,7 +1098,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   float bcol[TL::NR];                    // bias arrays are zero-padded to the N granule (GEMM_BN)
 #pragma unroll
   for (int j = 0; j < TL::NR; ++j) bcol[j] = 0.0f;
-  if (p.epi.bias) {
+  if (p.epi.bias && !SW) {
 #pragma unroll
     for (int j = 0; j < TL::NR; ++j) bcol[j] = p.epi.bias[n0 + wn * (TL::BN / TL::WN) + j * 32 + col];
   }
@@ -1034,6 +1127,93 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     }
     if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
     if (tid < TL::BN && p.epi.ln_in) cd_tab[tid] = cd_pre;
+  }
+  if constexpr (SW) {
+    // this lane's 4-column bias runs (zero-padded arrays: every read in range)
+    float4 b4[TL::NR][4];
+#pragma unroll
+    for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        b4[j][q4] = p.epi.bias ? *(const float4*)(p.epi.bias + n0 + wn * (TL::BN / TL::WN) + j * 32 + 8 * q4 + 4 * (lane >> 5))
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (SC::F32) {
+      using EV = EpiView<TL, true>;
+      if (kg == 0) {
+#pragma unroll
+        for (int i = 0; i < TL::MR; ++i)
+#pragma unroll
+          for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const int r = wm * (TL::BM / TL::WM) + i * 32 + col;
+              const int c = wn * (TL::BN / TL::WN) + j * 32 + 8 * q4 + 4 * (lane >> 5);
+              *(float4*)(img + EV::fidx(r, c)) =
+                  make_float4(acc[i][j][4 * q4] + b4[j][q4].x, acc[i][j][4 * q4 + 1] + b4[j][q4].y,
+                              acc[i][j][4 * q4 + 2] + b4[j][q4].z, acc[i][j][4 * q4 + 3] + b4[j][q4].w);
+            }
+      }
+      __syncthreads();
+      if (p.epi.ln_in || p.epi.ln_out)
+        epilogue<T, EPI, EV, true>(p, img, m0, n0, (long)blockIdx.y * p.split_x, rs_tab, cd_tab);
+      else
+        epilogue<T, EPI, EV, false>(p, img, m0, n0, (long)blockIdx.y * p.split_x, rs_tab, cd_tab);
+      return;
+    } else {
+      // compute-type output from registers into a bf16 image [BM][BN] (16-byte slots ^ row % 16)
+      constexpr int RB = TL::BN * 2, SL = TL::BN / 8;
+      char* im = smem;
+      __syncthreads();                   // the tables are visible; every wave is done with the image above
+      if (kg == 0) {
+        const bool fold = p.epi.ln_in != nullptr, fold2 = p.epi.ln2_in != nullptr;
+#pragma unroll
+        for (int i = 0; i < TL::MR; ++i) {
+          const int r = wm * (TL::BM / TL::WM) + i * 32 + col;
+          float2 st = make_float2(0.f, 0.f), st2 = make_float2(0.f, 0.f);
+          if (fold) st = rs_tab[r];
+          if (fold2) st2 = rs2_tab[r];
+#pragma unroll
+          for (int j = 0; j < TL::NR; ++j)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const int c = wn * (TL::BN / TL::WN) + j * 32 + 8 * q4 + 4 * (lane >> 5);
+              const float bb[4] = {b4[j][q4].x, b4[j][q4].y, b4[j][q4].z, b4[j][q4].w};
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float a = acc[i][j][4 * q4 + e];
+                if (fold2) a = ln_fold2(st, st2, a, cd_tab[c + e], c23_tab[c + e]);
+                else if (fold) a = ln_fold(st, a, cd_tab[c + e]);
+                else a += bb[e];
+                if constexpr (EPI == EPI_RELU) a = fmaxf(a, 0.0f);
+                if constexpr (EPI == EPI_SWISH) a = swishf(a);
+                v[e] = a;
+              }
+              const uint2 pk = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                          (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+              *(uint2*)(im + r * RB + ((((c >> 3) ^ (r & 15)) << 4) | ((c & 4) * 2))) = pk;
+            }
+        }
+      }
+      __syncthreads();
+      const bool vec = (p.epi.ldc * (long)sizeof(T)) % 16 == 0;
+#pragma unroll 4
+      for (int idx = tid; idx < TL::BM * SL; idx += TL::NT) {
+        const int r = idx / SL, c = idx - r * SL;
+        const int m = m0 + r, n = n0 + 8 * c;
+        if (m >= p.M || n >= p.N) continue;
+        const uint4 v = *(const uint4*)(im + r * RB + ((c ^ (r & 15)) << 4));
+        if (vec && n + 8 <= p.N) {
+          if (p.epi.wt) store16_wt(p.epi.C, ((long)m * p.epi.ldc + n) * (long)sizeof(T), v);
+          else *(uint4*)((T*)p.epi.C + (long)m * p.epi.ldc + n) = v;
+        } else {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          for (int e = 0; e < 8 && n + e < p.N; ++e)
+            ((T*)p.epi.C)[(long)m * p.epi.ldc + n + e] = (T)((w[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+        }
+      }
+      return;
+    }
   }
   constexpr int WPP = TL::WM / TL::EP;   // wave rows per pass
 #pragma unroll
@@ -1511,6 +1691,26 @@ void launch_epi(const GemmParams& p, const ALArgs& args, hipStream_t st) {
   if constexpr (ALoad::kConv) {
     cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad>), grid, block, 0, st, p, al);
     return;
+  }
+  if constexpr (sizeof(T) == 2) {
+    // the swapped-operand epilogues (SwapCfg); CFM_GEMM_SWAP=0 keeps the unswapped kernels (A/B)
+    const bool resid_ok = TL::EP == 1 && !p.epi.out_scalar;
+    if (g_gemm_swap && p.epi.utt_tp <= 0) {
+      switch (p.epi.mode) {
+        case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_RELU: cfm_launch((gemm_kernel<T, EPI_RELU, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_SWISH: cfm_launch((gemm_kernel<T, EPI_SWISH, TL, ALoad, true>), grid, block, 0, st, p, al); return;
+        case EPI_RESID:
+          if constexpr (TL::EP == 1) {
+            if (resid_ok) {
+              cfm_launch((gemm_kernel<T, EPI_RESID, TL, ALoad, true>), grid, block, 0, st, p, al);
+              return;
+            }
+          }
+          break;
+        default: break;
+      }
+    }
   }
   switch (p.epi.mode) {
     case EPI_STORE: cfm_launch((gemm_kernel<T, EPI_STORE, TL, ALoad>), grid, block, 0, st, p, al); break;
