@@ -22,12 +22,6 @@ struct LayerW {
   long qkv_wf = -1, qkv_lc = -1, qkv_ld = -1;
   long pw1_wf = -1, pw1_lc = -1, pw1_ld = -1;
   long ff2_w1f = -1, ff2_lc = -1, ff2_ld = -1;
-  // norm_out fold (cfm_encoder::ln_fold2, layers l >= 1): the previous layer's norm_out and this layer's
-  // norm_feed_forward1 both folded into linear1: W'' = W diag(g_out g_ff1), column terms c1 (of the
-  // packed W''), c2 = sum_k g_ff1 W, c3 = sum_k b_out g_ff1 W, c4 = sum_k b_ff1 W + bias, and the
-  // previous norm_out's constants (per 128-column granule: sum g, sum g^2, sum g b, 0; then mean b,
-  // sum (b - mean b)^2) - GemmEpi::ln2_k
-  long ff1_w1d = -1, ff1_c1 = -1, ff1_c2 = -1, ff1_c3 = -1, ff1_c4 = -1, prev_out_k = -1;
 };
 
 }  // namespace cfm
@@ -65,11 +59,6 @@ struct cfm_encoder {
   // one launch (gemm_glu_dw); CFM_GLU_DW=0 keeps the two launches (A/B)
   bool fuse_glu_dw = true;
   bool fuse_conv12 = true;     // conv.0 on the matrix cores inside conv.2's implicit GEMM (CFM_CONV12=0: two kernels)
-  // with ln_fold: each layer's norm_out is not materialised - the last residual GEMM of layer l writes
-  // y and the sums of GemmEpi::ln2_out, layer l+1's linear1 folds norm_out and norm_feed_forward1
-  // together and its linear2 reads the residual through norm_out (CFM_LN_FOLD2=0: one LayerNorm
-  // launch per layer as before)
-  bool ln_fold2 = false;
   // bf16 eval forward with the LayerNorm fold, dkp = 64, T' <= 256: each head's q | k | v projection
   // and its attention in one launch (qkv_rel_attention_fused); CFM_QKV_ATTN=0 keeps the QKV GEMM +
   // attention pair (A/B)

@@ -130,26 +130,6 @@ struct GemmEpi {
   int ln_width;
   const float* ln_c;   // [Npad] sum_k W'[n][k] (of the packed, rounded W')
   const float* ln_d;   // [Npad] sum_k beta[k] W[n][k] + bias[n]
-  // Two stacked LayerNorms folded into one GEMM (norm_out of layer l, then norm_feed_forward1 of
-  // layer l+1; DESIGN.md §4 "norm_out fold").  Producer (EPI_RESID with ln_out): with ln2_g / ln2_b
-  // (the first LayerNorm's gamma / beta) also writes per row and granule g, around the granule mean
-  // m_g, (sum (y-m_g) g, sum (y-m_g)^2 g^2, sum (y-m_g) g^2, sum (y-m_g) g b) to ln2_out.
-  // Consumer (EPI_SWISH with ln_in = the producer's (mean, M2) partials): ln2_in = those sums,
-  // ln2_k = the first LayerNorm's constants [granule g: (sum g, sum g^2, sum g b, 0)] then
-  // (mean b, sum (b - mean b)^2); W'' = W diag(g1 g2) and out = r2 (r1 (acc - m1 ln_c) + ln_c3 -
-  // m2 ln_c2) + ln_d, (m1, r1) / (m2, r2) the row statistics of the two LayerNorms' inputs.
-  const float4* ln2_in;
-  float4* ln2_out;
-  const float* ln2_g;
-  const float* ln2_b;
-  const float* ln2_k;
-  const float* ln_c2;  // [Npad] sum_k g2[k] W[n][k]
-  const float* ln_c3;  // [Npad] sum_k b1[k] g2[k] W[n][k]
-  // EPI_RESID residual read through a LayerNorm (the un-materialised norm_out): x = (y - m) r g + b
-  // with (m, r) from the row's granule partials xln_in (ln_parts per row, ln_width columns).
-  const float2* xln_in;
-  const float* xln_g;
-  const float* xln_b;
   // Utterance-aligned rows (EPI_GLU_DW): GEMM row m is frame t = m % 256 of utterance b = m / 256,
   // A / output row b * utt_tp + t (t < utt_tp; utt_M real rows); 0 = rows are plain.
   int utt_tp, utt_M;

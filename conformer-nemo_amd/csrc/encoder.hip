@@ -141,64 +141,6 @@ struct Packer {
     d_off = f32(nullptr, Npad, [&](long i) { return dd[i]; });
     return o;
   }
-  // Two stacked LayerNorms (g1, b1) then (g2, b2) folded into one GEMM (GemmEpi::ln2_in):
-  // W'' = val * diag(g1 g2) packed as mat(); c1[n] = sum_k W''[n][k] (packed, rounded),
-  // c2[n] = sum_k g2[k] val, c3[n] = sum_k b1[k] g2[k] val, c4[n] = sum_k b2[k] val + bias(n)
-  long mat_fold2(int N, int K, std::function<float(int, int)> val, const float* g1, const float* b1, const float* g2,
-                 const float* b2, std::function<float(int)> bias, long& c1_off, long& c2_off, long& c3_off,
-                 long& c4_off) {
-    const long o = mat(N, K, [&](int n, int k) { return val(n, k) * (g1[k] * g2[k]); });
-    const long Npad = round_up(N, GEMM_BN);
-    std::vector<float> c1(Npad, 0.0f), c2(Npad, 0.0f), c3(Npad, 0.0f), c4(Npad, 0.0f);
-    if (!dry) {
-      for (int n = 0; n < N; ++n) {
-        double s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0;
-        for (int k = 0; k < K; ++k) {
-          const float v = val(n, k);
-          const float wq = v * (g1[k] * g2[k]);
-          s1 += (h->es == 4) ? (double)wq : (double)host_bf2f(host_f2bf(wq));
-          s2 += (double)g2[k] * v;
-          s3 += (double)b1[k] * (double)g2[k] * v;
-          s4 += (double)b2[k] * v;
-        }
-        c1[n] = (float)s1;
-        c2[n] = (float)s2;
-        c3[n] = (float)s3;
-        c4[n] = (float)(s4 + (double)bias(n));
-      }
-    }
-    c1_off = f32(nullptr, Npad, [&](long i) { return c1[i]; });
-    c2_off = f32(nullptr, Npad, [&](long i) { return c2[i]; });
-    c3_off = f32(nullptr, Npad, [&](long i) { return c3[i]; });
-    c4_off = f32(nullptr, Npad, [&](long i) { return c4[i]; });
-    return o;
-  }
-  // a LayerNorm's constants for GemmEpi::ln2_k over d columns in 128-column granules
-  long ln_consts(int d, const float* g, const float* b) {
-    const int np = (d + LN_GRANULE - 1) / LN_GRANULE;
-    std::vector<float> k(4L * np + 4, 0.0f);
-    if (!dry) {
-      double bs = 0.0;
-      for (int j = 0; j < d; ++j) bs += b[j];
-      const double bm = bs / d;
-      double bv = 0.0;
-      for (int j = 0; j < d; ++j) bv += ((double)b[j] - bm) * ((double)b[j] - bm);
-      for (int gi = 0; gi < np; ++gi) {
-        double sg = 0.0, sg2 = 0.0, sgb = 0.0;
-        for (int j = gi * LN_GRANULE; j < std::min(d, (gi + 1) * LN_GRANULE); ++j) {
-          sg += g[j];
-          sg2 += (double)g[j] * g[j];
-          sgb += (double)g[j] * b[j];
-        }
-        k[4 * gi] = (float)sg;
-        k[4 * gi + 1] = (float)sg2;
-        k[4 * gi + 2] = (float)sgb;
-      }
-      k[4 * np] = (float)bm;
-      k[4 * np + 1] = (float)bv;
-    }
-    return f32(nullptr, (long)k.size(), [&](long i) { return k[i]; });
-  }
   // packed [Npad][Kpad] compute-type matrix; val(n, k) for n < N, k < K (others zero)
   long mat(int N, int K, std::function<float(int, int)> val) {
     const long Npad = round_up(N, GEMM_BN), Kp = h->kpad(K);
@@ -267,18 +209,6 @@ void pack_all(cfm_encoder* h, Packer& pk, const std::map<std::string, const floa
     const float* b_conv = get(p + "norm_conv.bias");
     const float* g_ff2 = get(p + "norm_feed_forward2.weight");
     const float* b_ff2 = get(p + "norm_feed_forward2.bias");
-    if (h->ln_fold2 && l > 0) {
-      const std::string pp = "layers." + std::to_string(l - 1) + ".";
-      const float* go = get(pp + "norm_out.weight");
-      const float* bo = get(pp + "norm_out.bias");
-      const float* gf = get(p + "norm_feed_forward1.weight");
-      const float* bf = get(p + "norm_feed_forward1.bias");
-      const float* w11 = get(p + "feed_forward1.linear1.weight");
-      const float* b11 = get(p + "feed_forward1.linear1.bias");
-      Lw.ff1_w1d = pk.mat_fold2(dff, d, [=](int n, int k) { return w11[(long)n * d + k]; }, go, bo, gf, bf,
-                                [=](int n) { return b11[n]; }, Lw.ff1_c1, Lw.ff1_c2, Lw.ff1_c3, Lw.ff1_c4);
-      Lw.prev_out_k = pk.ln_consts(d, go, bo);
-    }
     if (h->ln_fold) {
       const float* w21 = get(p + "feed_forward2.linear1.weight");
       const float* b21 = get(p + "feed_forward2.linear1.bias");
@@ -428,7 +358,7 @@ void ensure_streams(cfm_encoder* h, int n) {
 // workspace layout
 // ---------------------------------------------------------------------------------------------
 struct WsLayout {
-  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, LS, LS2, LS4, PE, LEN, total;
+  long X1, X2, X, Hn, U, QK, Vt, O, G, S, P, PN, Y, LS, PE, LEN, total;
   int T1, T2, Tp, M, Tpad;
 };
 
@@ -462,10 +392,6 @@ WsLayout ws_layout_core(const cfm_encoder* h, int B, int T1, int T2, bool front)
   w.PN = h->cfg.conv_norm_type == 1 ? take(M * h->d * 4) : -1;
   w.Y = h->has_out_proj ? take(M * h->dout * 4) : -1;
   w.LS = h->ln_fold ? take(M * ((h->d + LN_GRANULE - 1) / LN_GRANULE) * 8) : -1;   // folded-LayerNorm row partials
-  // norm_out fold: the un-normalised layer output's (mean, M2) partials and ln2 sums (kept apart from LS:
-  // the next layer's linear2 reads them while writing LS)
-  w.LS2 = h->ln_fold2 ? take(M * ((h->d + LN_GRANULE - 1) / LN_GRANULE) * 8) : -1;
-  w.LS4 = h->ln_fold2 ? take(M * ((h->d + LN_GRANULE - 1) / LN_GRANULE) * 16) : -1;
   w.PE = front ? -1 : take((long)(2 * w.Tp - 1) * h->d * es);
   w.LEN = front ? -1 : take((long)B * 4);
   w.total = round_up(off, 256);
@@ -556,10 +482,6 @@ cfm_status cfm_encoder_create(const cfm_encoder_cfg* cfg, int device, int comput
     if (const char* mb = getenv("CFM_MICROBATCH")) h->microbatches = std::max(1, std::min(8, atoi(mb)));
     h->ln_fold = h->dtype == DT_BF16 && h->d % 4 == 0;
     if (const char* lf = getenv("CFM_LN_FOLD")) h->ln_fold = atoi(lf) != 0 && h->d % 4 == 0;
-    // norm_out fold: off by default until its micro-batch (multi-stream) determinism is understood
-    // (tests/test_gpu_encoder.py::test_batch_invariance_full_size); CFM_LN_FOLD2=1 turns it on
-    h->ln_fold2 = false;
-    if (const char* lf = getenv("CFM_LN_FOLD2")) h->ln_fold2 = h->ln_fold && atoi(lf) != 0;
     if (const char* gd = getenv("CFM_GLU_DW")) h->fuse_glu_dw = atoi(gd) != 0;
     if (const char* cc = getenv("CFM_CONV12")) h->fuse_conv12 = atoi(cc) != 0;
     if (const char* qa = getenv("CFM_QKV_ATTN")) h->fuse_qkv_attn = atoi(qa) != 0;
@@ -747,7 +669,10 @@ void pos_gemm(cfm_encoder* h, int Tp, void* dst, hipStream_t st, const void* pe_
 // compute-type copy when an out_proj follows).
 void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const int32_t* lens, const char* Pbuf,
                      hipStream_t st, StageTimer* tm) {
-    const int dt = h->dtype, d = h->d, H = h->H, dkp = h->dkp, Tp = wl.Tp, M = wl.M, L = h->L;
+    // CFM_DBG_LAYERS=n (debugging only): run the first n layers (the last of them ends in its norm_out)
+    static const int dbg_layers = [] { const char* e = getenv("CFM_DBG_LAYERS"); return e ? atoi(e) : 0; }();
+    const int dt = h->dtype, d = h->d, H = h->H, dkp = h->dkp, Tp = wl.Tp, M = wl.M,
+              L = dbg_layers > 0 ? std::min(h->L, dbg_layers) : h->L;
     const int es = h->es;
     auto W = [&](long off) { return (const void*)(h->wbuf + off); };
     auto Wf = [&](long off) { return (const float*)(h->wbuf + off); };
@@ -766,10 +691,6 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
       if (!fold) return;
       e.bias = nullptr; e.ln_in = lns; e.ln_parts = lnp; e.ln_width = d; e.ln_c = Wf(lc); e.ln_d = Wf(ld);
     };
-    // norm_out fold: layer l's norm_out is applied by layer l+1's FFN1 GEMMs (GemmEpi::ln2_in / xln_in)
-    const bool fold2 = fold && h->ln_fold2;
-    float2* lns2 = fold2 ? (float2*)(ws + wl.LS2) : nullptr;
-    float4* ln4 = fold2 ? (float4*)(ws + wl.LS4) : nullptr;
     const long ldp = (long)L * H * dkp;
     if (L > 0) {
       TM(ST_LN);
@@ -778,26 +699,16 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
 
     for (int l = 0; l < L; ++l) {
       const LayerW& Lw = h->layers[l];
-      // X / Hn hold the previous layer's output before its norm_out (y, bf16 copy), LS2 / LS4 its sums
-      const bool in2 = fold2 && l > 0;
       // ---- FFN1 (conformer_modules.py:99-101) ----
       {
         TM(ST_FFN_UP);
-        GemmEpi e = epi_of(EPI_SWISH, in2 ? nullptr : Wf(Lw.ff1_b1));
+        GemmEpi e = epi_of(EPI_SWISH, Wf(Lw.ff1_b1));
         e.C = ws + wl.U; e.ldc = h->dff;
-        if (in2) {
-          e.ln_in = lns2; e.ln_parts = lnp; e.ln_width = d; e.ln_c = Wf(Lw.ff1_c1); e.ln_d = Wf(Lw.ff1_c4);
-          e.ln2_in = ln4; e.ln2_k = Wf(Lw.prev_out_k); e.ln_c2 = Wf(Lw.ff1_c2); e.ln_c3 = Wf(Lw.ff1_c3);
-        }
-        gemm(dt, Hn, d, M, d, W(in2 ? Lw.ff1_w1d : Lw.ff1_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
+        gemm(dt, Hn, d, M, d, W(Lw.ff1_w1), (int)h->kpad(d), h->dff, e, h->zero_page, st);
         TM(ST_FFN_DOWN);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff1_b2), 0.5f);
         r.X = X; r.ldx = d;
         produce(r);
-        if (in2) {
-          const LayerW& Lp = h->layers[l - 1];
-          r.xln_in = lns2; r.xln_g = Wf(Lp.ln_w[4]); r.xln_b = Wf(Lp.ln_b[4]); r.ln_width = d;
-        }
         gemm(dt, ws + wl.U, h->dff, M, h->dff, W(Lw.ff1_w2), (int)h->kpad(h->dff), d, r, h->zero_page, st);
       }
       // ---- rel-pos MHSA (conformer_modules.py:103-110) ----
@@ -900,15 +811,10 @@ void run_layer_stack(cfm_encoder* h, char* ws, const WsLayout& wl, int B, const 
         TM(ST_FFN_DOWN);
         GemmEpi r = epi_of(EPI_RESID, Wf(Lw.ff2_b2), 0.5f);
         r.X = X; r.ldx = d;
-        if (fold2 && l + 1 < L) {
-          r.xb = Hn; r.ln_out = lns2; r.ln_parts = lnp;
-          r.ln2_out = ln4; r.ln2_g = Wf(Lw.ln_w[4]); r.ln2_b = Wf(Lw.ln_b[4]);
-        }
         gemm(dt, ws + wl.U, h->dff, M, h->dff, W(Lw.ff2_w2), (int)h->kpad(h->dff), d, r, h->zero_page, st);
       }
       // ---- norm_out (conformer_modules.py:120), fused with the next layer's first LayerNorm ----
       const bool next = l + 1 < L;
-      if (fold2 && next) continue;   // applied by the next layer's FFN1 GEMMs
       const bool want_t = next || h->has_out_proj;
       TM(ST_LN);
       layernorm(dt, X, M, d, Wf(Lw.ln_w[4]), Wf(Lw.ln_b[4]), X, next ? Wf(h->layers[l + 1].ln_w[0]) : nullptr,

@@ -59,10 +59,7 @@ struct Tile {
   // column (c, d)
   static constexpr int RS_OFF = (NSTAGE * STAGE_BYTES > EPI_BYTES) ? NSTAGE * STAGE_BYTES : EPI_BYTES;
   static constexpr int CD_OFF = RS_OFF + BM * 8;
-  // the norm_out fold's second row table (mean, rstd) and column table (c2, c3) (GemmEpi::ln2_in)
-  static constexpr int RS2_OFF = CD_OFF + BN * 8;
-  static constexpr int C23_OFF = RS2_OFF + BM * 8;
-  static constexpr int LDS_BYTES = C23_OFF + BN * 8;
+  static constexpr int LDS_BYTES = CD_OFF + BN * 8;
   static_assert(GA >= 1 && GB >= 1 && MR >= 1 && NR >= 1, "tile");
   static_assert(BKB == 64 || BKB == 128 || BKB == 256, "stage depth");
   // 256-byte K-steps run only where the host checked p.kb % 256 == 0 (dispatch)
@@ -272,11 +269,6 @@ CFM_DEV int real_row(const GemmParams& p, int m, int BM) {
 // Folded LayerNorm (GemmEpi::ln_in): rs[r] = (mean, rstd) of the pass's local row r, cd[j] = (c, d)
 // of the tile's local column j.
 CFM_DEV float ln_fold(float2 s, float v, float2 cd) { return s.y * (v - s.x * cd.x) + cd.y; }
-// Two stacked LayerNorms (GemmEpi::ln2_in): s / s2 = (mean, rstd) of the first / second one's input,
-// cd = (c1, c4), c23 = (c2, c3) of the column
-CFM_DEV float ln_fold2(float2 s, float2 s2, float v, float2 cd, float2 c23) {
-  return s2.y * (s.y * (v - s.x * cd.x) + c23.y - s2.x * c23.x) + cd.y;
-}
 
 // Sum over the 32 lanes of a half-wave, the same value in every lane: DPP quad permutes and row
 // mirrors (VALU) for 16 lanes, one xor-16 shuffle.
@@ -294,13 +286,12 @@ CFM_DEV float halfwave_sum(float v) {
 
 // FOLD: the LayerNorm fold is active for this launch (GemmEpi::ln_in set: consumer; ln_out / xb
 // set: EPI_RESID producer) - a compile-time flag, so no per-element branches in the unrolled loops.
-template <typename T, int EPI, class TL, bool FOLD, bool FOLD2 = false>
+template <typename T, int EPI, class TL, bool FOLD>
 CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, long xoff, const float2* rs,
-                      const float2* cd, const float2* rs2 = nullptr, const float2* c23 = nullptr) {
+                      const float2* cd) {
   const GemmEpi& e = p.epi;
   const int tid = threadIdx.x;
   constexpr bool fold = FOLD;
-  static_assert(!FOLD2 || FOLD, "the norm_out fold is a LayerNorm fold");
   if constexpr (EPI == EPI_RESID || EPI == EPI_SCALE_F32) {
     // fp32 output (N % 4 == 0), 4 columns per thread-chunk
     constexpr int CPR = TL::BN / 4;                 // chunks per row
@@ -355,19 +346,6 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
       for (int q = 0; q < NP; ++q) {
         const int m = min(m0 + r0 + q * RPP, p.M - 1);
         xv[q] = *(const float4*)(XI + xoff + (long)m * e.ldx + nc);
-      }
-      if constexpr (FOLD) {
-        if (e.xln_g) {   // the residual is norm_out(y): y read, normalised here (rs = y's row statistics)
-          const float4 gg = *(const float4*)(e.xln_g + nc), bb = *(const float4*)(e.xln_b + nc);
-#pragma unroll
-          for (int q = 0; q < NP; ++q) {
-            const float2 st = rs[r0 + q * RPP];
-            xv[q].x = (xv[q].x - st.x) * st.y * gg.x + bb.x;
-            xv[q].y = (xv[q].y - st.x) * st.y * gg.y + bb.y;
-            xv[q].z = (xv[q].z - st.x) * st.y * gg.z + bb.z;
-            xv[q].w = (xv[q].w - st.x) * st.y * gg.w + bb.w;
-          }
-        }
       }
     }
 #pragma unroll
@@ -428,16 +406,6 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
           const float a0 = o.x - mean, a1 = o.y - mean, a2 = o.z - mean, a3 = o.w - mean;
           const float q2 = halfwave_sum(ok ? (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3) : 0.0f);
           if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln_out[(long)m * e.ln_parts + g] = make_float2(mean, q2);
-          if (e.ln2_out) {
-            // the sums the consumer's second LayerNorm statistics are formed from (GemmEpi::ln2_out)
-            const float4 gg = *(const float4*)(e.ln2_g + nc), bb = *(const float4*)(e.ln2_b + nc);
-            const float u0 = a0 * gg.x, u1 = a1 * gg.y, u2 = a2 * gg.z, u3 = a3 * gg.w;
-            const float sa = halfwave_sum(ok ? (u0 + u1) + (u2 + u3) : 0.0f);
-            const float sb = halfwave_sum(ok ? (u0 * u0 + u1 * u1) + (u2 * u2 + u3 * u3) : 0.0f);
-            const float sc = halfwave_sum(ok ? (u0 * gg.x + u1 * gg.y) + (u2 * gg.z + u3 * gg.w) : 0.0f);
-            const float sd = halfwave_sum(ok ? (u0 * bb.x + u1 * bb.y) + (u2 * bb.z + u3 * bb.w) : 0.0f);
-            if ((cc & 31) == 0 && m < p.M && cnt > 0) e.ln2_out[(long)m * e.ln_parts + g] = make_float4(sa, sb, sc, sd);
-          }
         }
       }
     }
@@ -581,9 +549,8 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
     for (int q = 0; q < NP; ++q) {
       const int r = r0 + q * RPP;
       const int m = m0 + r;
-      float2 st, st2;
+      float2 st;
       if constexpr (fold) st = rs[r];
-      if constexpr (FOLD2) st2 = rs2[r];
       float zf[VE];
       if constexpr (EPI == EPI_SWISH_BWD) {
         // z row chunk of this output chunk (host guarantees N % VE == 0); rows past M read row M-1
@@ -594,8 +561,7 @@ CFM_DEV void epilogue(const GemmParams& p, const float* img, int m0, int n0, lon
 #pragma unroll
       for (int i = 0; i < VE; ++i) {
         float v = img[r * TL::EPS + cc * VE + i];
-        if constexpr (FOLD2) v = ln_fold2(st, st2, v, cd[cc * VE + i], c23[cc * VE + i]);
-        else if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
+        if constexpr (fold) v = ln_fold(st, v, cd[cc * VE + i]);
         if constexpr (EPI == EPI_RELU) v = fmaxf(v, 0.0f);
         if constexpr (EPI == EPI_SWISH) v = swishf(v);
         if constexpr (EPI == EPI_SWISH_BWD) {
@@ -722,67 +688,6 @@ CFM_DEV void pack_chunks16(const float* v, uint4& c0, uint4& c1) {
   c1 = make_uint4(s2[0], s3[0], s2[1], s3[1]);
 }
 
-// norm_out fold tables (GemmEpi::ln2_in): row tid's (mean, rstd) of y (the first LayerNorm's input,
-// from its (mean, M2) granule partials, prefetched in ln_pre) and of w = LN1(y) (the second one's
-// input), formed from the producer's granule sums around m_g and LN1's constants:
-//   S_A = sum_k (y_k - m1) g_k        = sum_g A_g + (m_g - m1) G_g
-//   m2  = mean(b) + r1 S_A / W
-//   S_B = sum_k (y_k - m1)^2 g_k^2    = sum_g B_g + 2 (m_g - m1) C_g + (m_g - m1)^2 G2_g
-//   S_D = sum_k (y_k - m1) g_k b_k    = sum_g D_g + (m_g - m1) GB_g
-//   W var2 = r1^2 S_B + 2 r1 (S_D - m2 S_A) + sum (b - mean b)^2 + W (mean b - m2)^2
-// and column tid's (c1, c4) / (c2, c3).
-template <class P>
-CFM_DEV void ln2_tables(const P& p, int m0, int n0, int BM, int BN, const float2 (&ln_pre)[LN_PRE], float2 cd_pre,
-                        float2* rs_tab, float2* cd_tab, float2* rs2_tab, float2* c23_tab) {
-  const int tid = threadIdx.x;
-  const GemmEpi& e = p.epi;
-  const int W = e.ln_width, np = e.ln_parts;
-  if (tid < BM) {
-    const long row = real_row(p, m0 + tid, BM);
-    const float2* pp = e.ln_in + row * np;
-    const float4* qq = e.ln2_in + row * np;
-    auto cnt = [&](int g) { return (float)min(LN_GRANULE, W - g * LN_GRANULE); };
-    float sm = 0.0f;
-#pragma unroll
-    for (int g = 0; g < LN_PRE; ++g) sm += g < np ? cnt(g) * ln_pre[g].x : 0.0f;
-    for (int g = LN_PRE; g < np; ++g) sm += cnt(g) * pp[g].x;
-    const float m1 = sm / (float)W;
-    // the first LN_PRE granules' sums and constants load unconditionally (clamped granule; a load under
-    // a per-granule branch would be issued and waited for one at a time)
-    float4 s4p[LN_PRE], k4p[LN_PRE];
-#pragma unroll
-    for (int g = 0; g < LN_PRE; ++g) {
-      const int gc = min(g, np - 1);
-      s4p[g] = qq[gc];
-      k4p[g] = *(const float4*)(e.ln2_k + 4 * gc);   // (sum g, sum g^2, sum g b, 0) of granule gc
-    }
-    float q1 = 0.0f, sa = 0.0f, sb = 0.0f, sd = 0.0f;
-    auto add = [&](int g, float2 pg, float4 s4, float4 k4) {
-      const float dm = pg.x - m1;
-      q1 += pg.y + cnt(g) * dm * dm;
-      sa += s4.x + dm * k4.x;
-      sb += s4.y + 2.0f * dm * s4.z + dm * dm * k4.y;
-      sd += s4.w + dm * k4.z;
-    };
-#pragma unroll
-    for (int g = 0; g < LN_PRE; ++g)
-      if (g < np) add(g, ln_pre[g], s4p[g], k4p[g]);
-    for (int g = LN_PRE; g < np; ++g) add(g, pp[g], qq[g], *(const float4*)(e.ln2_k + 4 * g));
-    const float r1 = 1.0f / sqrtf(q1 / (float)W + 1e-5f);
-    const float bmean = e.ln2_k[4 * np], bvar = e.ln2_k[4 * np + 1];
-    const float m2 = bmean + r1 * sa / (float)W;
-    const float db = bmean - m2;
-    const float q2 = r1 * r1 * sb + 2.0f * r1 * (sd - m2 * sa) + bvar + (float)W * db * db;
-    rs_tab[tid] = make_float2(m1, r1);
-    rs2_tab[tid] = make_float2(m2, 1.0f / sqrtf(fmaxf(q2, 0.0f) / (float)W + 1e-5f));
-  }
-  if (tid < BN) {
-    const int nc = n0 + tid;
-    cd_tab[tid] = cd_pre;
-    c23_tab[tid] = make_float2(e.ln_c2[nc], e.ln_c3[nc]);
-  }
-}
-
 // SW (bf16 dense STORE / RELU / SWISH / RESID): the MFMA operands are swapped (weight rows as the A
 // operand), so each lane's accumulator groups hold 4 consecutive output COLUMNS of one row.  The epilogue
 // then works from registers: RESID writes its fp32 image as float4 runs (swizzled, EpiView SWZ), the
@@ -842,19 +747,16 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 
   // folded LayerNorm operands, loaded now and consumed by the epilogue (the loads complete during
   // the main loop): row tid's first LN_PRE granule partials, column tid's (c, d)
-  // (the residual's partials instead for EPI_RESID's LayerNorm-on-read, GemmEpi::xln_in)
   float2 ln_pre[LN_PRE];
   float2 cd_pre = make_float2(0.0f, 0.0f);
-  const float2* ln_src = p.epi.ln_in ? p.epi.ln_in : p.epi.xln_in;
+  const float2* ln_src = p.epi.ln_in;
   if (ln_src) {
     const int np = p.epi.ln_parts;
     const float2* pp = ln_src + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
 #pragma unroll
     for (int g = 0; g < LN_PRE; ++g) ln_pre[g] = pp[min(g, np - 1)];
-    if (p.epi.ln_in) {
-      const int nc = n0 + min(tid, TL::BN - 1);
-      cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
-    }
+    const int nc = n0 + min(tid, TL::BN - 1);
+    cd_pre = make_float2(p.epi.ln_c[nc], p.epi.ln_d[nc]);
   }
 
   auto stage = [&](int kt, int slot) {
@@ -897,13 +799,6 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
     if (s < npro && s < nk) stage(s, s);
   float2* rs_tab = (float2*)(smem + TL::RS_OFF);
   float2* cd_tab = (float2*)(smem + TL::CD_OFF);
-  float2* rs2_tab = (float2*)(smem + TL::RS2_OFF);
-  float2* c23_tab = (float2*)(smem + TL::C23_OFF);
-  if constexpr (EPI == EPI_SWISH) {
-    // norm_out fold: both LayerNorms' row statistics, computed while the first stages land (the
-    // tables sit behind the ring and the epilogue image; read after the epilogue's first barrier)
-    if (p.epi.ln2_in) ln2_tables(p, m0, n0, TL::BM, TL::BN, ln_pre, cd_pre, rs_tab, cd_tab, rs2_tab, c23_tab);
-  }
   if constexpr (kAheadTile) {
     if (ahead) {
       // Read-ahead loop: K-step kt's fragments (all substeps) are in registers when kt starts, and
@@ -1105,7 +1000,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
   // folded LayerNorm: (mean, rstd) of row tid from its granule partials (Chan et al.'s pairwise
   // combination of (count, mean, M2)) and (c, d) of column tid, from the values prefetched at the
   // kernel start; visible after the first pass's barrier
-  if (ln_src && !p.epi.ln2_in) {
+  if (ln_src) {
     const int W = p.epi.ln_width, np = p.epi.ln_parts;
     const float2* pp = ln_src + (long)real_row(p, m0 + min(tid, TL::BM - 1), TL::BM) * np;
     float sm = 0.0f;
@@ -1126,7 +1021,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
       m2 += pg.y + (float)min(LN_GRANULE, W - g * LN_GRANULE) * dm * dm;
     }
     if (tid < TL::BM) rs_tab[tid] = make_float2(mean, 1.0f / sqrtf(m2 / (float)W + 1e-5f));
-    if (tid < TL::BN && p.epi.ln_in) cd_tab[tid] = cd_pre;
+    if (tid < TL::BN) cd_tab[tid] = cd_pre;
   }
   if constexpr (SW) {
     // this lane's 4-column bias runs (zero-padded arrays: every read in range)
@@ -1165,13 +1060,12 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
       char* im = smem;
       __syncthreads();                   // the tables are visible; every wave is done with the image above
       if (kg == 0) {
-        const bool fold = p.epi.ln_in != nullptr, fold2 = p.epi.ln2_in != nullptr;
+        const bool fold = p.epi.ln_in != nullptr;
 #pragma unroll
         for (int i = 0; i < TL::MR; ++i) {
           const int r = wm * (TL::BM / TL::WM) + i * 32 + col;
-          float2 st = make_float2(0.f, 0.f), st2 = make_float2(0.f, 0.f);
+          float2 st = make_float2(0.f, 0.f);
           if (fold) st = rs_tab[r];
-          if (fold2) st2 = rs2_tab[r];
 #pragma unroll
           for (int j = 0; j < TL::NR; ++j)
 #pragma unroll
@@ -1182,8 +1076,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 float a = acc[i][j][4 * q4 + e];
-                if (fold2) a = ln_fold2(st, st2, a, cd_tab[c + e], c23_tab[c + e]);
-                else if (fold) a = ln_fold(st, a, cd_tab[c + e]);
+                if (fold) a = ln_fold(st, a, cd_tab[c + e]);
                 else a += bb[e];
                 if constexpr (EPI == EPI_RELU) a = fmaxf(a, 0.0f);
                 if constexpr (EPI == EPI_SWISH) a = swishf(a);
@@ -1233,17 +1126,7 @@ __global__ __launch_bounds__(TL::NT) void gemm_kernel(GemmParams p, ALoad aload)
         }
     }
     __syncthreads();
-    bool done = false;
-    if constexpr (EPI == EPI_SWISH) {
-      if (p.epi.ln2_in) {
-        epilogue<T, EPI, EpiView<TL>, true, true>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
-                                                  rs_tab + pass * EpiView<TL>::BM, cd_tab,
-                                                  rs2_tab + pass * EpiView<TL>::BM, c23_tab);
-        done = true;
-      }
-    }
-    if (done) {
-    } else if (p.epi.ln_in || p.epi.ln_out)
+    if (p.epi.ln_in || p.epi.ln_out)
       epilogue<T, EPI, EpiView<TL>, true>(p, img, m0 + pass * EpiView<TL>::BM, n0, (long)blockIdx.y * p.split_x,
                                           rs_tab + pass * EpiView<TL>::BM, cd_tab);
     else
@@ -1893,9 +1776,6 @@ int set_gemm_tile_override(int tile) {
 void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int Kpad, int N, const GemmEpi& epi,
           const void* zero_page, hipStream_t st) {
   if (M <= 0) return;
-  if ((epi.xln_in && (epi.mode != EPI_RESID || !epi.ln_out)) || (epi.ln2_in && (epi.mode != EPI_SWISH || !epi.ln_in)) ||
-      (epi.ln2_out && (epi.mode != EPI_RESID || !epi.ln_out)))
-    fail(CFM_ERR_INVALID_ARG, "gemm: norm_out fold operands on the wrong epilogue");
   const int es = dtype_size(dtype);
   GemmParams p = make_params(es, M, Wp, Kpad, N, epi);
   DenseArgs a{(const char*)A, lda * es, M, (long)K * es, (const char*)zero_page};

@@ -272,21 +272,29 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
     if (s + D < nsteps) issue(s + D);
     const char* ia = smem + (s % NST) * STG + ai * (TK * 256);
     const char* ib = smem + (s % NST) * STG + (MI + bi) * (TK * 256);
+    // every substep's fragments are read up front (two register sets; the barrier above orders them),
+    // so the second substep's reads land while the first substep's MFMAs run: read, wait, multiply per
+    // substep left each wave's MFMAs waiting on its own transposing reads
+    constexpr int NKS = TK / 16;
+    uint4 fa[NKS][2], fb[NKS][2];
 #pragma unroll
-    for (int ks = 0; ks < TK; ks += 16) {
-      uint4 fa[2], fb[2];
+    for (int q = 0; q < NKS; ++q) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(ia, acol + i * 32, ks, lane);
+      for (int i = 0; i < 2; ++i) fa[q][i] = tr_frag(ia, acol + i * 32, 16 * q, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = tr_frag(ib, bcol + j * 32, ks, lane);
+      for (int j = 0; j < 2; ++j) fb[q][j] = tr_frag(ib, bcol + j * 32, 16 * q, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < NKS; ++q) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[i], fb[j]);
+        for (int j = 0; j < 2; ++j) mfma_slab<bf16_t>(acc[i][j], fa[q][i], fb[q][j]);
       if (bias) {   // lane l holds 8 frame rows of column (l & 31) of fragment i
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const uint32_t u[4] = {fa[i].x, fa[i].y, fa[i].z, fa[i].w};
+          const uint32_t u[4] = {fa[q][i].x, fa[q][i].y, fa[q][i].z, fa[q][i].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             bsum[i] += bf2f((bf16_t)(u[e] & 0xffffu)) + bf2f((bf16_t)(u[e] >> 16));

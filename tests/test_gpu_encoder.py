@@ -124,6 +124,18 @@ def test_batch_invariance_full_size(compute):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(y3.cpu().numpy(), y)
         np.testing.assert_array_equal(yl3.cpu().numpy(), yl)
+    # beside small elementwise kernels on another stream that share CUs with the forward's blocks (the
+    # case that showed the round-4 norm_out fold's drift): still bitwise equal
+    enc.set_microbatches(1)
+    side = torch.cuda.Stream()
+    junk = torch.randn(16 << 20, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        for _ in range(100):
+            junk.mul_(1.0001).add_(1e-6)
+    y4, _ = enc.forward(torch.from_numpy(x).cuda(), torch.from_numpy(lens).cuda())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(y4.cpu().numpy(), y)
 
 
 def test_dropin_module_forward():

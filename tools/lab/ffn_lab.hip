@@ -71,7 +71,7 @@ CFM_DEV void waitv_rt(int n) {
 // consecutive output COLUMNS of one row: the epilogue converts in registers and writes 8-byte runs
 // into a swizzled bf16 LDS image, then stores 16-byte row chunks.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, int NS, int EPI>
+template <int BM, int BN, int BK, int NS, int EPI, bool OVL = false>
 struct G4 {
   static constexpr int WM = 2, WN = 2, TWM = BM / WM, TWN = BN / WN, MR = TWM / 32, NR = TWN / 32;
   static constexpr int SLOTS = BK / 16, RPI = 1024 / BK, SWDIV = 16 / SLOTS;
@@ -81,7 +81,7 @@ struct G4 {
   static constexpr int RING = NS * STAGE;
   static constexpr int IMG_BYTES = (EPI == L_RESID) ? BM * BN * 4 : BM * BN * 2;
   // the epilogue image sits behind the ring, or over it (after a barrier) when both do not fit
-  static constexpr bool OVERLAY = RING + IMG_BYTES > 160 * 1024;
+  static constexpr bool OVERLAY = OVL || RING + IMG_BYTES > 160 * 1024;
   static constexpr int IMG_OFF = OVERLAY ? 0 : RING;
   static constexpr int LDS = OVERLAY ? (RING > IMG_BYTES ? RING : IMG_BYTES) : RING + IMG_BYTES;
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -89,9 +89,9 @@ struct G4 {
   static CFM_DEV int swz(int row) { return (row / SWDIV) % SLOTS; }
 };
 
-template <int BM, int BN, int BK, int NS, int EPI>
-__global__ __launch_bounds__(256, 1) void g4_kernel(LP p) {
-  using C = G4<BM, BN, BK, NS, EPI>;
+template <int BM, int BN, int BK, int NS, int EPI, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void g4_kernel(LP p) {
+  using C = G4<BM, BN, BK, NS, EPI, (OCC > 1)>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -133,14 +133,6 @@ __global__ __launch_bounds__(256, 1) void g4_kernel(LP p) {
 
   // epilogue operands, loaded before the loop
   const int h = lane >> 5, l32 = lane & 31;
-  float4 bias4[C::NR][4];
-#pragma unroll
-  for (int j = 0; j < C::NR; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + wn * C::TWN + j * 32 + 8 * g + 4 * h;
-      bias4[j][g] = p.bias ? *(const float4*)(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
 
   f32x16 acc[C::MR][C::NR];
 #pragma unroll
@@ -167,33 +159,42 @@ __global__ __launch_bounds__(256, 1) void g4_kernel(LP p) {
   wait_lgkm0();
   raw_barrier();
   stamp(p, 1);
-  uint4 afc[C::MR], bfc[C::NR];
-  read_frags(0, 0, afc, bfc);
+  uint4 fa[2][C::MR], fb[2][C::NR];
+  read_frags(0, 0, fa[0], fb[0]);
   int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  auto kstep = [&](int kt, auto par0) {
+    constexpr int P0 = decltype(par0)::value;
     if (kt + NS - 1 < nk && !(p.probe & 1)) stage(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
     const int nslot = slot == NS - 1 ? 0 : slot + 1;
 #pragma unroll
     for (int kk = 0; kk < C::KSUB; ++kk) {
-      uint4 afn[C::MR], bfn[C::NR];
-      if (kk + 1 < C::KSUB) {
-        read_frags(slot, kk + 1, afn, bfn);
-      } else if (kt + 1 < nk) {
+      const int cur = (P0 + kk) & 1;
+      const bool last = kk + 1 == C::KSUB, more = kt + 1 < nk;
+      if (!last) {
+        read_frags(slot, kk + 1, fa[cur ^ 1], fb[cur ^ 1]);
+      } else if (more) {
         waitv_rt(C::G * min(NS - 2, nk - 2 - kt));
-        wait_lgkm0();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
         raw_barrier();
-        read_frags(nslot, 0, afn, bfn);
       }
 #pragma unroll
       for (int i = 0; i < C::MR; ++i)
 #pragma unroll
-        for (int j = 0; j < C::NR; ++j) acc[i][j] = mfma16_32x32x16(bfc[j], afc[i], acc[i][j]);
-#pragma unroll
-      for (int i = 0; i < C::MR; ++i) afc[i] = afn[i];
-#pragma unroll
-      for (int j = 0; j < C::NR; ++j) bfc[j] = bfn[j];
+        for (int j = 0; j < C::NR; ++j) acc[i][j] = mfma16_32x32x16(fb[cur][j], fa[cur][i], acc[i][j]);
+      if (last && more) {
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(nslot, 0, fa[cur ^ 1], fb[cur ^ 1]);
+      }
     }
     slot = nslot;
+  };
+  if constexpr (C::KSUB % 2 == 0) {
+    for (int kt = 0; kt < nk; ++kt) kstep(kt, std::integral_constant<int, 0>{});
+  } else {
+    for (int kt = 0; kt < nk; kt += 2) {
+      kstep(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < nk) kstep(kt + 1, std::integral_constant<int, 1>{});
+    }
   }
 
   stamp(p, 2);
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256, 1) void g4_kernel(LP p) {
         for (int g = 0; g < 4; ++g) {
           const int ml = wm * C::TWM + i * 32 + l32;
           const int nl = wn * C::TWN + j * 32 + 8 * g + 4 * h;
-          const float4 b = bias4[j][g];
+          const float4 b = p.bias ? *(const float4*)(p.bias + n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
           float4 v = make_float4(acc[i][j][4 * g] + b.x, acc[i][j][4 * g + 1] + b.y, acc[i][j][4 * g + 2] + b.z,
                                  acc[i][j][4 * g + 3] + b.w);
           *(float4*)(img + ml * RB + (((nl >> 2) ^ (ml & 7)) << 4)) = v;
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(256, 1) void g4_kernel(LP p) {
         for (int g = 0; g < 4; ++g) {
           const int ml = wm * C::TWM + i * 32 + l32;
           const int nl = wn * C::TWN + j * 32 + 8 * g + 4 * h;
-          const float4 b = bias4[j][g];
+          const float4 b = p.bias ? *(const float4*)(p.bias + n0 + nl) : make_float4(0.f, 0.f, 0.f, 0.f);
           float v0 = acc[i][j][4 * g] + b.x, v1 = acc[i][j][4 * g + 1] + b.y;
           float v2 = acc[i][j][4 * g + 2] + b.z, v3 = acc[i][j][4 * g + 3] + b.w;
           if constexpr (EPI == L_SWISH) { v0 = swishf(v0); v1 = swishf(v1); v2 = swishf(v2); v3 = swishf(v3); }
@@ -318,12 +319,12 @@ struct Variant {
   int bm, bn;
 };
 
-template <int BM, int BN, int BK, int NS, int EPI>
+template <int BM, int BN, int BK, int NS, int EPI, int OCC = 1>
 void launch_g4(const LP& p0, hipStream_t st) {
   LP p = p0;
   p.Mtiles = (p.M + BM - 1) / BM;
   p.Ntiles = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((g4_kernel<BM, BN, BK, NS, EPI>), dim3(p.Mtiles * p.Ntiles), dim3(256), 0, st, p);
+  hipLaunchKernelGGL((g4_kernel<BM, BN, BK, NS, EPI, OCC>), dim3(p.Mtiles * p.Ntiles), dim3(256), 0, st, p);
 }
 
 typedef int (*bench_fn)(int, int, int, int, int, int, int, float*);
@@ -336,19 +337,19 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs;
   if (!strcmp(shape, "ffn_up")) {
     N = 2048; K = 512; epi = L_SWISH; libtile = 11;
-    vs.push_back({"g4 256x128 bk64 ns4", launch_g4<256, 128, 64, 4, L_SWISH>, 256, 128});
-    vs.push_back({"g4 128x256 bk128 ns2", launch_g4<128, 256, 128, 2, L_SWISH>, 128, 256});
-    vs.push_back({"g4 256x128 bk128 ns2", launch_g4<256, 128, 128, 2, L_SWISH>, 256, 128});
+    vs.push_back({"g4 256x128 bk64 ns3 occ2", launch_g4<256, 128, 64, 3, L_SWISH, 2>, 256, 128});
+    vs.push_back({"g4 256x128 bk64 ns2 occ2", launch_g4<256, 128, 64, 2, L_SWISH, 2>, 256, 128});
+    vs.push_back({"g4 128x256 bk64 ns3 occ2", launch_g4<128, 256, 64, 3, L_SWISH, 2>, 128, 256});
+    vs.push_back({"g4 128x128 bk128 ns2 occ2", launch_g4<128, 128, 128, 2, L_SWISH, 2>, 128, 128});
+    vs.push_back({"g4 256x128 bk64 ns4 occ1", launch_g4<256, 128, 64, 4, L_SWISH, 1>, 256, 128});
   } else if (!strcmp(shape, "ffn_up_store")) {
     N = 2048; K = 512; epi = L_STORE; libtile = 11;
     vs.push_back({"g4 256x128 bk64 ns4", launch_g4<256, 128, 64, 4, L_STORE>, 256, 128});
 
   } else if (!strcmp(shape, "ffn_down")) {
     N = 512; K = 2048; epi = L_RESID; libtile = 14;
-    vs.push_back({"g4 128x128 bk64 ns4", launch_g4<128, 128, 64, 4, L_RESID>, 128, 128});
-    vs.push_back({"g4 128x128 bk128 ns2", launch_g4<128, 128, 128, 2, L_RESID>, 128, 128});
-    vs.push_back({"g4 128x128 bk128 ns4", launch_g4<128, 128, 128, 4, L_RESID>, 128, 128});
-    vs.push_back({"g4 128x128 bk128 ns3", launch_g4<128, 128, 128, 3, L_RESID>, 128, 128});
+    vs.push_back({"g4 128x128 bk128 ns3 occ1", launch_g4<128, 128, 128, 3, L_RESID, 1>, 128, 128});
+    vs.push_back({"g4 64x128 bk128 ns2 occ2", launch_g4<64, 128, 128, 2, L_RESID, 2>, 64, 128});
   } else {
     fprintf(stderr, "unknown shape\n");
     return 1;

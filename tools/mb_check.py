@@ -31,6 +31,17 @@ def main():
         enc.set_microbatches(1)
         enc._workspace(enc.workspace_size(32, 1000)).fill_(255)
     y1, _ = enc.forward(x, ln)
+    if os.environ.get("MB_JUNK2"):   # beside small-LDS elementwise kernels that can share CUs with the forward's blocks
+        side = torch.cuda.Stream()
+        j = torch.randn(64 << 20, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            for _ in range(200):
+                j.mul_(1.0001).add_(1e-6)
+        y1b, _ = enc.forward(x, ln)
+        torch.cuda.synchronize()
+        print(label, f"junk2 {(y1 - y1b).abs().max().item():.3e}", flush=True)
+        return
     if os.environ.get("MB_JUNK"):   # run the single-stream forward again beside unrelated work on another stream
         side = torch.cuda.Stream()
         a = torch.randn(8192, 8192, device="cuda", dtype=torch.bfloat16)
