@@ -255,6 +255,12 @@ int wgrad_tn_tiles(int N, int K, bool ones, int bfn);
 int wgrad_tn_blocks(int bfn);
 void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bool ones, int bfn, Drop bdr, long rows,
               int S, long chunk, float* out, long ldo, int Kout, long split_stride, hipStream_t st);
+// conv.2's weight gradient [dW2 | db2] = dY2^T . [im2col(X1) | 1] with the im2col formed by the loader
+// (wgrad_tn.hip): dy frame-major (rows = B*T2*F2 output pixels) x C, x1 = [B][T1][F1][C]; partial
+// tiles [s][C][ldo] (columns tap * C + c, the bias at column 9C when `ones`) per `chunk` rows
+bool wgrad_tn_conv_supported(int dtype, int C, long lda);
+void wgrad_tn_conv(const void* dy, long lda, const void* x1, int B, int T1, int F1, int T2, int F2, int C, bool ones,
+                   long rows, int S, long chunk, float* out, long ldo, long split_stride, hipStream_t st);
 
 // ---- backward building blocks (backward.hip) ----
 // dst[i][j] = transpose ? src[j][i] : src[i][j] in the compute type for i < rows_pad, j < cols_pad;

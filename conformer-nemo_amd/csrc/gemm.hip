@@ -1162,7 +1162,7 @@ constexpr int G8_BUF = 4 * G8_HALF;     // one K-tile: A0 | B0 | A1 | B1
 static_assert(2 * G8_BUF >= T8::BM / T8::EP * T8::EPS * 4, "epilogue image fits the ring");
 CFM_DEV int g8_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
 
-template <int EPI, class ALoad>
+template <int EPI, class ALoad, bool SPREAD = false>
 __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
   __shared__ __attribute__((aligned(16))) char smem[2 * G8_BUF];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1192,11 +1192,12 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
   const uint32_t sbase = lds_addr(smem);
   const int nk = p.kb / 128;
 
-  auto issue = [&](int kt, int h) {   // K-half h of K-tile kt, A then B: 4 glds
+  auto issue = [&](int kt, int h, int parts = 3) {   // K-half h of K-tile kt, A (parts & 1) then B (parts & 2)
     const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
     const bool live = kt < nk;        // past the end: the zero page (uniform vmcnt counts)
     const int kb0 = kt * 128 + h * 64;
-    if constexpr (ALoad::kConv) {
+    if (!(parts & 1)) {
+    } else if constexpr (ALoad::kConv) {
       const int tapb = (int)aload.tapb;   // bytes of one 3x3 tap (C * 2); a K-half never straddles two
       int tap = 0;                        // wave-uniform: count the tap boundaries below kb0 (no division)
 #pragma unroll
@@ -1214,8 +1215,10 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
       for (int i = 0; i < 2; ++i)
         glds16_asm(live ? aload.src(ast, i, kb0, lo[i]) : (const void*)zsrc, base + (i * 8 + wave) * 1024);
     }
+    if (parts & 2) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
+      for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
+    }
   };
 
   f32x4 acc[8][4];
@@ -1252,8 +1255,18 @@ __global__ __launch_bounds__(512) void gemm8_kernel(GemmParams p, ALoad aload) {
     for (int q = 0; q < 4; ++q) {
       // R_q
       read_frags(kt, q);
-      if (q == 1) issue(kt + 1, 1);
-      if (q == 3) issue(kt + 2, 0);
+      if constexpr (SPREAD) {
+        // one operand's half per phase (2 glds), each as early as its region's last read allows: B1 was
+        // last read in R_2 of kt-1, A1 in R_3 of kt-1, B0 in R_0 of kt, A0 in R_1 of kt (the counts seen
+        // by the vmcnt(8) waits are unchanged: the same 8 glds are younger at each wait)
+        if (q == 0) issue(kt + 1, 1, 2);
+        if (q == 1) issue(kt + 1, 1, 1);
+        if (q == 2) issue(kt + 2, 0, 2);
+        if (q == 3) issue(kt + 2, 0, 1);
+      } else {
+        if (q == 1) issue(kt + 1, 1);
+        if (q == 3) issue(kt + 2, 0);
+      }
       if (wm == 1 && (q & 1)) wait_vmcnt<8>();   // before the barrier preceding row 0's R_{q+1}
       raw_barrier();
       // M_q
@@ -1636,6 +1649,8 @@ int g_gemm8 = [] { const char* s = getenv("CFM_GEMM8"); return s ? atoi(s) : 1; 
 // measured no faster than the tiled 256x256 kernel in the forward (4.957-4.966 against 4.963-4.968 ms)
 // and 0.07 ms slower per training step - these GEMMs lose their time in the fill and the epilogue)
 int g_gemm8_dense = [] { const char* s = getenv("CFM_GEMM8_DENSE"); return s ? atoi(s) : 0; }();
+// 8-phase loop: one operand half (2 glds) per phase instead of both halves every other phase (A/B)
+int g_g8_spread = [] { const char* s = getenv("CFM_G8_SPREAD"); return s ? atoi(s) : 0; }();
 // write-through (sc1) output stores: CFM_GEMM_WT=0 turns them off (A/B measurements)
 int g_gemm_wt = [] { const char* s = getenv("CFM_GEMM_WT"); return s ? atoi(s) : 1; }();
 // K-group tiles (KG > 1, >= 3 ring stages): the whole next K-step's fragments are read while the
@@ -1789,8 +1804,12 @@ void gemm(int dtype, const void* A, long lda, int M, int K, const void* Wp, int 
     a.fill(al);
     p.Mtiles = (M + 255) / 256;
     p.Ntiles = (N + 255) / 256;
-    if (epi.mode == EPI_SWISH)
+    if (epi.mode == EPI_SWISH && g_g8_spread)
+      cfm_launch((gemm8_kernel<EPI_SWISH, ALoadDense<2>, true>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    else if (epi.mode == EPI_SWISH)
       cfm_launch((gemm8_kernel<EPI_SWISH, ALoadDense<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    else if (g_g8_spread)
+      cfm_launch((gemm8_kernel<EPI_SWISH_Z, ALoadDense<2>, true>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
     else
       cfm_launch((gemm8_kernel<EPI_SWISH_Z, ALoadDense<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
     return;
@@ -1880,7 +1899,10 @@ void gemm_conv(int dtype, const ConvGeom& g, int B, const void* Wp, int Kpad, in
     a.fill(al);
     p.Mtiles = (M + 255) / 256;
     p.Ntiles = (N + 255) / 256;
-    cfm_launch((gemm8_kernel<EPI_RELU, ALoadConv<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    if (g_g8_spread)
+      cfm_launch((gemm8_kernel<EPI_RELU, ALoadConv<2>, true>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
+    else
+      cfm_launch((gemm8_kernel<EPI_RELU, ALoadConv<2>>), dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, al);
     return;
   }
   int tile = pick_tile(dtype, M, N, epi.mode, true);

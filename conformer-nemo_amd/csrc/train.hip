@@ -2145,7 +2145,26 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   else
     cfm_launch(relu_mask_kernel<bf16_t>, dim3(ew_grid(n2)), dim3(256), 0, st, dX2, S.T_<const bf16_t>(S.tp.X2), n2);
   const bool need_c1 = Gp(S.i_c1w) || Gp(S.i_c1b);
-  if (Gp(S.i_c2w) || Gp(S.i_c2b)) {   // [dW2 | db2] = dY2^T . [im2col(X1) | 1]
+  // the frame-major compute-type dY2 (the TN weight gradient's A operand and the transposed conv's input)
+  bool pa_dy2 = false;
+  static const bool tn_conv_on = [] { const char* e = getenv("CFM_TN_CONV"); return e ? atoi(e) != 0 : true; }();
+  if ((Gp(S.i_c2w) || Gp(S.i_c2b)) && tn_conv_on && wgrad_tn_conv_supported(dt, g.C, S.kpad(g.C))) {
+    // [dW2 | db2] = dY2^T . [im2col(X1) | 1] on the frame-major TN kernel with the im2col formed by its
+    // loader: no transposed dY2, no 1.47 GB im2col image.  One row split per CU over the 256x256 tiles.
+    S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
+    pa_dy2 = true;
+    const long K9 = 9L * g.C, Kb = K9 + 4;
+    const long tiles = (long)((g.C + 255) / 256) * ((K9 + 255) / 256);
+    long nsp = std::max<long>(1, std::min<long>(256 / tiles, wgrad_splits(g.C, (int)Kb, g.M2)));
+    const long chunk = round_up((g.M2 + nsp - 1) / nsp, 32);
+    nsp = (g.M2 + chunk - 1) / chunk;
+    float* part = S.W_<float>(S.wl.part);
+    float* tmp = S.W_<float>(S.wl.gtmp);   // (C, 9C) permuted gradient
+    wgrad_tn_conv(pa, S.kpad(g.C), S.T_(S.tp.X1), g.B, g.T1, g.F1, g.T2, g.F2, g.C, Gp(S.i_c2b) != nullptr, g.M2,
+                  (int)nsp, chunk, part, Kb, (long)g.C * Kb, st);
+    slab_sum_wb(part, (int)nsp, g.C, (int)K9, tmp, Gp(S.i_c2b), st);
+    if (Gp(S.i_c2w)) S.perm(tmp, 5, Gp(S.i_c2w), true, K9, g.C, (int)K9);
+  } else if (Gp(S.i_c2w) || Gp(S.i_c2b)) {   // [dW2 | db2] = dY2^T . [im2col(X1) | 1]
     S.pack(dX2, false, g.C, (int)g.M2, g.C, true, 1.0f, pat, g.M2p, g.C, (int)g.M2p);
     const dim3 grid((unsigned)((g.M2p + 31) / 32), (unsigned)((S.npad(9L * g.C + 4) + 31) / 32));
     const dim3 grid64((unsigned)((g.M2p + 63) / 64), (unsigned)((S.npad(9L * g.C + 4) + 255) / 256));   // 4 row tiles / block
@@ -2171,7 +2190,7 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
     // dY1 = conv2's transposed conv as four stride-phase implicit GEMMs straight from dY2 (no dCol
     // image, no col2im): phase (pt, pf) of the input pixels gathers the (1+pt)(1+pf) taps reaching it.
     // The phase-major result (compute type) is masked by conv1's ReLU inside conv1's weight-gradient kernel.
-    S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
+    if (!pa_dy2) S.pack(dX2, false, g.C, (int)g.M2, g.C, false, 1.0f, pa, S.kpad(g.C), (int)g.M2, S.kpad(g.C));
     char* dy1 = (char*)S.W_<float>(S.wl.dy1);
     const PhaseRows pr(g.B, g.T1, g.F1);
     char* wp = (char*)wt;

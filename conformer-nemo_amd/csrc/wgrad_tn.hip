@@ -194,6 +194,10 @@ struct TnArgs {
   float* C; long ldc, cz1, cz2;
   int M, N, Nout, K, Z2, Ktot, ones;
   float alpha;
+  // CONV (conv.2's weight gradient): B is the implicit im2col of the conv.2 input X1 [b][T1][F1][C]
+  // (= p.B): frame row r = (b, t2, f2) of the T2 x F2 output grid, column tap * C + c reads
+  // X1[b][2 t2 - 1 + tap / 3][2 f2 - 1 + tap % 3][c] (zero outside the image); C % 128 == 0
+  int cT1, cF1, cT2, cF2, cC;
 };
 
 // Output tile (128*MI) x (128*NI) on 4*MI*NI waves of 64 x 64; a stage holds MI A and NI B column
@@ -202,7 +206,7 @@ struct TnArgs {
 // Bias (p.ones): the block whose column tile is (row tile % column tiles) also sums its A fragments
 // (frame rows of dy for its columns) in VALU beside the MFMAs (waves of the first wave column) and
 // writes sum_r A[r][m] at output column p.N - no appended ones column, so no extra column tile.
-template <int MI, int NI>
+template <int MI, int NI, bool CONV = false>
 __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
   constexpr int TM = TB * MI, TN = TB * NI, NW = 4 * MI * NI, WN = 2 * NI;
   constexpr int STG = (MI + NI) * TK * 256;          // one stage: MI A images, NI B images
@@ -228,6 +232,9 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
   long gstep[G];
   int grow[G];
   bool gok[G];
+  // CONV: this lane's output pixel (b, t2, f2) for its row of the next stage, advanced by TK rows per
+  // stage (F2 >= 16: at most two wraps of f2), and its tap's pixel offset (kt, kf) and channel base
+  int cb[G], ct2[G], cf2[G], ckt[G], ckf[G], ccc[G];
   const void* zp = (const void*)&g_zero16;
 #pragma unroll
   for (int j = 0; j < G; ++j) {
@@ -235,6 +242,7 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
     const int row = rg * 4 + (lane >> 4), pc = lane & 15;
     const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
     grow[j] = row;
+    cb[j] = ct2[j] = cf2[j] = ckt[j] = ckf[j] = ccc[j] = 0;
     if (im < MI) {
       const int na = m0 + im * TB + ch * 8;
       gok[j] = na < p.M;
@@ -245,6 +253,17 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
       gok[j] = kb < p.N;
       gp[j] = (const char*)(B + (long)row * p.ldb + kb);
       gstep[j] = (long)TK * p.ldb * 2;
+      if constexpr (CONV) {
+        const int tap = kb / p.cC;
+        ckt[j] = tap / 3;
+        ckf[j] = tap - 3 * ckt[j];
+        ccc[j] = kb - tap * p.cC;
+        const int r = z2 * p.K + row, grid2 = p.cT2 * p.cF2;   // global frame row of stage 0
+        cb[j] = r / grid2;
+        const int rem = r - cb[j] * grid2;
+        ct2[j] = rem / p.cF2;
+        cf2[j] = rem - ct2[j] * p.cF2;
+      }
     }
   }
   auto issue = [&](int s) {
@@ -253,7 +272,20 @@ __global__ __launch_bounds__(256 * MI * NI) void tn_glds_kernel(TnArgs p) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int gi = w * G + j, im = gi >> 3, rg = gi & 7;
-      glds16((gok[j] && r0 + grow[j] < rows) ? (const void*)gp[j] : zp, base + im * (TK * 256) + rg * 1024);
+      const void* src = (gok[j] && r0 + grow[j] < rows) ? (const void*)gp[j] : zp;
+      if constexpr (CONV) {
+        if (im >= MI) {
+          const int t1 = 2 * ct2[j] - 1 + ckt[j], f1 = 2 * cf2[j] - 1 + ckf[j];
+          const bool in = t1 >= 0 && t1 < p.cT1 && f1 >= 0 && f1 < p.cF1;
+          src = (gok[j] && in && r0 + grow[j] < rows)
+                    ? (const void*)(p.B + (((long)cb[j] * p.cT1 + t1) * p.cF1 + f1) * p.cC + ccc[j])
+                    : zp;
+          cf2[j] += TK;
+          while (cf2[j] >= p.cF2) { cf2[j] -= p.cF2; ++ct2[j]; }
+          while (ct2[j] >= p.cT2) { ct2[j] -= p.cT2; ++cb[j]; }
+        }
+      }
+      glds16(src, base + im * (TK * 256) + rg * 1024);
       gp[j] += gstep[j];
     }
   };
@@ -396,6 +428,26 @@ void wgrad_tn(const void* A, long lda, int N, const void* B, long ldb, int K, bo
   else
     cfm_launch(wgrad_tn_kernel<0>, grid, block, 0, st, (const bf16_t*)A, lda, N, (const bf16_t*)B, ldb, K,
                ones ? 1 : 0, bdr, rows, chunk, out, ldo, Kout, split_stride);
+}
+
+// conv.2's weight gradient straight from the frame-major dY2 (rows x C, lda) and the conv.2 input X1
+// ([B][T1][F1][C], compute type): out[s][n][tap * C + c] (ld ldo, split stride split_stride) partial sums
+// over frame-row chunks of `chunk` rows (S = ceil(rows / chunk) splits), the bias sums at column 9C when
+// `ones`.  256x256 tiles (one block per CU, 16 waves): the per-CU L2 -> LDS stream is the bound of this
+// long-K product, and the larger tile halves its bytes per MFMA.  No im2col image is written.
+bool wgrad_tn_conv_supported(int dtype, int C, long lda) { return dtype == DT_BF16 && C % 256 == 0 && lda % 8 == 0; }
+void wgrad_tn_conv(const void* dy, long lda, const void* x1, int B, int T1, int F1, int T2, int F2, int C, bool ones,
+                   long rows, int S, long chunk, float* out, long ldo, long split_stride, hipStream_t st) {
+  (void)B;
+  TnArgs p{};
+  p.A = (const bf16_t*)dy; p.lda = lda; p.az2 = chunk * lda;
+  p.B = (const bf16_t*)x1; p.ldb = 9L * C; p.bz2 = 0;
+  p.C = out; p.ldc = ldo; p.cz2 = split_stride;
+  p.M = C; p.N = 9 * C; p.Nout = 9 * C; p.K = (int)chunk; p.Z2 = S; p.Ktot = (int)rows; p.ones = ones ? 1 : 0;
+  p.alpha = 1.0f;
+  p.cT1 = T1; p.cF1 = F1; p.cT2 = T2; p.cF2 = F2; p.cC = C;
+  const dim3 grid((unsigned)((9 * C + 255) / 256), (unsigned)((C + 255) / 256), (unsigned)S);
+  cfm_launch((tn_glds_kernel<2, 2, true>), grid, dim3(1024), 0, st, p);
 }
 
 }  // namespace cfm
