@@ -174,7 +174,7 @@ __device__ __forceinline__ void bar() {
 }
 
 #ifndef CFM_TN_NST
-#define CFM_TN_NST 3
+#define CFM_TN_NST 4
 #endif
 // ring stages (prefetch distance NST - 1): 3 x 16 KB, so three blocks (12 waves) share a CU's LDS; same-box
 // training A/B (tools/train_lib_ab.sh): 31.49-31.61 ms/step at 3 stages against 31.70-31.77 at 4, 2 and 5
