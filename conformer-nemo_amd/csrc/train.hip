@@ -2147,6 +2147,9 @@ void train_backward(Step& S, const float* dy_bdt, float* const* G) {
   const bool need_c1 = Gp(S.i_c1w) || Gp(S.i_c1b);
   // the frame-major compute-type dY2 (the TN weight gradient's A operand and the transposed conv's input)
   bool pa_dy2 = false;
+  // CFM_TN_CONV=0: the im2col image + packed GEMM (A/B).  The bias as column sums of the fp32 dY2 instead of
+  // the kernel's bf16 row sums measured slower (29.79-29.85 against 29.70-29.78 ms per step,
+  // profiles/r05m_tn_conv_bias_ab.txt).
   static const bool tn_conv_on = [] { const char* e = getenv("CFM_TN_CONV"); return e ? atoi(e) != 0 : true; }();
   if ((Gp(S.i_c2w) || Gp(S.i_c2b)) && tn_conv_on && wgrad_tn_conv_supported(dt, g.C, S.kpad(g.C))) {
     // [dW2 | db2] = dY2^T . [im2col(X1) | 1] on the frame-major TN kernel with the im2col formed by its
