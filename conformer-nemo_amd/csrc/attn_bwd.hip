@@ -423,16 +423,25 @@ __global__ __launch_bounds__(256) void attn_dscore_kernel(float* __restrict__ P,
 // Row reduction over one block's 32 query rows for values held in 32x32 accumulator layout
 // (v[e] belongs to row acc_row(e, lane)): the 32 lanes of a half-wave, then the waves through LDS
 // in a fixed order.  Every lane returns the block-wide value of its 16 rows.
+template <int CTRL> CFM_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// reduction over the 32 lanes of a half-wave, the same value in every lane: DPP quad permutes and row
+// mirrors (VALU, in-row sources only) for 16 lanes, one xor-16 shuffle (pairwise commutative steps, so every
+// lane computes the same bits)
+template <bool MAX>
+CFM_DEV float halfwave_red(float v) {
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+  v = op(v, dpp_f<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = op(v, dpp_f<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op(v, dpp_f<0x141>(v));   // row_half_mirror
+  v = op(v, dpp_f<0x140>(v));   // row_mirror
+  return op(v, __shfl_xor(v, 16, 32));
+}
 template <bool MAX>
 CFM_DEV void block_rows(float (&v)[16], float* red, float* fin, int w, int nw, int lane) {
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) {
-      const float t = __shfl_xor(v[e], o, 64);
-      v[e] = MAX ? fmaxf(v[e], t) : v[e] + t;
-    }
-  }
+  for (int e = 0; e < 16; ++e) v[e] = halfwave_red<MAX>(v[e]);
   if ((lane & 31) == 0) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) red[w * 32 + acc_row(e, lane)] = v[e];
@@ -579,13 +588,19 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
     }
   }
   block_rows<false>(sum, red, fin, w, nw, lane);
-  // attention dropout: dp is the gradient of the dropped probabilities -> chain through the mask
+  // attention dropout: dp is the gradient of the dropped probabilities -> chain through the mask (kept
+  // as one bit per element for the P staging below: one hash per element)
+  uint32_t keep = 0;
   if (adrop.thr) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const uint64_t rb = ((uint64_t)bh * Tp + (uint64_t)min(i0 + acc_row(e, lane), Tp - 1)) * (uint64_t)Tp;
 #pragma unroll
-      for (int c = 0; c < 2; ++c) dp[c][e] *= drop_mul(adrop, rb + (uint64_t)(64 * w + 32 * c + l32));
+      for (int c = 0; c < 2; ++c) {
+        const float m = drop_mul(adrop, rb + (uint64_t)(64 * w + 32 * c + l32));
+        dp[c][e] *= m;
+        keep |= (m != 0.0f ? 1u : 0u) << (16 * c + e);
+      }
     }
   }
   float D[16];
@@ -609,12 +624,12 @@ __global__ __launch_bounds__(512) void attn_bwd_scores_kernel(
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int row = acc_row(e, lane);
-    const uint64_t rb = ((uint64_t)bh * Tp + (uint64_t)min(i0 + row, Tp - 1)) * (uint64_t)Tp;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int j = 64 * w + 32 * c + l32;
       // P goes to the dv GEMM: the dropped probabilities (the forward's P.V operand)
-      Ps[row * SP + j] = f2bf(adrop.thr ? sc[c][e] * drop_mul(adrop, rb + j) : sc[c][e]);
+      const float pm = ((keep >> (16 * c + e)) & 1u) ? sc[c][e] * adrop.scale : 0.0f;
+      Ps[row * SP + j] = f2bf(adrop.thr ? pm : sc[c][e]);
       dSs[row * SP + j] = f2bf(sc[c][e] * (dp[c][e] - D[e]));
     }
   }

@@ -75,6 +75,7 @@ struct Drop {
   uint32_t thr;    // 0 = no dropout
   uint32_t key;    // per (step, site)
   float scale;     // 1 / (1 - p)
+  uint32_t k0;     // mix32(key): the element-independent half of the hash for indices below 2^32
 };
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
@@ -82,7 +83,12 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 }
 __device__ __forceinline__ float drop_mul(const Drop& d, uint64_t e) {
   if (d.thr == 0) return 1.0f;
-  const uint32_t h = mix32((uint32_t)e ^ mix32(d.key ^ (uint32_t)(e >> 32) * 0x9e3779b9u));
+  // the inner mix depends only on e >> 32, which is 0 for every index below 2^32: taken from d.k0, and
+  // computed only when some lane of the wave has a larger index (a wave-uniform branch)
+  const uint32_t hi = (uint32_t)(e >> 32);
+  uint32_t km = d.k0;
+  if (__builtin_amdgcn_ballot_w64(hi != 0)) km = mix32(d.key ^ hi * 0x9e3779b9u);
+  const uint32_t h = mix32((uint32_t)e ^ km);
   return h >= d.thr ? d.scale : 0.0f;
 }
 
@@ -97,6 +103,7 @@ inline Drop make_drop(float p, uint64_t seed, int site) {
   const double t = (p < 1.0f ? (double)p : 1.0) * 4294967296.0;
   d.thr = (uint32_t)(t > 4294967295.0 ? 4294967295.0 : (t < 1.0 ? 1.0 : t));
   d.key = host_mix32((uint32_t)seed ^ host_mix32((uint32_t)(seed >> 32) + 0x632be5abu * (uint32_t)site));
+  d.k0 = host_mix32(d.key);
   d.scale = p < 1.0f ? 1.0f / (1.0f - p) : 0.0f;
   return d;
 }
