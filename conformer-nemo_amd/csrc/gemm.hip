@@ -1527,28 +1527,237 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   raw_barrier();
   if (wm == 1) raw_barrier();
   f32x16 xd;
-  for (int kt = 0; kt < nk; ++kt) {
+  // timing probes (CFM_GEMM_PROBE, wrong results): 8 no X1 computation in the loop, 16 no W2 / patch
+  // LDS-DMA in the loop, 32 no MFMAs in the M phases, 64 no fragment reads
+  const int probe = p.probe;
+  const int nkl = (probe & 128) ? 0 : nk;   // 128: no main loop (prologue + epilogue only)
+  for (int kt = 0; kt < nkl; ++kt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       // R_q
-      read_frags(kt, q);
+      if (!(probe & 64)) read_frags(kt, q);
       // the A halves the DMA version loads at R_1 / R_3: contraction issued one phase earlier
-      if (q == 0) xd = x1_mfma(kt + 1, 1);
-      if (q == 1) { issue_b(kt + 1, 1); x1_store(kt + 1, 1, xd); }
-      if (q == 2) xd = x1_mfma(kt + 2, 0);
-      if (q == 3) { issue_b(kt + 2, 0); issue_patch((kt + 4) / ktap); x1_store(kt + 2, 0, xd); }
+      if (!(probe & 8)) {
+        if (q == 0) xd = x1_mfma(kt + 1, 1);
+        if (q == 1) x1_store(kt + 1, 1, xd);
+        if (q == 2) xd = x1_mfma(kt + 2, 0);
+        if (q == 3) x1_store(kt + 2, 0, xd);
+      }
+      if (!(probe & 16)) {
+        if (q == 1) issue_b(kt + 1, 1);
+        if (q == 3) { issue_b(kt + 2, 0); issue_patch((kt + 4) / ktap); }
+      }
       if (wm == 1 && (q & 1)) wait_vmcnt<5>();   // before the barrier preceding row 0's R_{q+1}
       raw_barrier();
       // M_q
       wait_lgkm0();
       __builtin_amdgcn_s_setprio(1);
+      if (!(probe & 32)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[(q & 1) * 4 + i][j] = mfma16_16x16x32(af[i], bfr[j], acc[(q & 1) * 4 + i][j]);
+          for (int j = 0; j < 4; ++j)
+            acc[(q & 1) * 4 + i][j] = mfma16_16x16x32(af[i], bfr[j], acc[(q & 1) * 4 + i][j]);
+      }
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0 && (q & 1)) wait_vmcnt<5>();
+      raw_barrier();
+    }
+  }
+  if (wm == 0) raw_barrier();   // re-align the barrier counts of the two wave rows
+  wait_vmcnt<0>();
+  wait_lgkm0();
+  raw_barrier();
+
+  if (probe & 256) {   // 256: no epilogue (keep the accumulators live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0];
+    if (t == 1234.5f) ((float*)p.epi.C)[threadIdx.x] = t;
+    return;
+  }
+  float* img = (float*)smem;
+  float bcol[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bcol[j] = p.epi.bias ? p.epi.bias[n0 + wn * 64 + j * 16 + fr] : 0.0f;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            img[(i * 16 + fc * 4 + e) * T8::EPS + wn * 64 + j * 16 + fr] = acc[i][j][e] + bcol[j];
+    }
+    __syncthreads();
+    epilogue<bf16_t, EPI_RELU, EpiView<T8>, false>(p, img, m0 + pass * 128, n0, 0, nullptr, nullptr);
+  }
+}
+
+__global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args ca) {
+  __shared__ __attribute__((aligned(16))) char smem[C12_LDS];
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int C = ca.C;
+
+  // block -> tile as gemm8_kernel (giving each XCD parity one of the two column tiles, so that an XCD's L2
+  // holds half of W2, measured neutral: profiles/r04g_conv12_xcd_cols_ab.txt)
+  const int nblocks = p.Mtiles * p.Ntiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nblocks >> 3, rr = nblocks & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int mt = wg / p.Ntiles, ntl = wg - mt * p.Ntiles;
+  const int m0 = mt * 256, n0 = ntl * 256;
+
+  // B staging (W2 rows): as gemm8_kernel
+  int rows[2], lo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rows[i] = (i * 8 + wave) * 16 + (lane >> 2);
+    lo[i] = ((lane & 3) ^ g8_swz(rows[i])) * 16;
+  }
+  const char* wrow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) wrow[i] = p.W + (long)(n0 + rows[i]) * p.ldw_b + lo[i];
+  const char* zsrc = ca.zero + lane * 16;
+  const uint32_t sbase = lds_addr(smem);
+  const int nk = p.kb / 128;
+  const int ktap = C / 64;                       // K-tiles per conv.2 tap
+
+  // this lane's X1 row (tile row 32 * wave + (lane & 31)) and its conv2-input pixel base (ring grid)
+  const int xrow = 32 * wave + (lane & 31);
+  const int am = m0 + xrow;
+  const bool arow_ok = am < p.M;
+  const int amc = min(am, p.M - 1);
+  const int af2 = amc % ca.F2, bt = amc / ca.F2;
+  const int at2 = bt % ca.T2, ab = bt / ca.T2;
+  const uint4* prow = ca.patch + 2 * (((long)ab * (ca.T1 + 2) + 2 * at2) * (ca.F1 + 2) + 2 * af2) + (lane >> 5);
+  const uint32_t pbase = sbase + 2 * G8_BUF;     // patch fragments
+  const char* w1img = smem + 2 * G8_BUF + C12_PATCH;
+
+  // LDS-DMA of this wave's patch rows for conv.2 tap `tap` (clamped) into buffer tap & 1
+  auto issue_patch = [&](int tap) {
+    tap = min(tap, 8);
+    const int kt2 = tap / 3, kf2 = tap - 3 * kt2;
+    const void* src = arow_ok ? (const void*)(prow + 2 * (kt2 * (ca.F1 + 2) + kf2)) : (const void*)zsrc;
+    glds16_asm(src, pbase + (tap & 1) * 8192 + wave * 1024);
+  };
+  auto issue_b = [&](int kt, int h) {   // K-half h of K-tile kt of W2: 2 LDS-DMA
+    const uint32_t base = sbase + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const bool live = kt < nk;
+    const int kb0 = kt * 128 + h * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16_asm(live ? wrow[i] + kb0 : zsrc, base + G8_HALF + (i * 8 + wave) * 1024);
+  };
+  // X1 for K-half (kt, h): 32 channels of tap kt / ktap, rows 32 * wave + (lane & 31).  Two halves so
+  // that the MFMA's latency is not waited for inside one R phase: x1_mfma issues the contraction, one
+  // phase later x1_store converts (bf16 pairs, ReLU as a packed int16 max on the bf16 bits: negative
+  // values have the sign bit set, so max(x, 0) as int16 is max(x, +0) as bf16), regroups and writes.
+  auto x1_mfma = [&](int kt, int h) -> f32x16 {
+    if (kt >= nk) return f32x16{};
+    const int tap = kt / ktap;
+    const int c0 = (kt - tap * ktap) * 64 + 32 * h;
+    const uint4 wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
+    const uint4 pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
+                                                 f32x16{}, 0, 0, 0);
+  };
+  auto x1_store = [&](int kt, int h, const f32x16& d) {
+    if (kt >= nk) return;
+    typedef __attribute__((ext_vector_type(2))) short s16x2;
+    uint32_t q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t u = (uint32_t)f2bf(d[2 * i]) | ((uint32_t)f2bf(d[2 * i + 1]) << 16);
+      q[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
+    }
+    const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(q[1], q[3], false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(q[4], q[6], false, false);
+    const auto s3 = __builtin_amdgcn_permlane32_swap(q[5], q[7], false, false);
+    char* img = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const int hi = lane >> 5, sw = g8_swz(xrow);
+    // lanes < 32: channels 0-7 / 16-23 of the K-half, lanes >= 32: 8-15 / 24-31
+    *(uint4*)(img + xrow * 64 + ((hi) ^ sw) * 16) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    *(uint4*)(img + xrow * 64 + ((2 + hi) ^ sw) * 16) = make_uint4(s2[0], s3[0], s2[1], s3[1]);
+  };
+  auto compute_x1 = [&](int kt, int h) { x1_store(kt, h, x1_mfma(kt, h)); };
+
+  // conv.0's weights into LDS (C x 32 B), once per block, before any LDS-DMA is in flight (plain loads:
+  // hipcc waits for them here); visible to every wave after the raw barrier
+  for (int i = tid; i < 2 * C; i += 512) ((uint4*)w1img)[i] = ca.w1h[i];
+  wait_lgkm0();
+  raw_barrier();
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int fslot = (fc ^ g8_swz(fr)) * 16;
+  uint4 af[8], bfr[4];
+  auto read_frags = [&](int kt, int h) {   // K-half h of K-tile kt: the wave's 128 rows and 64 columns
+    const char* hb = smem + (kt & 1) * G8_BUF + h * 2 * G8_HALF;
+    const int r0 = wm * 128 + fr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const uint4*)(hb + (r0 + i * 16) * 64 + fslot);
+    const int c0 = wn * 64 + fr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = *(const uint4*)(hb + G8_HALF + (c0 + j * 16) * 64 + fslot);
+  };
+
+  // prologue: tap 0's patch and the B halves (0,0), (0,1); the A halves (0,0), (0,1) computed, (1,0)'s
+  // contraction issued (stored in R_0 of K-tile 0)
+  issue_patch(0);
+  issue_b(0, 0);
+  issue_b(0, 1);
+  wait_vmcnt<4>();            // tap 0's patch has landed (this wave's own rows: no barrier needed)
+  compute_x1(0, 0);
+  compute_x1(0, 1);
+  f32x16 xd0 = x1_mfma(1, 0), xd1;
+  wait_vmcnt<2>();            // B (0,0) complete; (0,1) in flight
+  wait_lgkm0();
+  raw_barrier();
+  if (wm == 1) raw_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // R_h: K-half h's fragments; K-half h of K-tile kt + 1 into the other buffer (its last readers
+      // finished R_h of K-tile kt - 1, two phases ago): W2 by LDS-DMA, X1 computed (contraction one
+      // phase earlier)
+      read_frags(kt, h);
+      if (h == 0) {
+        x1_store(kt + 1, 0, xd0);
+        xd1 = x1_mfma(kt + 1, 1);
+        issue_b(kt + 1, 0);
+        issue_patch((kt + 4) / ktap);
+      } else {
+        x1_store(kt + 1, 1, xd1);
+        xd0 = x1_mfma(kt + 2, 0);
+        issue_b(kt + 1, 1);
+      }
+      // before the barrier preceding row 0's next R phase: that phase's W2 half has landed (three
+      // younger LDS-DMA per wave: the next half's two and a patch)
+      if (wm == 1) wait_vmcnt<3>();
+      raw_barrier();
+      // M_h: 32 MFMAs
+      wait_lgkm0();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_16x16x32(af[i], bfr[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0) wait_vmcnt<3>();
       raw_barrier();
     }
   }
@@ -1939,11 +2148,15 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   e.C = X2;
   e.ldc = C;
   GemmParams p = make_params(2, M, Wp, Kpad, C, e);
-  p.probe = 0;
+  p.probe = g_gemm_probe & (8 | 16 | 32 | 64 | 128 | 256);   // timing studies only (wrong results), see conv12_kernel
   p.Mtiles = (M + 255) / 256;
   p.Ntiles = (C + 255) / 256;
   Conv12Args a{(const uint4*)patch, w1h, (const char*)zero_page, T1, F1, T2, F2, C};
-  cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
+  // CFM_CONV12B=1: two phases of 32 MFMAs per K-tile instead of four of 16 (half the barriers)
+  const char* tp_env = getenv("CFM_CONV12B");   // read per call (tests switch it between forwards)
+  const bool two_phase = tp_env && atoi(tp_env) != 0;
+  if (two_phase) cfm_launch(conv12b_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
+  else cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
 }
 
 bool gemm_tconv_supported(int dtype, int C) { return C > 0 && ((long)C * dtype_size(dtype)) % 128 == 0; }

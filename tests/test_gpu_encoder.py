@@ -383,6 +383,28 @@ def test_bf16_fused_conv12_matches_two_kernels(B, T, monkeypatch):
     assert d <= 5e-3
 
 
+@pytest.mark.parametrize("B,T", [(2, 333), (32, 1000)])
+def test_conv12_two_phase_loop_is_bitwise_the_four_phase_loop(B, T, monkeypatch):
+    """conv12b_kernel (CFM_CONV12B=1: two phases of 32 MFMAs per K-tile, half the barriers) issues the same
+    MFMAs in the same K order per accumulator as conv12_kernel: the encoder output is bitwise equal."""
+    z = np.load(os.path.join(GOLDEN, "enc_large17.npz"))
+    cfg = dict(json.loads(str(z["cfg_json"])), n_layers=2)
+    sd = {k: v for k, v in make_state_dict(json.loads(str(z["cfg_json"])), int(z["seed"])).items()
+          if not k.startswith("layers.") or k.split(".")[1] in ("0", "1")}
+    g = torch.Generator().manual_seed(B + T + 1)
+    x = torch.randn(B, 80, T, generator=g).numpy()
+    lens = np.array([T - (5 * i) % (T // 2) for i in range(B)], dtype=np.int64)
+    monkeypatch.setenv("CFM_CONV12", "1")
+    enc = native(cfg, "bf16")
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("CFM_CONV12B", flag)
+        out[flag] = run(enc, sd, x, lens)
+    assert np.isfinite(out["1"][0]).all()
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+
+
 @pytest.mark.parametrize("compute", ["bf16", "fp16"])
 def test_fused_conv12_matches_reference(compute, monkeypatch):
     """The fused front end through the whole Large-17 encoder against the reference outputs, under the
