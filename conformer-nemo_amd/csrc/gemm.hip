@@ -275,6 +275,13 @@ CFM_DEV float ln_fold(float2 s, float v, float2 cd) { return s.y * (v - s.x * cd
 template <int CTRL> CFM_DEV float dpp_mov(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+// two fp32 -> a packed pair of the 16-bit compute type, as f2bf rounds each: bf16 in one v_cvt_pk_bf16_f32
+#ifdef CFM_HALF_F16
+CFM_DEV uint32_t pk_bf16x2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+#else
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+CFM_DEV uint32_t pk_bf16x2(float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2_t{(__bf16)a, (__bf16)b}); }
+#endif
 CFM_DEV float halfwave_sum(float v) {
   v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]
@@ -1454,14 +1461,24 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   // that the MFMA's latency is not waited for inside one R phase: x1_mfma issues the contraction, one
   // phase later x1_store converts (bf16 pairs, ReLU as a packed int16 max on the bf16 bits: negative
   // values have the sign bit set, so max(x, 0) as int16 is max(x, +0) as bf16), regroups and writes.
-  auto x1_mfma = [&](int kt, int h) -> f32x16 {
-    if (kt >= nk) return f32x16{};
-    const int tap = kt / ktap;
-    const int c0 = (kt - tap * ktap) * 64 + 32 * h;
-    const uint4 wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
-    const uint4 pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+  // its operands (W1 rows, this wave's patch rows) read before the phase's fragment reads, so the
+  // contraction waits only for them; past the last K-tile the clamped K-tile's operands (the result is
+  // not stored), so the result is not consumed in the phase it is issued in
+  auto x1_ops = [&](int kt, int h, uint4& wf, uint4& pf) {
+    const int ktc = min(kt, nk - 1);
+    const int tap = ktc / ktap;
+    const int c0 = (ktc - tap * ktap) * 64 + 32 * h;
+    wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
+    pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+  };
+  auto x1_mma = [&](const uint4& wf, const uint4& pf) -> f32x16 {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
                                                  f32x16{}, 0, 0, 0);
+  };
+  auto x1_mfma = [&](int kt, int h) -> f32x16 {
+    uint4 wf, pf;
+    x1_ops(kt, h, wf, pf);
+    return x1_mma(wf, pf);
   };
   auto x1_store = [&](int kt, int h, const f32x16& d) {
     if (kt >= nk) return;
@@ -1469,7 +1486,7 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
     uint32_t q[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const uint32_t u = (uint32_t)f2bf(d[2 * i]) | ((uint32_t)f2bf(d[2 * i + 1]) << 16);
+      const uint32_t u = pk_bf16x2(d[2 * i], d[2 * i + 1]);
       q[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
     }
     const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
@@ -1535,12 +1552,16 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       // R_q
+      uint4 xw, xp;
+      if (!(probe & 8)) {
+        if (q == 0) x1_ops(kt + 1, 1, xw, xp);
+        if (q == 2) x1_ops(kt + 2, 0, xw, xp);
+      }
       if (!(probe & 64)) read_frags(kt, q);
       // the A halves the DMA version loads at R_1 / R_3: contraction issued one phase earlier
       if (!(probe & 8)) {
-        if (q == 0) xd = x1_mfma(kt + 1, 1);
+        if (q == 0 || q == 2) xd = x1_mma(xw, xp);
         if (q == 1) x1_store(kt + 1, 1, xd);
-        if (q == 2) xd = x1_mfma(kt + 2, 0);
         if (q == 3) x1_store(kt + 2, 0, xd);
       }
       if (!(probe & 16)) {
@@ -1660,14 +1681,24 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
   // that the MFMA's latency is not waited for inside one R phase: x1_mfma issues the contraction, one
   // phase later x1_store converts (bf16 pairs, ReLU as a packed int16 max on the bf16 bits: negative
   // values have the sign bit set, so max(x, 0) as int16 is max(x, +0) as bf16), regroups and writes.
-  auto x1_mfma = [&](int kt, int h) -> f32x16 {
-    if (kt >= nk) return f32x16{};
-    const int tap = kt / ktap;
-    const int c0 = (kt - tap * ktap) * 64 + 32 * h;
-    const uint4 wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
-    const uint4 pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+  // its operands (W1 rows, this wave's patch rows) read before the phase's fragment reads, so the
+  // contraction waits only for them; past the last K-tile the clamped K-tile's operands (the result is
+  // not stored), so the result is not consumed in the phase it is issued in
+  auto x1_ops = [&](int kt, int h, uint4& wf, uint4& pf) {
+    const int ktc = min(kt, nk - 1);
+    const int tap = ktc / ktap;
+    const int c0 = (ktc - tap * ktap) * 64 + 32 * h;
+    wf = *(const uint4*)(w1img + (c0 + (lane & 31)) * 32 + (lane >> 5) * 16);
+    pf = *(const uint4*)(smem + 2 * G8_BUF + (tap & 1) * 8192 + wave * 1024 + lane * 16);
+  };
+  auto x1_mma = [&](const uint4& wf, const uint4& pf) -> f32x16 {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wf), __builtin_bit_cast(f16x8, pf),
                                                  f32x16{}, 0, 0, 0);
+  };
+  auto x1_mfma = [&](int kt, int h) -> f32x16 {
+    uint4 wf, pf;
+    x1_ops(kt, h, wf, pf);
+    return x1_mma(wf, pf);
   };
   auto x1_store = [&](int kt, int h, const f32x16& d) {
     if (kt >= nk) return;
@@ -1675,7 +1706,7 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
     uint32_t q[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const uint32_t u = (uint32_t)f2bf(d[2 * i]) | ((uint32_t)f2bf(d[2 * i + 1]) << 16);
+      const uint32_t u = pk_bf16x2(d[2 * i], d[2 * i + 1]);
       q[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0}));
     }
     const auto s0 = __builtin_amdgcn_permlane32_swap(q[0], q[2], false, false);
@@ -1734,15 +1765,17 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
       // R_h: K-half h's fragments; K-half h of K-tile kt + 1 into the other buffer (its last readers
       // finished R_h of K-tile kt - 1, two phases ago): W2 by LDS-DMA, X1 computed (contraction one
       // phase earlier)
+      uint4 xw, xp;
+      x1_ops(h == 0 ? kt + 1 : kt + 2, h ^ 1, xw, xp);
       read_frags(kt, h);
       if (h == 0) {
         x1_store(kt + 1, 0, xd0);
-        xd1 = x1_mfma(kt + 1, 1);
+        xd1 = x1_mma(xw, xp);
         issue_b(kt + 1, 0);
         issue_patch((kt + 4) / ktap);
       } else {
         x1_store(kt + 1, 1, xd1);
-        xd0 = x1_mfma(kt + 2, 0);
+        xd0 = x1_mma(xw, xp);
         issue_b(kt + 1, 1);
       }
       // before the barrier preceding row 0's next R phase: that phase's W2 half has landed (three
@@ -2152,9 +2185,10 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   p.Mtiles = (M + 255) / 256;
   p.Ntiles = (C + 255) / 256;
   Conv12Args a{(const uint4*)patch, w1h, (const char*)zero_page, T1, F1, T2, F2, C};
-  // CFM_CONV12B=1: two phases of 32 MFMAs per K-tile instead of four of 16 (half the barriers)
+  // two phases of 32 MFMAs per K-tile (conv12b_kernel, default) or four of 16 (conv12_kernel, CFM_CONV12B=0):
+  // the same products in the same K order (bitwise equal), 886 -> 738 us per forward (profiles/r05u_conv12b_ab.txt)
   const char* tp_env = getenv("CFM_CONV12B");   // read per call (tests switch it between forwards)
-  const bool two_phase = tp_env && atoi(tp_env) != 0;
+  const bool two_phase = !tp_env || atoi(tp_env) != 0;
   if (two_phase) cfm_launch(conv12b_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
   else cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
 }
