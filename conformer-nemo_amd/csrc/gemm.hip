@@ -1620,6 +1620,9 @@ __global__ __launch_bounds__(512) void conv12_kernel(GemmParams p, Conv12Args ca
   }
 }
 
+// PROBE: timing studies only (CFM_GEMM_PROBE bits as conv12_kernel's: 8 no X1, 16 no LDS-DMA, 32 no main MFMAs,
+// 64 no fragment reads, 256 no epilogue; wrong results)
+template <bool PROBE>
 __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args ca) {
   __shared__ __attribute__((aligned(16))) char smem[C12_LDS];
   typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
@@ -1765,18 +1768,16 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
       // R_h: K-half h's fragments; K-half h of K-tile kt + 1 into the other buffer (its last readers
       // finished R_h of K-tile kt - 1, two phases ago): W2 by LDS-DMA, X1 computed (contraction one
       // phase earlier)
+      const int pb = PROBE ? p.probe : 0;
       uint4 xw, xp;
-      x1_ops(h == 0 ? kt + 1 : kt + 2, h ^ 1, xw, xp);
-      read_frags(kt, h);
+      if (!(pb & 8)) x1_ops(h == 0 ? kt + 1 : kt + 2, h ^ 1, xw, xp);
+      if (!(pb & 64)) read_frags(kt, h);
       if (h == 0) {
-        x1_store(kt + 1, 0, xd0);
-        xd1 = x1_mma(xw, xp);
-        issue_b(kt + 1, 0);
-        issue_patch((kt + 4) / ktap);
+        if (!(pb & 8)) { x1_store(kt + 1, 0, xd0); xd1 = x1_mma(xw, xp); }
+        if (!(pb & 16)) { issue_b(kt + 1, 0); issue_patch((kt + 4) / ktap); }
       } else {
-        x1_store(kt + 1, 1, xd1);
-        xd0 = x1_mma(xw, xp);
-        issue_b(kt + 1, 1);
+        if (!(pb & 8)) { x1_store(kt + 1, 1, xd1); xd0 = x1_mma(xw, xp); }
+        if (!(pb & 16)) issue_b(kt + 1, 1);
       }
       // before the barrier preceding row 0's next R phase: that phase's W2 half has landed (three
       // younger LDS-DMA per wave: the next half's two and a patch)
@@ -1785,10 +1786,12 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
       // M_h: 32 MFMAs
       wait_lgkm0();
       __builtin_amdgcn_s_setprio(1);
+      if (!(pb & 32)) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_16x16x32(af[i], bfr[j], acc[i][j]);
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_16x16x32(af[i], bfr[j], acc[i][j]);
+      }
       __builtin_amdgcn_s_setprio(0);
       if (wm == 0) wait_vmcnt<3>();
       raw_barrier();
@@ -1799,6 +1802,15 @@ __global__ __launch_bounds__(512) void conv12b_kernel(GemmParams p, Conv12Args c
   wait_lgkm0();
   raw_barrier();
 
+  if (PROBE && (p.probe & 256)) {   // keep the accumulators live
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0];
+    if (t == 1234.5f) ((float*)p.epi.C)[threadIdx.x] = t;
+    return;
+  }
   float* img = (float*)smem;
   float bcol[4];
 #pragma unroll
@@ -2189,7 +2201,8 @@ void conv12_fused(const float* x_bft, int B, int F, int T, int T1, int F1, int T
   // the same products in the same K order (bitwise equal), 886 -> 738 us per forward (profiles/r05u_conv12b_ab.txt)
   const char* tp_env = getenv("CFM_CONV12B");   // read per call (tests switch it between forwards)
   const bool two_phase = !tp_env || atoi(tp_env) != 0;
-  if (two_phase) cfm_launch(conv12b_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
+  if (two_phase && p.probe) cfm_launch(conv12b_kernel<true>, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
+  else if (two_phase) cfm_launch(conv12b_kernel<false>, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
   else cfm_launch(conv12_kernel, dim3(p.Mtiles * p.Ntiles), dim3(512), 0, st, p, a);
 }
 
