@@ -234,6 +234,280 @@ void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, in
                bt, lo, ldo);
 }
 
+// ---- the logits with the hidden formed in registers (bf16, round 5) ----------------------------------
+// One block = one utterance's 16 frames x 16 labels = 256 lattice rows, all Cm logit columns in chunks of
+// 256. The block's f' and g' rows (fp32) sit in LDS for its whole life; each wave builds the MFMA
+// A-fragments of act(f' + g') (x dropout), rounded to the compute type exactly as joint_hidden_kernel
+// stores them, straight from those rows: a 16 x 32 fragment of v_mfma_f32_16x16x32 is one frame t and
+// the 16 labels, so a lane reads its label's 8 g' values and the frame's 8 f' values (a broadcast). The
+// hidden lattice never goes to memory. W_out streams from L2 through a two-stage LDS ring (64 K per
+// stage, 128-byte rows XOR-swizzled by row pair); the <= 16 tail columns past the last whole chunk
+// (V + 1 = 1025 -> 1024 + 1) ride along chunk 0 as one more 16-column fragment on the left waves.
+// Waves: 4 (frames: 4 each) x 2 (columns: 128 each); accumulators go straight from registers to the
+// fp32 rows (stride C, any alignment): per store, 16 consecutive columns of 4 label rows.
+namespace jl {
+constexpr int TT = 16, UT = 16, NC = 256, KS = 64, HMAX = 640;
+constexpr int BROWS = NC + 16;                          // + the tail columns (chunk 0)
+constexpr int STAGE = BROWS * KS * 2;                   // 34816 B
+constexpr int FG_BYTES = 2 * 16 * (HMAX + 4) * 4;       // f' and g' rows, stride H + 4 floats
+constexpr int LDS = FG_BYTES + 2 * STAGE;               // 152064 B
+}  // namespace jl
+
+struct JointLogits {
+  const float* f; const float* g; const bf16_t* w; const float* bias; float* out;
+  long ldw, ldo;
+  int B, T, U, H, Cm, ntail;
+  int split;   // W loads by waves 0-3 only (CFM_JOINT_SPLIT, default 1)
+  int probe;   // timing probes only (CFM_JOINT_PROBE): 1 no logits stores, 2 no MFMAs, 4 no hidden formation
+  Drop drop;
+};
+
+typedef float jf2 __attribute__((ext_vector_type(2)));
+typedef short js2 __attribute__((ext_vector_type(2)));
+#ifndef CFM_HALF_F16
+typedef __bf16 jbf2 __attribute__((ext_vector_type(2)));
+CFM_DEV uint32_t jpk(jf2 v) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, jbf2)); }   // RNE, as f2bf
+CFM_DEV uint32_t relu_pk(uint32_t v, js2 z) { return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(js2, v), z)); }
+#endif
+template <int ACT> CFM_DEV float joint_act(float x) {
+  if constexpr (ACT == CFM_JOINT_RELU) return fmaxf(x, 0.0f);
+  else if constexpr (ACT == CFM_JOINT_SIGMOID) return 1.0f / (1.0f + expf(-x));
+  else return tanhf(x);
+}
+
+template <int ACT, bool DROP, bool PROBE = false>
+__global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
+  __shared__ __attribute__((aligned(16))) char smem[jl::LDS];
+  const int hs = p.H + 4;
+  float* Fs = (float*)smem;   // rows 0..15: f' of frames t0.., rows 16..31: g' of labels u0..
+  const float* Gs = Fs + 16 * hs;
+  char* Bs = smem + jl::FG_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nut = (p.U + jl::UT - 1) / jl::UT, ntt = (p.T + jl::TT - 1) / jl::TT;
+  const int ut = blockIdx.x % nut, rest = blockIdx.x / nut;
+  const int tt = rest % ntt, b = rest / ntt;
+  const int t0 = tt * jl::TT, u0 = ut * jl::UT;
+  {
+    const int h4 = p.H / 4;
+    for (int i = tid; i < 32 * h4; i += 512) {
+      const int r = i / h4, c = i - r * h4;
+      const bool isf = r < 16;
+      const int x = isf ? t0 + r : u0 + r - 16, X = isf ? p.T : p.U;
+      const float* src = isf ? p.f + ((long)b * p.T + min(x, X - 1)) * p.H : p.g + ((long)b * p.U + min(x, X - 1)) * p.H;
+      float4 v = *(const float4*)(src + c * 4);   // clamped row, zeroed past the end
+      if (x >= X) v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      *(float4*)(Fs + r * hs + c * 4) = v;
+    }
+  }
+  const int kst = p.H / jl::KS, nstage = kst * (p.Cm / jl::NC);
+  const bool tail = p.ntail > 0;
+  // stage s -> ring slot s & 1 by LDS-DMA: wave-chunk cw = 8 W rows x 128 B; lane l fills slot (row
+  // 8 cw + l / 8, position l % 8), i.e. the row's 16-byte K piece (l % 8) ^ ((row / 2) % 8)
+  const uint32_t bs0 = lds_addr(Bs);
+  // lane l's K piece is the same for every wave-chunk of a wave: rows 8 cw + l / 8 with cw = wave + 4 i
+  // (or + 8 i) have (row / 2) % 8 = (4 (wave % 2) + l / 16) % 8; 32-bit element offsets from the stage's
+  // wave-uniform W base
+  const int lq = (lane & 7) ^ ((((wave & 1) << 2) + (lane >> 4)) & 7);
+  const int lo = (wave * 8 + (lane >> 3)) * (int)p.ldw + lq * 8;
+  const int ldw = (int)p.ldw;
+  auto issue = [&](int s) {
+    const int c = s / kst, ks = s - c * kst;
+    const bf16_t* wb = p.w + (long)c * jl::NC * p.ldw + ks * jl::KS;
+    const uint32_t dst = bs0 + (s & 1) * jl::STAGE;
+    if (!p.split) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16_asm(wb + lo + i * 64 * ldw, dst + (wave + 8 * i) * 1024);
+    } else if (wave < 4) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) glds16_asm(wb + lo + i * 32 * ldw, dst + (wave + 4 * i) * 1024);
+    }
+  };
+  // split: waves 0-3 move W and wait for it; waves 4-7 issue no loads, so their logits stores drain while
+  // they compute (vmcnt counts stores and loads in one in-order counter per wave)
+  const bool waiter = !p.split || wave < 4;
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int ul = lane & 15, kq = lane >> 4;
+  // A-fragment of frame row tr (0..15) at K offset kk: act(f' + g') (x dropout) in the compute type
+  auto afrag = [&](int tr, int kk, const float4& g0, const float4& g1) {
+    const float* fr = Fs + tr * hs + kk;
+    const float4 f0 = *(const float4*)fr, f1 = *(const float4*)(fr + 4);
+#ifndef CFM_HALF_F16
+    if constexpr (ACT == CFM_JOINT_RELU && !DROP) {
+      // packed: 4 v_pk_add_f32, 4 v_cvt_pk_bf16_f32, then ReLU on the bf16 pairs as 16-bit integers
+      // (v_pk_max_i16: a sign-magnitude value is negative iff its sign bit is set; rounding keeps signs)
+      const jf2 s0 = jf2{f0.x, f0.y} + jf2{g0.x, g0.y}, s1 = jf2{f0.z, f0.w} + jf2{g0.z, g0.w};
+      const jf2 s2 = jf2{f1.x, f1.y} + jf2{g1.x, g1.y}, s3 = jf2{f1.z, f1.w} + jf2{g1.z, g1.w};
+      const js2 z = js2{0, 0};
+      return make_uint4(relu_pk(jpk(s0), z), relu_pk(jpk(s1), z), relu_pk(jpk(s2), z), relu_pk(jpk(s3), z));
+    }
+#endif
+    float v[8] = {f0.x + g0.x, f0.y + g0.y, f0.z + g0.z, f0.w + g0.w, f1.x + g1.x, f1.y + g1.y, f1.z + g1.z, f1.w + g1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = joint_act<ACT>(v[e]);
+    if constexpr (DROP) {
+      const long row = ((long)b * p.T + t0 + tr) * p.U + u0 + ul;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= drop_mul(p.drop, (uint64_t)row * p.H + kk + e);
+    }
+#ifndef CFM_HALF_F16
+    return make_uint4(jpk(jf2{v[0], v[1]}), jpk(jf2{v[2], v[3]}), jpk(jf2{v[4], v[5]}), jpk(jf2{v[6], v[7]}));
+#else
+    return Vec16<bf16_t>::from_f32(v);
+#endif
+  };
+  // the four A-fragments (frame rows wr * 4 + i, the 16 labels) of K offset kk
+  auto build4 = [&](int kk, uint4* a) {
+    const float4 g0 = *(const float4*)(Gs + ul * hs + kk), g1 = *(const float4*)(Gs + ul * hs + kk + 4);
+    if (PROBE && (p.probe & 4)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = make_uint4(__float_as_uint(g0.x), __float_as_uint(g0.y), __float_as_uint(g1.x), __float_as_uint(g1.y));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = afrag(wr * 4 + i, kk, g0, g1);
+    }
+  };
+  __syncthreads();   // f', g' rows in LDS (compiler-visible loads: drained here)
+  constexpr bool PIPE = ACT == CFM_JOINT_RELU && !DROP;
+  uint4 af[4];
+  if constexpr (PIPE) build4(8 * kq, af);
+  issue(0);
+  wait_vmcnt<0>();
+  __syncthreads();
+  for (int s = 0; s < nstage; ++s) {
+    const int c = s / kst, ks = s - c * kst;
+    if (s + 1 < nstage) issue(s + 1);
+    const char* bs = Bs + (s & 1) * jl::STAGE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      // the next K sub-step's fragments (K restarts with every column chunk) are formed while this
+      // sub-step's MFMAs run: they depend on the resident f' / g' rows only, not on the W ring
+      // (ReLU without dropout: the cheap formation; the others keep it in place, for their registers)
+      uint4 an[4];
+      if constexpr (PIPE) {
+        int kn = ks * 2 + sub + 1;
+        if (kn == 2 * kst) kn = 0;
+        build4(kn * 32 + 8 * kq, an);
+      } else {
+        build4((ks * 2 + sub) * 32 + 8 * kq, af);
+      }
+      const int q = sub * 4 + kq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = wc * 128 + j * 16 + ul;
+        const uint4 bf = *(const uint4*)(bs + n * 128 + ((q ^ ((n >> 1) & 7)) << 4));
+        if (!(PROBE && (p.probe & 2))) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = mfma16_16x16x32(af[i], bf, acc[i][j]);
+        }
+      }
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = an[i];
+      }
+    }
+    if (ks == kst - 1 && !(PROBE && (p.probe & 1))) {
+      // accumulator element r of lane l: label row 4 * (l >> 4) + r, column l & 15. Whole tiles (every
+      // block but the last label tile's) store without per-element conditions.
+      const int n0 = c * jl::NC + wc * 128 + ul;
+      float bn[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bn[j] = p.bias[n0 + j * 16];
+      const bool full = t0 + jl::TT <= p.T && u0 + jl::UT <= p.U;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = t0 + wr * 4 + i;
+        float* o = p.out + (((long)b * p.T + t) * p.U + u0 + 4 * kq) * p.ldo + n0;
+        if (full) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[r * p.ldo + j * 16] = acc[i][j][r] + bn[j];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t < p.T && u0 + 4 * kq + r < p.U) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) o[r * p.ldo + j * 16] = acc[i][j][r] + bn[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    }
+    if (waiter) wait_vmcnt<0>();   // stage s + 1 landed (and this wave's logits stores left)
+    __syncthreads();
+  }
+  if (!tail) return;
+  // the <= 16 tail columns Cm..: their whole W rows (16 x H, zero past C) in the ring, then per wave two
+  // frame rows x one 16-column fragment over all of K
+  {
+    const int kb = p.H / 8;   // 16-byte pieces per row
+    for (int i = tid; i < 16 * kb; i += 512) {
+      const int r = i / kb, q = i - r * kb;
+      *(uint4*)(Bs + r * p.H * 2 + q * 16) = *(const uint4*)(p.w + (long)(p.Cm + r) * p.ldw + q * 8);
+    }
+  }
+  __syncthreads();
+  f32x4 at[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+  for (int k0 = 0; k0 < p.H; k0 += 32) {
+    const int kk = k0 + 8 * kq;
+    const float4 g0 = *(const float4*)(Gs + ul * hs + kk), g1 = *(const float4*)(Gs + ul * hs + kk + 4);
+    const uint4 bt = *(const uint4*)(Bs + ul * p.H * 2 + kk * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) at[i] = mfma16_16x16x32(afrag(wave * 2 + i, kk, g0, g1), bt, at[i]);
+  }
+  if (ul < p.ntail) {
+    const int n = p.Cm + ul;
+    const float bn = p.bias[n];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = t0 + wave * 2 + i;
+      const long rowb = ((long)b * p.T + t) * p.U + u0 + 4 * kq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (t < p.T && u0 + 4 * kq + r < p.U) p.out[(rowb + r) * p.ldo + n] = at[i][r] + bn;
+    }
+  }
+}
+
+// the fused form applies: bf16, H a multiple of 64 up to 640, whole 256-column chunks + <= 16 tail columns
+bool joint_logits_fusable(int dt, int H, int C) {
+  const char* e = getenv("CFM_JOINT_FUSED");   // read per call: 0 = the hidden kernel + logits GEMM (A/B)
+  const bool on = !(e && !atoi(e));
+  return on && dt == DT_BF16 && H % jl::KS == 0 && H <= jl::HMAX && C >= jl::NC && C % jl::NC <= 16;
+}
+
+void joint_logits(const float* f, const float* g, int B, int T, int U, int H, int act, const bf16_t* w, long ldw,
+                  const float* bias, int C, float* out, Drop drop, hipStream_t st) {
+  JointLogits p;
+  p.f = f; p.g = g; p.w = w; p.bias = bias; p.out = out; p.ldw = ldw; p.ldo = C;
+  p.B = B; p.T = T; p.U = U; p.H = H; p.ntail = C % jl::NC; p.Cm = C - p.ntail; p.drop = drop;
+  const char* se = getenv("CFM_JOINT_SPLIT");
+  p.split = se ? atoi(se) : 1;
+  const char* pe = getenv("CFM_JOINT_PROBE");
+  p.probe = pe ? atoi(pe) : 0;
+  const long blocks = (long)B * ((T + jl::TT - 1) / jl::TT) * ((U + jl::UT - 1) / jl::UT);
+  if (blocks > 0x7fffffffL) fail(CFM_ERR_UNSUPPORTED, "joint: too many lattice tiles");
+  const dim3 grid((unsigned)blocks), block(512);
+  const bool d = drop.thr != 0;
+  if (p.probe && act == CFM_JOINT_RELU && !d)
+    cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, false, true>, grid, block, 0, st, p);
+  else if (act == CFM_JOINT_RELU)
+    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, true>, grid, block, 0, st, p)
+      : cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, false>, grid, block, 0, st, p);
+  else if (act == CFM_JOINT_SIGMOID)
+    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_SIGMOID, true>, grid, block, 0, st, p)
+      : cfm_launch(joint_logits_kernel<CFM_JOINT_SIGMOID, false>, grid, block, 0, st, p);
+  else
+    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_TANH, true>, grid, block, 0, st, p)
+      : cfm_launch(joint_logits_kernel<CFM_JOINT_TANH, false>, grid, block, 0, st, p);
+}
+
 // in-place log_softmax over rows of C fp32 values, one wave per row
 __global__ __launch_bounds__(256) void row_log_softmax_kernel(float* __restrict__ x, long rows, int C) {
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -263,7 +537,8 @@ JWs jws(const cfm_rnnt_joint* h, int B, int T, int U) {
   w.ag = take((long)B * U * h->kp(h->H2) * h->es);
   w.fp = take((long)B * T * h->H * 4);
   w.gp = take((long)B * U * h->H * 4);
-  w.hid = take((long)B * T * U * Hp * h->es);
+  // the hidden lattice exists only on the unfused path (the fused logits kernel forms it in registers)
+  w.hid = take(joint_logits_fusable(h->dtype, h->H, h->C) ? 0 : (long)B * T * U * Hp * h->es);
   w.total = round_up(off, 256);
   return w;
 }
@@ -508,7 +783,11 @@ void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu
     // each chunk's hidden is read back while it is still in the Infinity Cache (CFM_JOINT_CHUNK, 0 = whole)
     static const int chunk_env = [] { const char* e = getenv("CFM_JOINT_CHUNK"); return e ? atoi(e) : 0; }();
     const int chunk = (drop.thr == 0 && chunk_env > 0) ? std::min(chunk_env, B) : B;
-    for (int b0 = 0; b0 < B; b0 += chunk) {
+    const bool fused = joint_logits_fusable(dt, h->H, h->C);
+    if (fused)
+      joint_logits(fp, gp, B, T, U, h->H, h->act, (const bf16_t*)(h->wbuf + h->w_out), h->kp(h->H),
+                   (const float*)(h->wbuf + h->b_out), h->C, out, drop, st);
+    for (int b0 = 0; b0 < (fused ? 0 : B); b0 += chunk) {
       const int nb = std::min(chunk, B - b0);
       const long r0 = (long)b0 * T * U, nrows = (long)nb * T * U;
       const float* fpc = fp + (long)b0 * T * h->H;

@@ -87,3 +87,62 @@ def test_joint_tail_columns_match_torch():
     assert rel_l2(lo.cpu().numpy(), ref.cpu().numpy()) <= GATE["bf16"]
     assert rel_l2(lo[..., 1024:].cpu().numpy(), ref[..., 1024:].cpu().numpy()) <= GATE["bf16"]
     assert rel_l2(lo[..., 1000:1024].cpu().numpy(), ref[..., 1000:1024].cpu().numpy()) <= GATE["bf16"]
+
+
+def _native_pair(act, dims, seed):
+    from conformer_amd.joint import NativeJoint
+    H1, H2, H, C = dims
+    g = torch.Generator().manual_seed(seed)
+    w = [torch.randn(H, H1, generator=g) / H1 ** 0.5, torch.randn(H, generator=g) * 0.1,
+         torch.randn(H, H2, generator=g) / H2 ** 0.5, torch.randn(H, generator=g) * 0.1,
+         torch.randn(C, H, generator=g) / H ** 0.5, torch.randn(C, generator=g) * 0.1]
+    j = NativeJoint(H1, H2, H, C, activation=act, compute="bf16")
+    j.set_weights(*[t.cuda() for t in w])
+    return j
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "sigmoid"])
+@pytest.mark.parametrize("shape", [(2, 37, 13, 512, 640, 640, 1025), (1, 20, 101, 512, 640, 640, 1040),
+                                   (3, 9, 5, 64, 48, 128, 512), (2, 16, 16, 512, 640, 640, 300)],
+                         ids=["cfg4like", "u101_tail16", "small_no_tail", "unfused_c300"])
+def test_joint_fused_logits_match_hidden_gemm_path(act, shape, monkeypatch):
+    """The logits kernel that forms act(f' + g') in registers (csrc/joint.hip, joint_logits_kernel) against
+    the hidden kernel + logits GEMM (CFM_JOINT_FUSED=0) on the same weights: the same bf16 hidden values
+    and W, only the fp32 accumulation order differs (rel-L2 <= 1e-5), eval and with joint_net's dropout."""
+    B, T, U, H1, H2, H, C = shape
+    j = _native_pair(act, (H1, H2, H, C), 3)
+    torch.manual_seed(4)
+    enc = torch.randn(B, H1, T, device="cuda")
+    dec = torch.randn(B, H2, U, device="cuda")
+    outs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CFM_JOINT_FUSED", fused)
+        outs[fused] = (j.forward(enc, dec), j.forward(enc, dec, log_softmax=True),
+                       j.forward_train(enc, dec, 0.25, 1234))
+    torch.cuda.synchronize()
+    for a, b in zip(outs["1"], outs["0"]):
+        assert a.shape == (B, T, U, C) and torch.isfinite(a).all()
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= 1e-5
+    # dropout zeroed some hidden units: the training logits differ from the eval ones
+    assert not torch.equal(outs["1"][0], outs["1"][2])
+
+
+def test_joint_fused_logits_full_lattice():
+    """Config-4 lattice (T' = 400, U + 1 = 101, V + 1 = 1025, 4 utterances = 161600 rows x 1025): fused
+    against the hidden kernel + GEMM path, rel-L2 over the whole tensor and per utterance."""
+    j = _native_pair("relu", (512, 640, 640, 1025), 5)
+    torch.manual_seed(6)
+    enc = torch.randn(4, 512, 400, device="cuda")
+    dec = torch.randn(4, 640, 101, device="cuda")
+    os.environ["CFM_JOINT_FUSED"] = "1"
+    try:
+        a = j.forward(enc, dec).clone()
+        os.environ["CFM_JOINT_FUSED"] = "0"
+        b = j.forward(enc, dec)
+    finally:
+        os.environ.pop("CFM_JOINT_FUSED", None)
+    torch.cuda.synchronize()
+    for u in range(4):
+        d = (a[u].double() - b[u].double()).norm() / b[u].double().norm()
+        assert float(d) <= 1e-5
+    assert float((a[..., 1024] - b[..., 1024]).abs().max()) <= 1e-3
