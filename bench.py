@@ -626,7 +626,8 @@ def run_joint(args, world, rank, dev, dist, barrier):
         # the joint's bound: its GEMM FLOPs at the MFMA peak or its fp32 logits at the HBM peak
         t_mfma = f_joint / (PEAK[args.compute] * 1e12) * 1e3
         t_hbm = logit_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
-        roof = {"kernel": "joint (hidden + logits GEMM)", "bound": "hbm" if t_hbm >= t_mfma else "mfma",
+        fused = os.environ.get("CFM_JOINT_FUSED", "1") != "0" and args.compute == "bf16"
+        roof = {"kernel": "joint (logits kernel, hidden formed in registers)" if fused else "joint (hidden + logits GEMM)", "bound": "hbm" if t_hbm >= t_mfma else "mfma",
                 "floor_ms": round(max(t_mfma, t_hbm), 4), "achieved_ms": round(parts["joint"], 4),
                 "frac": round(max(t_mfma, t_hbm) / parts["joint"], 4),
                 "note": f"{f_joint / 1e9:.0f} GFLOP at {PEAK[args.compute]} TFLOP/s = {t_mfma:.3f} ms; "

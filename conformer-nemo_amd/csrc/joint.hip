@@ -4,9 +4,12 @@
 //   Hj[(b,t,u)] = act(f'[b,t] + g'[b,u])                   broadcast-add + activation, compute type
 //   out[(b,t,u)] = Hj . W_out^T + b_out                     the big GEMM (B*T*U x C x H), fp32 out
 //   optional log_softmax over C, one wave per row, in place
-// The hidden tensor is materialised in the compute type (HBM-bound pass, ~1/3 of the GEMM's own
-// output bytes) so the big contraction runs on the tuned LDS-DMA MFMA GEMM; its fp32 output rows
-// are C = V + 1 wide (odd), written with the epilogue's element stores.
+// bf16 (round 5, `joint_logits_kernel`): the hidden is never materialised - one kernel keeps a block's
+// f' / g' rows in LDS and forms act(f' + g') (x dropout) as MFMA A-fragments in registers, rounded as the
+// hidden kernel would store them; fp32 rows C = V + 1 wide (odd) go out from the accumulators.
+// Otherwise (fp32 compute, or shapes the fused kernel does not cover, or CFM_JOINT_FUSED=0) the hidden
+// tensor is materialised in the compute type and the contraction runs on the LDS-DMA MFMA GEMM, its
+// fp32 output rows written with the epilogue's element stores.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -241,16 +244,15 @@ void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, in
 // stores them, straight from those rows: a 16 x 32 fragment of v_mfma_f32_16x16x32 is one frame t and
 // the 16 labels, so a lane reads its label's 8 g' values and the frame's 8 f' values (a broadcast). The
 // hidden lattice never goes to memory. W_out streams from L2 through a two-stage LDS ring (64 K per
-// stage, 128-byte rows XOR-swizzled by row pair); the <= 16 tail columns past the last whole chunk
-// (V + 1 = 1025 -> 1024 + 1) ride along chunk 0 as one more 16-column fragment on the left waves.
+// stage, 128-byte rows XOR-swizzled by row pair), moved by waves 0-3 only; the <= 16 tail columns past
+// the last whole chunk (V + 1 = 1025 -> 1024 + 1) are one more pass over K after the last chunk.
 // Waves: 4 (frames: 4 each) x 2 (columns: 128 each); accumulators go straight from registers to the
 // fp32 rows (stride C, any alignment): per store, 16 consecutive columns of 4 label rows.
 namespace jl {
 constexpr int TT = 16, UT = 16, NC = 256, KS = 64, HMAX = 640;
-constexpr int BROWS = NC + 16;                          // + the tail columns (chunk 0)
-constexpr int STAGE = BROWS * KS * 2;                   // 34816 B
+constexpr int STAGE = NC * KS * 2;                      // 32 KB: 256 W rows x 128 B
 constexpr int FG_BYTES = 2 * 16 * (HMAX + 4) * 4;       // f' and g' rows, stride H + 4 floats
-constexpr int LDS = FG_BYTES + 2 * STAGE;               // 152064 B
+constexpr int LDS = FG_BYTES + 2 * STAGE;               // 147968 B
 }  // namespace jl
 
 struct JointLogits {
