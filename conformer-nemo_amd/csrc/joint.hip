@@ -5,8 +5,9 @@
 //   out[(b,t,u)] = Hj . W_out^T + b_out                     the big GEMM (B*T*U x C x H), fp32 out
 //   optional log_softmax over C, one wave per row, in place
 // bf16 (round 5, `joint_logits_kernel`): the hidden is never materialised - one kernel keeps a block's
-// f' / g' rows in LDS and forms act(f' + g') (x dropout) as MFMA A-fragments in registers, rounded as the
-// hidden kernel would store them; fp32 rows C = V + 1 wide (odd) go out from the accumulators.
+// f' / g' rows in LDS and forms act(f' + g') as MFMA A-fragments in registers, rounded as the
+// hidden kernel would store them; fp32 rows C = V + 1 wide (odd) go out from the accumulators (eval;
+// training keeps the path below, whose hidden kernel draws joint_net's dropout mask once per element).
 // Otherwise (fp32 compute, or shapes the fused kernel does not cover, or CFM_JOINT_FUSED=0) the hidden
 // tensor is materialised in the compute type and the contraction runs on the LDS-DMA MFMA GEMM, its
 // fp32 output rows written with the epilogue's element stores.
@@ -240,7 +241,7 @@ void joint_hidden(const float* f, const float* g, int B, int T, int U, int H, in
 // ---- the logits with the hidden formed in registers (bf16, round 5) ----------------------------------
 // One block = one utterance's 16 frames x 16 labels = 256 lattice rows, all Cm logit columns in chunks of
 // 256. The block's f' and g' rows (fp32) sit in LDS for its whole life; each wave builds the MFMA
-// A-fragments of act(f' + g') (x dropout), rounded to the compute type exactly as joint_hidden_kernel
+// A-fragments of act(f' + g'), rounded to the compute type exactly as joint_hidden_kernel
 // stores them, straight from those rows: a 16 x 32 fragment of v_mfma_f32_16x16x32 is one frame t and
 // the 16 labels, so a lane reads its label's 8 g' values and the frame's 8 f' values (a broadcast). The
 // hidden lattice never goes to memory. W_out streams from L2 through a two-stage LDS ring (64 K per
@@ -261,7 +262,6 @@ struct JointLogits {
   int B, T, U, H, Cm, ntail;
   int split;   // W loads by waves 0-3 only (CFM_JOINT_SPLIT, default 1)
   int probe;   // timing probes only (CFM_JOINT_PROBE): 1 no logits stores, 2 no MFMAs, 4 no hidden formation
-  Drop drop;
 };
 
 typedef float jf2 __attribute__((ext_vector_type(2)));
@@ -277,7 +277,7 @@ template <int ACT> CFM_DEV float joint_act(float x) {
   else return tanhf(x);
 }
 
-template <int ACT, bool DROP, bool PROBE = false>
+template <int ACT, bool PROBE = false>
 __global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
   __shared__ __attribute__((aligned(16))) char smem[jl::LDS];
   const int hs = p.H + 4;
@@ -334,12 +334,12 @@ __global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   const int ul = lane & 15, kq = lane >> 4;
-  // A-fragment of frame row tr (0..15) at K offset kk: act(f' + g') (x dropout) in the compute type
+  // A-fragment of frame row tr (0..15) at K offset kk: act(f' + g') in the compute type
   auto afrag = [&](int tr, int kk, const float4& g0, const float4& g1) {
     const float* fr = Fs + tr * hs + kk;
     const float4 f0 = *(const float4*)fr, f1 = *(const float4*)(fr + 4);
 #ifndef CFM_HALF_F16
-    if constexpr (ACT == CFM_JOINT_RELU && !DROP) {
+    if constexpr (ACT == CFM_JOINT_RELU) {
       // packed: 4 v_pk_add_f32, 4 v_cvt_pk_bf16_f32, then ReLU on the bf16 pairs as 16-bit integers
       // (v_pk_max_i16: a sign-magnitude value is negative iff its sign bit is set; rounding keeps signs)
       const jf2 s0 = jf2{f0.x, f0.y} + jf2{g0.x, g0.y}, s1 = jf2{f0.z, f0.w} + jf2{g0.z, g0.w};
@@ -351,11 +351,6 @@ __global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
     float v[8] = {f0.x + g0.x, f0.y + g0.y, f0.z + g0.z, f0.w + g0.w, f1.x + g1.x, f1.y + g1.y, f1.z + g1.z, f1.w + g1.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = joint_act<ACT>(v[e]);
-    if constexpr (DROP) {
-      const long row = ((long)b * p.T + t0 + tr) * p.U + u0 + ul;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= drop_mul(p.drop, (uint64_t)row * p.H + kk + e);
-    }
 #ifndef CFM_HALF_F16
     return make_uint4(jpk(jf2{v[0], v[1]}), jpk(jf2{v[2], v[3]}), jpk(jf2{v[4], v[5]}), jpk(jf2{v[6], v[7]}));
 #else
@@ -374,7 +369,7 @@ __global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
     }
   };
   __syncthreads();   // f', g' rows in LDS (compiler-visible loads: drained here)
-  constexpr bool PIPE = ACT == CFM_JOINT_RELU && !DROP;
+  constexpr bool PIPE = ACT == CFM_JOINT_RELU;
   uint4 af[4];
   if constexpr (PIPE) build4(8 * kq, af);
   issue(0);
@@ -388,7 +383,7 @@ __global__ __launch_bounds__(512) void joint_logits_kernel(JointLogits p) {
     for (int sub = 0; sub < 2; ++sub) {
       // the next K sub-step's fragments (K restarts with every column chunk) are formed while this
       // sub-step's MFMAs run: they depend on the resident f' / g' rows only, not on the W ring
-      // (ReLU without dropout: the cheap formation; the others keep it in place, for their registers)
+      // (ReLU: the cheap formation; the others keep it in place, for their registers)
       uint4 an[4];
       if constexpr (PIPE) {
         int kn = ks * 2 + sub + 1;
@@ -485,10 +480,10 @@ bool joint_logits_fusable(int dt, int H, int C) {
 }
 
 void joint_logits(const float* f, const float* g, int B, int T, int U, int H, int act, const bf16_t* w, long ldw,
-                  const float* bias, int C, float* out, Drop drop, hipStream_t st) {
+                  const float* bias, int C, float* out, hipStream_t st) {
   JointLogits p;
   p.f = f; p.g = g; p.w = w; p.bias = bias; p.out = out; p.ldw = ldw; p.ldo = C;
-  p.B = B; p.T = T; p.U = U; p.H = H; p.ntail = C % jl::NC; p.Cm = C - p.ntail; p.drop = drop;
+  p.B = B; p.T = T; p.U = U; p.H = H; p.ntail = C % jl::NC; p.Cm = C - p.ntail;
   const char* se = getenv("CFM_JOINT_SPLIT");
   p.split = se ? atoi(se) : 1;
   const char* pe = getenv("CFM_JOINT_PROBE");
@@ -496,18 +491,14 @@ void joint_logits(const float* f, const float* g, int B, int T, int U, int H, in
   const long blocks = (long)B * ((T + jl::TT - 1) / jl::TT) * ((U + jl::UT - 1) / jl::UT);
   if (blocks > 0x7fffffffL) fail(CFM_ERR_UNSUPPORTED, "joint: too many lattice tiles");
   const dim3 grid((unsigned)blocks), block(512);
-  const bool d = drop.thr != 0;
-  if (p.probe && act == CFM_JOINT_RELU && !d)
-    cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, false, true>, grid, block, 0, st, p);
+  if (p.probe && act == CFM_JOINT_RELU)
+    cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, true>, grid, block, 0, st, p);
   else if (act == CFM_JOINT_RELU)
-    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, true>, grid, block, 0, st, p)
-      : cfm_launch(joint_logits_kernel<CFM_JOINT_RELU, false>, grid, block, 0, st, p);
+    cfm_launch(joint_logits_kernel<CFM_JOINT_RELU>, grid, block, 0, st, p);
   else if (act == CFM_JOINT_SIGMOID)
-    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_SIGMOID, true>, grid, block, 0, st, p)
-      : cfm_launch(joint_logits_kernel<CFM_JOINT_SIGMOID, false>, grid, block, 0, st, p);
+    cfm_launch(joint_logits_kernel<CFM_JOINT_SIGMOID>, grid, block, 0, st, p);
   else
-    d ? cfm_launch(joint_logits_kernel<CFM_JOINT_TANH, true>, grid, block, 0, st, p)
-      : cfm_launch(joint_logits_kernel<CFM_JOINT_TANH, false>, grid, block, 0, st, p);
+    cfm_launch(joint_logits_kernel<CFM_JOINT_TANH>, grid, block, 0, st, p);
 }
 
 // in-place log_softmax over rows of C fp32 values, one wave per row
@@ -539,8 +530,8 @@ JWs jws(const cfm_rnnt_joint* h, int B, int T, int U) {
   w.ag = take((long)B * U * h->kp(h->H2) * h->es);
   w.fp = take((long)B * T * h->H * 4);
   w.gp = take((long)B * U * h->H * 4);
-  // the hidden lattice exists only on the unfused path (the fused logits kernel forms it in registers)
-  w.hid = take(joint_logits_fusable(h->dtype, h->H, h->C) ? 0 : (long)B * T * U * Hp * h->es);
+  // the hidden lattice (training, and the unfused path; the fused eval kernel forms it in registers)
+  w.hid = take((long)B * T * U * Hp * h->es);
   w.total = round_up(off, 256);
   return w;
 }
@@ -785,10 +776,13 @@ void joint_forward(cfm_rnnt_joint* h, const float* enc_bdt, const float* dec_bdu
     // each chunk's hidden is read back while it is still in the Infinity Cache (CFM_JOINT_CHUNK, 0 = whole)
     static const int chunk_env = [] { const char* e = getenv("CFM_JOINT_CHUNK"); return e ? atoi(e) : 0; }();
     const int chunk = (drop.thr == 0 && chunk_env > 0) ? std::min(chunk_env, B) : B;
-    const bool fused = joint_logits_fusable(dt, h->H, h->C);
+    // eval: the fused logits kernel. Training keeps the hidden kernel + GEMM: with joint_net's dropout
+    // the fused kernel would hash every hidden element once per 256-column chunk (RNN-T training step
+    // 43.8-44.2 -> 44.9-45.0 ms, profiles/r05jd_joint_fused_ab.txt)
+    const bool fused = drop.thr == 0 && joint_logits_fusable(dt, h->H, h->C);
     if (fused)
       joint_logits(fp, gp, B, T, U, h->H, h->act, (const bf16_t*)(h->wbuf + h->w_out), h->kp(h->H),
-                   (const float*)(h->wbuf + h->b_out), h->C, out, drop, st);
+                   (const float*)(h->wbuf + h->b_out), h->C, out, st);
     for (int b0 = 0; b0 < (fused ? 0 : B); b0 += chunk) {
       const int nb = std::min(chunk, B - b0);
       const long r0 = (long)b0 * T * U, nrows = (long)nb * T * U;

@@ -108,7 +108,8 @@ def _native_pair(act, dims, seed):
 def test_joint_fused_logits_match_hidden_gemm_path(act, shape, monkeypatch):
     """The logits kernel that forms act(f' + g') in registers (csrc/joint.hip, joint_logits_kernel) against
     the hidden kernel + logits GEMM (CFM_JOINT_FUSED=0) on the same weights: the same bf16 hidden values
-    and W, only the fp32 accumulation order differs (rel-L2 <= 1e-5), eval and with joint_net's dropout."""
+    and W, only the fp32 accumulation order differs (rel-L2 <= 1e-5). With joint_net's dropout (training)
+    both settings run the hidden kernel + GEMM; the check there is that the masks are reproducible."""
     B, T, U, H1, H2, H, C = shape
     j = _native_pair(act, (H1, H2, H, C), 3)
     torch.manual_seed(4)
