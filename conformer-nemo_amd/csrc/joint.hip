@@ -592,6 +592,54 @@ __global__ __launch_bounds__(256) void joint_act_bwd_u_kernel(const float* __res
   dp[bu * H + j] = s;
 }
 
+// Both reductions in one pass over dh (round 5): block (128 columns, 16 frames, b). Each dz is formed once
+// (one dropout hash); df over u in ascending order (the same sums as joint_act_bwd_t_kernel, bitwise), dp
+// as per-tile partials over the tile's frames (ascending) summed over the tiles by joint_act_bwd_dp_kernel.
+constexpr int kActTT = 16;
+__global__ __launch_bounds__(128) void joint_act_bwd_tu_kernel(const float* __restrict__ f, const float* __restrict__ g,
+                                                               const float* __restrict__ dh, int B, int T, int U, int H,
+                                                               int act, Drop drop, float* __restrict__ df,
+                                                               float* __restrict__ part) {
+  const int j = blockIdx.x * 128 + threadIdx.x;
+  const int tt = blockIdx.y, b = blockIdx.z;
+  const int ntt = gridDim.y;
+  if (j >= H) return;
+  const int t0 = tt * kActTT;
+  const int nt = min(kActTT, T - t0);
+  float fv[kActTT], dfa[kActTT];
+#pragma unroll
+  for (int i = 0; i < kActTT; ++i) {
+    fv[i] = f[((long)b * T + t0 + min(i, nt - 1)) * H + j];
+    dfa[i] = 0.0f;
+  }
+  for (int u = 0; u < U; ++u) {
+    const float gv = g[((long)b * U + u) * H + j];
+    float dpa = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kActTT; ++i) {
+      const long row = ((long)b * T + t0 + min(i, nt - 1)) * U + u;
+      const float dz = dh[row * H + j] * drop_mul(drop, (uint64_t)row * H + j) * act_grad(act, fv[i] + gv);
+      if (i < nt) { dfa[i] += dz; dpa += dz; }
+    }
+    part[(((long)b * ntt + tt) * U + u) * H + j] = dpa;
+  }
+#pragma unroll
+  for (int i = 0; i < kActTT; ++i)
+    if (i < nt) df[((long)b * T + t0 + i) * H + j] = dfa[i];
+}
+__global__ __launch_bounds__(256) void joint_act_bwd_dp_kernel(const float* __restrict__ part, int B, int ntt, int U,
+                                                               int H, float* __restrict__ dp) {
+  const long n = (long)B * U * H;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long bu = i / H;
+    const int j = (int)(i - bu * H);
+    const long b = bu / U, u = bu - b * U;
+    float a = 0.0f;
+    for (int q = 0; q < ntt; ++q) a += part[((b * ntt + q) * U + u) * H + j];
+    dp[i] = a;
+  }
+}
+
 // joint_net[-1] weight/bias gradient partials (bf16 path): [S][C][H + 4] -> dW (C, H) and db at column H
 __global__ __launch_bounds__(256) void joint_slab_kernel(const float* __restrict__ part, int S, int N, int K,
                                                          float* __restrict__ w, float* __restrict__ b) {
@@ -619,7 +667,7 @@ JFast joint_fast_splits(const cfm_rnnt_joint* h, long rows) {
   return JFast{(rows + chunk - 1) / chunk, chunk};
 }
 
-struct JBWs { long er, dr, fp, gp, hid, dh, df, dp, dx, lin, a1, wtp, part, total; };
+struct JBWs { long er, dr, fp, gp, hid, dh, df, dp, dx, lin, a1, wtp, part, actp, total; };
 JBWs jbws(const cfm_rnnt_joint* h, int B, int T, int U) {
   JBWs w;
   long off = 0;
@@ -640,6 +688,7 @@ JBWs jbws(const cfm_rnnt_joint* h, int B, int T, int U) {
   w.dh = take(std::max(rows * h->H * 4, (long)B * T * h->kp(h->H1) * h->es + (long)B * U * h->kp(h->H2) * h->es + 512));
   w.df = take((long)B * T * h->H * 4);
   w.dp = take((long)B * U * h->H * 4);
+  w.actp = take((long)B * ((T + kActTT - 1) / kActTT) * U * h->H * 4);   // dp partials per 16-frame tile
   w.dx = take((long)std::max(B * T * h->H1, B * U * h->H2) * 4);
   const size_t l1 = fast ? 0 : cfm_op_linear_backward_ws_size(mode, (int)rows, h->H, h->C);
   const size_t l2 = cfm_op_linear_backward_ws_size(mode, B * T, h->H1, h->H);
@@ -918,10 +967,20 @@ cfm_status cfm_rnnt_joint_backward(cfm_rnnt_joint* h, const float* enc_bdt, cons
       lin_bwd(hid, rows, H, w_out, C, dlogits, dh, dw_out, db_out);
     }
     // dz = dh * dropout mask * act'(z); df = sum over u, dp = sum over t
-    cfm_launch(joint_act_bwd_t_kernel, dim3((H + 255) / 256, B * T), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act, drop,
-               df);
-    cfm_launch(joint_act_bwd_u_kernel, dim3((H + 255) / 256, B * U), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act, drop,
-               dp);
+    const char* tu_env = getenv("CFM_JOINT_ACT_FUSED");   // read per call: 0 = the two-pass form (A/B)
+    if (!tu_env || atoi(tu_env) != 0) {
+      const int ntt = (T + kActTT - 1) / kActTT;
+      float* actp = (float*)(ws + w.actp);
+      cfm_launch(joint_act_bwd_tu_kernel, dim3((H + 127) / 128, ntt, B), dim3(128), 0, st, fp, gp, dh, B, T, U, H, h->act,
+                 drop, df, actp);
+      cfm_launch(joint_act_bwd_dp_kernel, dim3(ew_grid((long)B * U * H)), dim3(256), 0, st, (const float*)actp, B, ntt, U, H,
+                 dp);
+    } else {
+      cfm_launch(joint_act_bwd_t_kernel, dim3((H + 255) / 256, B * T), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act,
+                 drop, df);
+      cfm_launch(joint_act_bwd_u_kernel, dim3((H + 255) / 256, B * U), dim3(256), 0, st, fp, gp, dh, B, T, U, H, h->act,
+                 drop, dp);
+    }
     // enc / pred Linears
     lin_bwd(er, (long)B * T, H1, w_enc, H, df, d_enc_bdt ? dxr : nullptr, dw_enc, db_enc);
     if (d_enc_bdt) transpose_out(dxr, B, T, H1, d_enc_bdt, st);

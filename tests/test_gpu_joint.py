@@ -147,3 +147,32 @@ def test_joint_fused_logits_full_lattice():
         d = (a[u].double() - b[u].double()).norm() / b[u].double().norm()
         assert float(d) <= 1e-5
     assert float((a[..., 1024] - b[..., 1024]).abs().max()) <= 1e-3
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+@pytest.mark.parametrize("dims", [(2, 37, 13, 64, 48, 128, 300), (1, 40, 101, 512, 640, 640, 1025)],
+                         ids=["ragged_t", "cfg4_u101"])
+def test_joint_act_backward_one_pass_matches_two_pass(act, dims, monkeypatch):
+    """joint_act_bwd_tu_kernel (one pass over dh: df per frame, dp as 16-frame tile partials + an ordered tile
+    sum) against the two reduction kernels (CFM_JOINT_ACT_FUSED=0), same dropout masks: every gradient of
+    cfm_rnnt_joint_backward. df and everything derived from it (d_enc, dW_enc, db_enc) and the output layer's
+    gradients within rel-L2 1e-6; dp's fp32 sum over the frames runs in another order (tile partials), and with
+    random dlogits it cancels heavily, so d_dec, dW_pred, db_pred within 1e-4."""
+    B, T, U, H1, H2, H, C = dims
+    j = _native_pair(act, (H1, H2, H, C), 7)
+    g = torch.Generator().manual_seed(8)
+    w_enc, w_pred, w_out = (torch.randn(H, H1, generator=g).cuda() / H1 ** 0.5,
+                            torch.randn(H, H2, generator=g).cuda() / H2 ** 0.5, torch.randn(C, H, generator=g).cuda() / H ** 0.5)
+    j.set_weights(w_enc, None, w_pred, None, w_out, None)
+    torch.manual_seed(9)
+    enc = torch.randn(B, H1, T, device="cuda")
+    dec = torch.randn(B, H2, U, device="cuda")
+    dl = torch.randn(B, T, U, C, device="cuda") * 1e-3
+    res = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("CFM_JOINT_ACT_FUSED", v)
+        res[v] = j.backward(enc, dec, dl, 0.2, 4321, w_enc, w_pred, w_out, (True,) * 8)
+    torch.cuda.synchronize()
+    for k, (a, b) in enumerate(zip(res["1"], res["0"])):
+        assert torch.isfinite(a).all()
+        assert rel_l2(a.cpu().numpy(), b.cpu().numpy()) <= (1e-4 if k in (1, 4, 5) else 1e-6), k
