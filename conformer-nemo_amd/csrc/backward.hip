@@ -49,18 +49,32 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict_
                                                         T* __restrict__ dst, long dst_ld, int rows_pad, int cols_pad) {
   const int lane = threadIdx.x & 63;
   for (long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows_pad; r += (long)gridDim.x * 4) {
-    const float* sr = src + r * src_ld;
+    // loads from a clamped row / column, the value selected afterwards: a load under a per-lane condition
+    // is branched around and waited for one at a time (cdna_hip_programming.md §5)
+    const float* sr = src + std::min<long>(r, rows - 1) * src_ld;   // rows, cols >= 1 (pack_matrix)
     T* dr = dst + r * dst_ld;
     const bool rok = r < rows;
-#pragma unroll 4
-    for (int c = 2 * lane; c < cols_pad; c += 128) {
-      const float v0 = (rok && c < cols) ? sr[c] : 0.0f;
-      const float v1 = (rok && c + 1 < cols) ? sr[c + 1] : 0.0f;
-      if constexpr (sizeof(T) == 4) {
-        *(float2*)(dr + c) = make_float2(v0, v1);
-      } else {
-        const bf16_t b0 = f2bf(v0), b1 = f2bf(v1);
-        *(uint32_t*)(dr + c) = (uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+    for (int c0 = 0; c0 < cols_pad; c0 += 512) {   // 4 x 128 columns: all 8 loads before any store
+      float v[4][2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + 128 * k + 2 * lane;
+        v[k][0] = sr[min(c, cols - 1)];
+        v[k][1] = sr[min(c + 1, cols - 1)];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + 128 * k + 2 * lane;
+        const float v0 = (rok && c < cols) ? v[k][0] : 0.0f;
+        const float v1 = (rok && c + 1 < cols) ? v[k][1] : 0.0f;
+        if (c < cols_pad) {
+          if constexpr (sizeof(T) == 4) {
+            *(float2*)(dr + c) = make_float2(v0, v1);
+          } else {
+            const bf16_t b0 = f2bf(v0), b1 = f2bf(v1);
+            *(uint32_t*)(dr + c) = (uint32_t)__builtin_bit_cast(uint16_t, b0) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+          }
+        }
       }
     }
   }
@@ -329,7 +343,7 @@ void pack_matrix(int dtype, const float* src, long src_ld, int rows, int cols, b
                  int rows_pad, int cols_pad, hipStream_t st) {
   if (rows_pad <= 0 || cols_pad <= 0) return;
   static const int rows_path = [] { const char* e = getenv("CFM_PACK_ROWS"); return e ? atoi(e) : 1; }();
-  if (rows_path && !transpose && dst_ld % 2 == 0 && cols_pad % 2 == 0) {
+  if (rows_path && !transpose && dst_ld % 2 == 0 && cols_pad % 2 == 0 && rows > 0 && cols > 0) {
     const dim3 g((unsigned)std::min<long>(((long)rows_pad + 3) / 4, 32768)), b(256);
     if (dtype == DT_F32)
       cfm_launch(pack_rows_kernel<float>, g, b, 0, st, src, src_ld, rows, cols, (float*)dst, dst_ld, rows_pad, cols_pad);
