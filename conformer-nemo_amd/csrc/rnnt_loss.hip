@@ -59,6 +59,10 @@ __device__ __forceinline__ int label_at(const Dims& d, const int32_t* labels, in
 }
 
 constexpr int kDenomRegs = 32;   // V <= 2048: single read of the logits row
+// KR: registers per lane for the row (V <= 64 KR; 0 = two passes for V > 2048). The loads are unconditional
+// (clamped column, the value selected afterwards): a load under a per-lane condition is branched around and
+// waited for alone. Summing KR < 32 terms drops only trailing zero terms, so the values are unchanged.
+template <int KR>
 __global__ __launch_bounds__(256) void rnnt_denom_kernel(const float* __restrict__ acts, const int32_t* __restrict__ labels,
                                                          const int32_t* __restrict__ act_lens,
                                                          const int32_t* __restrict__ label_lens, Dims d,
@@ -75,18 +79,19 @@ __global__ __launch_bounds__(256) void rnnt_denom_kernel(const float* __restrict
   if (t >= Tb || u >= Ub) return;
   const float* a = acts + row * d.V;
   float m = kNegInf, s = 0.0f;
-  if (d.V <= 64 * kDenomRegs) {
+  if constexpr (KR > 0) {
     // one pass over HBM: the row's logits stay in registers for the max and the exp-sum
-    float r[kDenomRegs];
+    float r[KR];
 #pragma unroll
-    for (int k = 0; k < kDenomRegs; ++k) {
-      const int v = lane + 64 * k;
-      r[k] = v < d.V ? a[v] : kNegInf;
+    for (int k = 0; k < KR; ++k) r[k] = a[min(lane + 64 * k, d.V - 1)];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      r[k] = lane + 64 * k < d.V ? r[k] : kNegInf;
       m = fmaxf(m, r[k]);
     }
     m = wave_max(m);
 #pragma unroll
-    for (int k = 0; k < kDenomRegs; ++k) s += lane + 64 * k < d.V ? expf(r[k] - m) : 0.0f;
+    for (int k = 0; k < KR; ++k) s += lane + 64 * k < d.V ? expf(r[k] - m) : 0.0f;
   } else {
     for (int v = lane; v < d.V; v += 64) m = fmaxf(m, a[v]);
     m = wave_max(m);
@@ -420,8 +425,13 @@ void loss_impl(const float* acts, const int32_t* labels, int labels_ld, const in
   float *llf = w + 5 * n, *llb = llf + B;
   Dims d{B, T, U, V, blank, labels_ld};
   const unsigned rows_blocks = (unsigned)((n + 3) / 4);
-  hipLaunchKernelGGL(rnnt_denom_kernel, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d,
-                       denom, lpb, lpl);
+  {
+    auto kern = rnnt_denom_kernel<0>;
+    if (V <= 64 * 8) kern = rnnt_denom_kernel<8>;
+    else if (V <= 64 * 17) kern = rnnt_denom_kernel<17>;   // V + 1 = 1025
+    else if (V <= 64 * kDenomRegs) kern = rnnt_denom_kernel<kDenomRegs>;
+    hipLaunchKernelGGL(kern, dim3(rows_blocks), dim3(256), 0, st, acts, labels, act_lens, label_lens, d, denom, lpb, lpl);
+  }
   HIP_OK(hipGetLastError());
   const int threads = std::min(1024, (U + 63) / 64 * 64);
   const int per_thread = (U + threads - 1) / threads;
